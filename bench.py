@@ -1,0 +1,196 @@
+#!/usr/bin/env python3
+"""bench.py -- encoded symbols/s at vocab=32000, 4096 streams per GPU (BASELINE.json c3).
+
+One bench step = one whole compression job over inputs already resident in HBM:
+reset every stream, encode ``--tokens`` symbols per stream (integer pmf rows
+[tokens, streams, V] + symbols), flush and pack the bitstreams; with N > 1 ranks
+the job also gathers every rank's bitstreams over RCCL (the path's one exchange
+step).  Streams are sharded (each rank owns its own 4096), so scaling is weak.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+After the timed region (never inside it): per-stream status, a full GPU decode
+round trip, and bit-exact parity of the packed bytes against the CPU oracle
+(oracle/, the C restatement pinned to the reference); the oracle's own time on
+the same tables is the cpu_baseline.  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+METRIC = "encoded symbols/sec at vocab=32000, batch=4096 streams; bit-exact round-trip"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def read_traffic(cfg):
+    """HBM bytes per row_stats launch from the committed rocprofv3 PMC summary, if it matches."""
+    p = os.path.join(HERE, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    keys = ("vocab", "streams", "tokens", "pmf_bits")
+    if all(d.get(k) == cfg.get(k) for k in keys):
+        return d.get("row_stats_bytes_per_launch")
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--vocab", type=int, default=32000)
+    ap.add_argument("--streams", type=int, default=4096, help="streams per GPU")
+    ap.add_argument("--tokens", type=int, default=16, help="symbols per stream per job")
+    ap.add_argument("--prec", type=int, default=48)
+    ap.add_argument("--pmf-bits", type=int, default=32, choices=(32, 64))
+    ap.add_argument("--cpu-baseline", default="on", choices=("on", "off"))
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-streams", type=int, default=0, help="oracle sample streams (0 = all)")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from lac_amd import synth
+    from lac_amd.batch import BatchCoder
+    from lac_amd.dist import gather_bitstreams
+
+    V, B, T, P = args.vocab, args.streams, args.tokens, args.prec
+    ebytes = args.pmf_bits // 8
+    t_gen = time.time()
+    pmf, sym = synth.softmax_tables(T, B, V, seed=1234 + 7919 * rank, device=dev,
+                                    scale_bits=31 if args.pmf_bits == 32 else 60)
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] tables {tuple(pmf.shape)} {pmf.dtype} ({pmf.numel() * ebytes / 2**30:.2f} GiB) "
+        f"in {time.time() - t_gen:.1f}s")
+    coder = BatchCoder(V, B, prec=P, pmf_bits=args.pmf_bits, capacity_bits=T * (P + 2) + 256, device=dev)
+
+    def job():
+        coder.reset()
+        coder.encode(pmf, sym)
+        coder.finish()
+        if world > 1:
+            return gather_bitstreams(coder.bits_tensor(), coder.nbits_tensor())
+        return None
+
+    for _ in range(args.warmup):
+        job()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    coder.lib.lac_profile_read(coder.ctx, None, None, 1)
+    coder.lib.lac_profile_enable(coder.ctx, 1)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        job()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if dist:
+        dist.barrier()
+    coder.lib.lac_profile_enable(coder.ctx, 0)
+    dt = t1 - t0
+    if dist:
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    import ctypes as C
+    ms = (C.c_double * 4)()
+    cnt = (C.c_int64 * 4)()
+    coder.lib.lac_profile_read(coder.ctx, C.cast(ms, C.c_void_p), C.cast(cnt, C.c_void_p), 1)
+
+    # ---------------- checks, outside the timed region
+    rc, err, err_step = coder.status()
+    data, nbits = coder.to_bytes() if rc == 0 else ([], None)
+    coder.decode_open()
+    dec = coder.decode(pmf)
+    round_trip = bool(torch.equal(dec, sym)) and rc == 0
+    if dist:
+        ok = torch.tensor([1 if round_trip else 0], device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        round_trip = bool(ok.item())
+
+    cpu = None
+    parity = {"round_trip_all_streams": round_trip, "stream_status_ok": rc == 0}
+    if rank == 0:
+        from oracle import oracle as coracle
+        S = B if (args.cpu_streams <= 0 or args.cpu_streams > B) else args.cpu_streams
+        if world > 1:
+            S = min(S, 256)
+        host = pmf[:, :S, :].cpu().numpy()
+        host = host.view(np.uint32) if args.pmf_bits == 32 else host.view(np.uint64)
+        hsym = sym[:, :S].cpu().numpy()
+        nthreads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        c0 = time.perf_counter()
+        out, onb, ost, orc = coracle.encode_batch(host, hsym, P, nthreads=nthreads)
+        c1 = time.perf_counter()
+        exact = orc == 0 and rc == 0 and all(
+            int(onb[b]) == int(nbits[b]) and out[b, :(int(onb[b]) + 7) // 8].tobytes() == data[b] for b in range(S))
+        parity.update({"oracle_streams_checked": S, "bit_exact_vs_oracle": bool(exact)})
+        if world == 1 and args.cpu_baseline == "on":
+            cpu = {"value": S * T / (c1 - c0), "unit": "symbols/s", "cores": nthreads, "kind": "port",
+                   "sample": f"C oracle (oracle/lac_oracle.c) on {S} streams x {T} symbols of the same tables, "
+                             f"{nthreads} threads, {c1 - c0:.2f}s"}
+        avg_bits = float(np.mean(nbits.astype(np.float64))) / T if nbits is not None else None
+        parity["bits_per_symbol"] = avg_bits
+
+    if rank == 0:
+        units = T * B                                       # symbols per row_stats launch (T <= 64)
+        rs_launch_ms = ms[0] / max(cnt[0], 1)
+        alg_bytes = units * (V * ebytes + 4)
+        achieved = alg_bytes / (rs_launch_ms * 1e-3) / 1e9 if cnt[0] else None
+        cfg = {"workload": f"c3: vocab={V}, {B} streams/GPU, {T} symbols/stream per job, prec={P}, "
+                           f"uint{args.pmf_bits} pmf rows",
+               "vocab": V, "streams": B, "tokens": T, "prec": P, "pmf_bits": args.pmf_bits,
+               "parallelism": f"streams sharded over {world} GPU(s)" + (", RCCL bitstream all-gather" if world > 1 else "")}
+        value = world * B * T * args.steps / dt
+        line = {
+            "metric": METRIC, "value": value, "unit": "symbols/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": f"u{args.pmf_bits}",
+            "data": "synthetic: logits 3*N(0,1) per step (torch.Generator seeded 1234+t), "
+                    f"pmf=max(1,floor(softmax*2^{31 if args.pmf_bits == 32 else 60})), symbols by inverse CDF",
+            "config": cfg,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+                         "traffic": read_traffic(cfg), "kernel": "k_row_stats",
+                         "kernel_ms_per_launch": rs_launch_ms, "launches": int(cnt[0]),
+                         "bytes_per_launch": alg_bytes,
+                         "other_kernels_ms_per_step": {"encode": ms[1] / args.steps, "finish": ms[2] / args.steps}},
+            "cpu_baseline": cpu,
+            "parity": parity,
+        }
+        print(json.dumps(line), flush=True)
+    coder.close()
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,148 @@
+/*
+ * lac.h -- C-ABI of liblac.so, the MI355X (gfx950) arithmetic coder.
+ *
+ * Plain pointers and sizes only; HIP streams are passed as `void *`
+ * (a hipStream_t, NULL = the default stream).  Device pointers are
+ * caller-owned and borrowed for the duration of the call (decode: for the
+ * decode session).  One handle <-> one device; a handle is not thread-safe,
+ * independent handles are.
+ *
+ * Each entry point replaces a piece of the reference's predictor->coder call
+ * surface (/root/reference):
+ *
+ *   lac_open / lac_encode_reset   A_to_bin.__init__ state l=0, h=2^prec-1
+ *                                 (arith_code.py:157-164); AC(pred, prec) (:144-155)
+ *   lac_encode                    A_to_bin.step/run per symbol (:187-192, :207-211):
+ *                                 receive_symbol (:169-175) with
+ *                                 CDFPredictor.symbol_to_range/fudged_dist
+ *                                 (:83-110) + decide_bit/emit_bit (:176-186),
+ *                                 for B independent streams, T steps per call
+ *   lac_encode_finish             A_to_bin.flush (:193-202) + bits() carry
+ *                                 resolution (:227-246) + group_bits (:336-347)
+ *   lac_encoded_lengths /         bytes(group_bits(bits(...))) of measure_compress
+ *   lac_copy_bits                 (:401-420): L bits, MSB first, zero padded
+ *   lac_flush_digits              the raw digits flush() yields (:193-202)
+ *   lac_decode_open               A_from_bin.__init__ (:248-256) over a bitstream
+ *   lac_decode_step(s)            A_from_bin.step/run (:264-299, :322-326) with
+ *                                 CDFPredictor.val_to_symbol (:94-97); n symbols
+ *                                 out per stream (the reference stores no n)
+ *
+ * Status codes: 0 = OK, negative = error; lac_last_error() describes the last
+ * failure on the calling thread.  Per-stream coder errors are sticky and are
+ * reported by lac_stream_status (the reference raises AssertionError or hangs):
+ *   LAC_E_SYMBOL_RANGE  symbol not in [0, V)       arith_code.py:100-101
+ *   LAC_E_ZERO_WIDTH    zero-probability symbol on the unfudged path
+ *                       (the reference loops forever)
+ *   LAC_E_TABLE         all-zero row, or row total >= 2^64
+ *   LAC_E_DECODE_RANGE  decoded range misses the value  arith_code.py:277-278
+ *   LAC_E_CAPACITY      stream exceeded capacity_bits
+ *   LAC_E_PREC          prec outside [2, 61] or 2^(prec-1) < V
+ */
+#ifndef LAC_H
+#define LAC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct lac_ctx lac_ctx;
+
+enum {
+    LAC_OK = 0,
+    LAC_E_ARG = -1,
+    LAC_E_PREC = -2,
+    LAC_E_SYMBOL_RANGE = -3,
+    LAC_E_ZERO_WIDTH = -4,
+    LAC_E_TABLE = -5,
+    LAC_E_DECODE_RANGE = -6,
+    LAC_E_CAPACITY = -7,
+    LAC_E_HIP = -8,
+    LAC_E_STATE = -9
+};
+
+/* Library identification and the last error message of this thread. */
+const char *lac_version(void);
+const char *lac_last_error(void);
+
+/* Create a coder for `streams` independent streams over a `vocab`-symbol
+ * alphabet at `prec` bits (arith_code.py:157-162), tables of `pmf_bits` = 32
+ * (uint32) or 64 (uint64) entries, each stream holding up to
+ * `capacity_bits` output bits.  Allocates all device state on `device`. */
+int lac_open(int device, int prec, int64_t vocab, int64_t streams, int pmf_bits,
+             uint64_t capacity_bits, lac_ctx **out);
+int lac_close(lac_ctx *ctx);
+
+/* Reset every stream to l = 0, h = 2^prec - 1 with an empty output. */
+int lac_encode_reset(lac_ctx *ctx, void *stream);
+
+/* Encode `steps` symbols per stream.  Row (t, b) of the integer pmf starts at
+ * element t*step_stride + b*stream_stride of pmf_dev (a stride of 0 re-uses
+ * one row: a static model); sym_dev is int32 [steps][streams].  trace_dev,
+ * when not NULL, receives per (t, b) two uint64 {E, k}: the k >= 0 digits the
+ * symbol emitted, as the integer E = sum d_i 2^(k-1-i) (first digit 0..3,
+ * the rest 0/1).  Asynchronous on `stream`. */
+int lac_encode(lac_ctx *ctx, const void *pmf_dev, int64_t step_stride, int64_t stream_stride,
+               const int32_t *sym_dev, int64_t steps, uint64_t *trace_dev, void *stream);
+
+/* Flush every stream and resolve carries into packed bytes (asynchronous). */
+int lac_encode_finish(lac_ctx *ctx, void *stream);
+
+/* Synchronise `stream`; err_host[streams] / err_step_host[streams] (either may
+ * be NULL) receive each stream's sticky status and the step it failed at.
+ * Returns the first non-zero stream status, or LAC_OK. */
+int lac_stream_status(lac_ctx *ctx, int32_t *err_host, int64_t *err_step_host, void *stream);
+
+/* After lac_encode_finish: synchronise and copy the bit length of each stream. */
+int lac_encoded_lengths(lac_ctx *ctx, uint64_t *nbits_host, void *stream);
+
+/* Device view of the encoded streams: stream b's bytes start at
+ * bits_dev + b*stride_bytes, nbits_dev[b] bits, MSB first, zero padded. */
+int lac_encoded_device(lac_ctx *ctx, const uint8_t **bits_dev, uint64_t *stride_bytes,
+                       const uint64_t **nbits_dev);
+
+/* Synchronise and copy stream b's packed bytes to dst_host + b*dst_stride. */
+int lac_copy_bits(lac_ctx *ctx, uint8_t *dst_host, uint64_t dst_stride, void *stream);
+
+/* Same, device to device (asynchronous on `stream`). */
+int lac_copy_bits_dev(lac_ctx *ctx, uint8_t *dst_dev, uint64_t dst_stride, void *stream);
+
+/* Per-stream bit counts (uint64 [streams]) copied device to device (async). */
+int lac_copy_nbits_dev(lac_ctx *ctx, uint64_t *dst_dev, void *stream);
+
+/* Synchronise and copy each stream's coder registers l, h (A_to_bin.l/.h,
+ * arith_code.py:161-162); either pointer may be NULL. */
+int lac_encoder_registers(lac_ctx *ctx, int64_t *l_host, int64_t *h_host, void *stream);
+
+/* The digits flush() emitted per stream (at most 8): digits_host[streams][8],
+ * count_host[streams].  Synchronises. */
+int lac_flush_digits(lac_ctx *ctx, int8_t *digits_host, int32_t *count_host, void *stream);
+
+/* Start decoding: stream b reads nbits_dev[b] bits at bits_dev + b*stride_bytes
+ * (bits_dev == NULL: this context's own encoded streams).  The buffers are
+ * borrowed until the next lac_decode_open / lac_close.  stride_bytes must be a
+ * multiple of 8 and every stream's region readable up to it. */
+int lac_decode_open(lac_ctx *ctx, const uint8_t *bits_dev, uint64_t stride_bytes,
+                    const uint64_t *nbits_dev, void *stream);
+
+/* Decode one symbol per stream from row b at pmf_dev + b*stream_stride. */
+int lac_decode_step(lac_ctx *ctx, const void *pmf_dev, int64_t stream_stride,
+                    int32_t *sym_out_dev, void *stream);
+
+/* Decode `steps` symbols per stream (rows as in lac_encode); sym_out_dev is
+ * int32 [steps][streams]. */
+int lac_decode_steps(lac_ctx *ctx, const void *pmf_dev, int64_t step_stride, int64_t stream_stride,
+                     int64_t steps, int32_t *sym_out_dev, void *stream);
+
+/* Live kernel timing: with profiling on, every kernel launch is bracketed by
+ * hipEvents recorded on its own stream.  lac_profile_read synchronises and
+ * returns, per kernel id (0 row_stats, 1 encode, 2 finish, 3 decode_step),
+ * the summed device milliseconds and the launch count; reset != 0 clears. */
+int lac_profile_enable(lac_ctx *ctx, int on);
+int lac_profile_read(lac_ctx *ctx, double *ms_total /*[4]*/, int64_t *launches /*[4]*/, int reset);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LAC_H */

@@ -1,0 +1,98 @@
+"""ctypes binding of liblac.so (include/lac.h).
+
+The library is built in-tree (``python -m lac_amd.build`` or
+``__graft_entry__.build()``) and loaded from ``lac_amd/liblac.so``.  There is no
+fallback: if the library is missing or fails to load, every coder entry point
+raises :class:`LacLibraryError`.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liblac.so")
+
+LAC_OK = 0
+LAC_E_ARG = -1
+LAC_E_PREC = -2
+LAC_E_SYMBOL_RANGE = -3
+LAC_E_ZERO_WIDTH = -4
+LAC_E_TABLE = -5
+LAC_E_DECODE_RANGE = -6
+LAC_E_CAPACITY = -7
+LAC_E_HIP = -8
+LAC_E_STATE = -9
+
+STATUS_NAMES = {
+    LAC_OK: "LAC_OK", LAC_E_ARG: "LAC_E_ARG", LAC_E_PREC: "LAC_E_PREC",
+    LAC_E_SYMBOL_RANGE: "LAC_E_SYMBOL_RANGE", LAC_E_ZERO_WIDTH: "LAC_E_ZERO_WIDTH",
+    LAC_E_TABLE: "LAC_E_TABLE", LAC_E_DECODE_RANGE: "LAC_E_DECODE_RANGE",
+    LAC_E_CAPACITY: "LAC_E_CAPACITY", LAC_E_HIP: "LAC_E_HIP", LAC_E_STATE: "LAC_E_STATE",
+}
+
+# (name, restype, argtypes) for every symbol include/lac.h declares
+_vp, _i, _i64, _u64 = C.c_void_p, C.c_int, C.c_int64, C.c_uint64
+PROTOTYPES = [
+    ("lac_version", C.c_char_p, []),
+    ("lac_last_error", C.c_char_p, []),
+    ("lac_open", _i, [_i, _i, _i64, _i64, _i, _u64, C.POINTER(_vp)]),
+    ("lac_close", _i, [_vp]),
+    ("lac_encode_reset", _i, [_vp, _vp]),
+    ("lac_encode", _i, [_vp, _vp, _i64, _i64, _vp, _i64, _vp, _vp]),
+    ("lac_encode_finish", _i, [_vp, _vp]),
+    ("lac_stream_status", _i, [_vp, _vp, _vp, _vp]),
+    ("lac_encoded_lengths", _i, [_vp, _vp, _vp]),
+    ("lac_encoded_device", _i, [_vp, C.POINTER(_vp), C.POINTER(_u64), C.POINTER(_vp)]),
+    ("lac_copy_bits", _i, [_vp, _vp, _u64, _vp]),
+    ("lac_copy_bits_dev", _i, [_vp, _vp, _u64, _vp]),
+    ("lac_copy_nbits_dev", _i, [_vp, _vp, _vp]),
+    ("lac_flush_digits", _i, [_vp, _vp, _vp, _vp]),
+    ("lac_encoder_registers", _i, [_vp, _vp, _vp, _vp]),
+    ("lac_decode_open", _i, [_vp, _vp, _u64, _vp, _vp]),
+    ("lac_decode_step", _i, [_vp, _vp, _i64, _vp, _vp]),
+    ("lac_decode_steps", _i, [_vp, _vp, _i64, _i64, _i64, _vp, _vp]),
+    ("lac_profile_enable", _i, [_vp, _i]),
+    ("lac_profile_read", _i, [_vp, _vp, _vp, _i]),
+]
+
+KERNEL_IDS = {"row_stats": 0, "encode": 1, "finish": 2, "decode_step": 3}
+
+
+class LacLibraryError(RuntimeError):
+    pass
+
+
+class LacError(RuntimeError):
+    def __init__(self, code, msg=""):
+        super().__init__(f"{STATUS_NAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def load():
+    """Load liblac.so (once).  Raises LacLibraryError if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise LacLibraryError(f"{LIB_PATH} is missing: build it with `python -m lac_amd.build` "
+                              "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    try:
+        lib = C.CDLL(LIB_PATH)
+    except OSError as e:
+        raise LacLibraryError(f"cannot load {LIB_PATH}: {e}") from e
+    for name, res, args in PROTOTYPES:
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc):
+    if rc != LAC_OK:
+        raise LacError(rc, load().lac_last_error().decode(errors="replace"))
+    return rc

@@ -1,0 +1,248 @@
+"""Batched device API: B independent streams coded on one MI355X.
+
+This is the batched counterpart of the reference's single-stream coder
+(``A_to_bin`` / ``A_from_bin``, /root/reference/arith_code.py:156-334) and of
+``measure_compress`` (:401-420).  Tables stay in HBM as torch tensors; they
+cross into liblac.so as raw device pointers (see include/lac.h).
+
+    coder = BatchCoder(vocab=32000, streams=4096, prec=48)
+    coder.encode(pmf, sym)           # pmf [steps, streams, V] uint32 in int32 storage
+    coder.finish()
+    data = coder.to_bytes()          # list of per-stream bytes (group_bits format)
+
+    coder.decode_open()              # decode this coder's own output
+    out = coder.decode(pmf)          # [steps, streams] int32 symbols
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import LacError, check
+
+_ASSERT_CODES = (_lib.LAC_E_SYMBOL_RANGE, _lib.LAC_E_DECODE_RANGE)
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def _stream_handle(device):
+    torch = _torch()
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class StreamError(LacError):
+    """A coder error on one or more streams (sticky, reported per stream)."""
+
+    def __init__(self, code, err, err_step):
+        first = int(np.flatnonzero(err)[0]) if np.any(err) else -1
+        super().__init__(code, f"stream {first} failed at step {int(err_step[first]) if first >= 0 else -1}")
+        self.err = err
+        self.err_step = err_step
+        self.first_stream = first
+
+
+class BatchCoder:
+    """Encoder/decoder for ``streams`` independent streams (one liblac context)."""
+
+    def __init__(self, vocab: int, streams: int, prec: int = 48, pmf_bits: int = 32,
+                 capacity_bits: int | None = None, device=None):
+        torch = _torch()
+        self.lib = _lib.load()
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise ValueError("BatchCoder needs a HIP device (torch 'cuda' device on ROCm)")
+        self.vocab, self.streams, self.prec, self.pmf_bits = int(vocab), int(streams), int(prec), int(pmf_bits)
+        self.capacity_bits = int(capacity_bits or 1 << 16)
+        ctx = C.c_void_p()
+        check(self.lib.lac_open(self.device.index or 0, self.prec, self.vocab, self.streams, self.pmf_bits,
+                                self.capacity_bits, C.byref(ctx)))
+        self.ctx = ctx
+        self._finished = False
+
+    # ------------------------------------------------------------ lifetime
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.lib.lac_close(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def _stream(self):
+        return _stream_handle(self.device)
+
+    # ------------------------------------------------------------ checks
+    def _check_pmf(self, pmf):
+        torch = _torch()
+        want = (torch.int32, torch.uint32) if self.pmf_bits == 32 else (torch.int64, torch.uint64)
+        if pmf.dtype not in want:
+            raise TypeError(f"pmf must be {want[0]} (bit pattern of uint{self.pmf_bits}), got {pmf.dtype}")
+        if pmf.device != self.device:
+            raise ValueError(f"pmf is on {pmf.device}, coder on {self.device}")
+        if pmf.shape[-1] != self.vocab:
+            raise ValueError(f"pmf rows have {pmf.shape[-1]} entries, vocab is {self.vocab}")
+        if pmf.stride(-1) != 1:
+            raise ValueError("pmf rows must be contiguous")
+
+    # ------------------------------------------------------------ encode
+    def reset(self):
+        check(self.lib.lac_encode_reset(self.ctx, self._stream))
+        self._finished = False
+
+    def encode(self, pmf, sym, trace=None):
+        """Encode sym[t, b] with row pmf[t, b, :] (or pmf[b, :] / pmf[:] broadcast).
+
+        ``pmf`` [steps, streams, V], [streams, V] (steps == 1), [V] (a static
+        row for every step and stream) or [steps, 1, V] / [1, streams, V] with
+        stride-0 broadcasting via ``expand``.  ``sym`` int32 [steps, streams].
+        ``trace`` (optional int64 device tensor [steps, streams, 2]) receives
+        per symbol {E, k} -- its raw digits.
+        """
+        torch = _torch()
+        self._check_pmf(pmf)
+        if sym.dtype != torch.int32 or sym.device != self.device:
+            raise TypeError("sym must be an int32 tensor on the coder's device")
+        sym = sym.contiguous()
+        steps = sym.shape[0] if sym.dim() == 2 else 1
+        if sym.numel() != steps * self.streams:
+            raise ValueError(f"sym must be [steps, {self.streams}]")
+        if pmf.dim() == 1:
+            step_stride, stream_stride = 0, 0
+        elif pmf.dim() == 2:
+            if steps != 1 or pmf.shape[0] != self.streams:
+                raise ValueError("a 2-D pmf is [streams, V] for one step")
+            step_stride, stream_stride = 0, pmf.stride(0)
+        else:
+            if pmf.shape[0] not in (1, steps) or pmf.shape[1] not in (1, self.streams):
+                raise ValueError("pmf must be [steps, streams, V]")
+            step_stride = pmf.stride(0) if pmf.shape[0] > 1 else 0
+            stream_stride = pmf.stride(1) if pmf.shape[1] > 1 else 0
+        tp = None
+        if trace is not None:
+            if trace.dtype != torch.int64 or trace.numel() != steps * self.streams * 2 or not trace.is_contiguous():
+                raise ValueError("trace must be a contiguous int64 tensor [steps, streams, 2]")
+            tp = C.c_void_p(trace.data_ptr())
+        check(self.lib.lac_encode(self.ctx, C.c_void_p(pmf.data_ptr()), step_stride, stream_stride,
+                                  C.c_void_p(sym.data_ptr()), steps, tp, self._stream))
+
+    def finish(self):
+        check(self.lib.lac_encode_finish(self.ctx, self._stream))
+        self._finished = True
+
+    def status(self):
+        err = np.zeros(self.streams, dtype=np.int32)
+        step = np.zeros(self.streams, dtype=np.int64)
+        rc = self.lib.lac_stream_status(self.ctx, err.ctypes.data_as(C.c_void_p), step.ctypes.data_as(C.c_void_p),
+                                        self._stream)
+        return rc, err, step
+
+    def raise_on_error(self):
+        rc, err, step = self.status()
+        if rc:
+            raise StreamError(rc, err, step)
+
+    def registers(self):
+        l = np.zeros(self.streams, dtype=np.int64)
+        h = np.zeros(self.streams, dtype=np.int64)
+        check(self.lib.lac_encoder_registers(self.ctx, l.ctypes.data_as(C.c_void_p), h.ctypes.data_as(C.c_void_p),
+                                             self._stream))
+        return l, h
+
+    def lengths(self):
+        n = np.zeros(self.streams, dtype=np.uint64)
+        check(self.lib.lac_encoded_lengths(self.ctx, n.ctypes.data_as(C.c_void_p), self._stream))
+        return n
+
+    def device_bits(self):
+        """(int pointer, stride_bytes, nbits pointer) of the packed output in HBM."""
+        p, s, n = C.c_void_p(), C.c_uint64(), C.c_void_p()
+        check(self.lib.lac_encoded_device(self.ctx, C.byref(p), C.byref(s), C.byref(n)))
+        return p.value, s.value, n.value
+
+    def bits_tensor(self, stride=None):
+        """Packed output copied into a fresh uint8 device tensor [streams, stride]."""
+        torch = _torch()
+        _, s, _ = self.device_bits()
+        stride = int(stride or s)
+        out = torch.zeros((self.streams, stride), dtype=torch.uint8, device=self.device)
+        check(self.lib.lac_copy_bits_dev(self.ctx, C.c_void_p(out.data_ptr()), stride, self._stream))
+        return out
+
+    def nbits_tensor(self):
+        """Per-stream bit counts as a fresh int64 device tensor (asynchronous copy)."""
+        torch = _torch()
+        out = torch.empty((self.streams,), dtype=torch.int64, device=self.device)
+        check(self.lib.lac_copy_nbits_dev(self.ctx, C.c_void_p(out.data_ptr()), self._stream))
+        return out
+
+    def to_bytes(self):
+        """Per-stream bytes (MSB first, last byte zero padded: group_bits format)."""
+        self.raise_on_error()
+        n = self.lengths()
+        _, s, _ = self.device_bits()
+        host = np.zeros((self.streams, s), dtype=np.uint8)
+        check(self.lib.lac_copy_bits(self.ctx, host.ctypes.data_as(C.c_void_p), s, self._stream))
+        return [host[b, :(int(n[b]) + 7) // 8].tobytes() for b in range(self.streams)], n
+
+    def flush_digits(self):
+        d = np.zeros((self.streams, 8), dtype=np.int8)
+        c = np.zeros(self.streams, dtype=np.int32)
+        check(self.lib.lac_flush_digits(self.ctx, d.ctypes.data_as(C.c_void_p), c.ctypes.data_as(C.c_void_p),
+                                        self._stream))
+        return [d[b, :max(int(c[b]), 0)].tolist() for b in range(self.streams)]
+
+    # ------------------------------------------------------------ decode
+    def decode_open(self, bits=None, nbits=None):
+        """Decode this coder's own output (no args), or ``bits`` (uint8 device
+        tensor [streams, stride], stride % 8 == 0) with ``nbits`` (uint64/int64
+        device tensor [streams])."""
+        if bits is None:
+            check(self.lib.lac_decode_open(self.ctx, None, 0, None, self._stream))
+            self._dec_keep = None
+            return
+        if bits.dim() != 2 or bits.shape[0] != self.streams or bits.stride(1) != 1:
+            raise ValueError("bits must be [streams, stride] with contiguous rows")
+        self._dec_keep = (bits, nbits)                        # borrowed by the library
+        check(self.lib.lac_decode_open(self.ctx, C.c_void_p(bits.data_ptr()), bits.stride(0),
+                                       C.c_void_p(nbits.data_ptr()), self._stream))
+
+    def decode(self, pmf, out=None):
+        """Decode one symbol per stream per step; pmf as in :meth:`encode`."""
+        torch = _torch()
+        self._check_pmf(pmf)
+        if pmf.dim() == 2:
+            pmf = pmf.unsqueeze(0)
+        if pmf.dim() == 1:
+            raise ValueError("give decode a [steps, streams, V] (or expanded) table")
+        steps = pmf.shape[0]
+        step_stride = pmf.stride(0) if steps > 1 else 0
+        stream_stride = pmf.stride(1) if pmf.shape[1] > 1 else 0
+        if out is None:
+            out = torch.empty((steps, self.streams), dtype=torch.int32, device=self.device)
+        check(self.lib.lac_decode_steps(self.ctx, C.c_void_p(pmf.data_ptr()), step_stride, stream_stride, steps,
+                                        C.c_void_p(out.data_ptr()), self._stream))
+        return out
+
+
+def digits_of(E: int, k: int):
+    """Raw digits of one symbol from its trace entry (first digit 0..3)."""
+    if k <= 0:
+        return []
+    return [E >> (k - 1)] + [(E >> (k - 1 - i)) & 1 for i in range(1, k)]

@@ -1,0 +1,187 @@
+// lac_core.h -- per-stream coder arithmetic for gfx950 (host-callable for unit checks).
+//
+// Everything here is exact integer arithmetic restating /root/reference/arith_code.py:
+//
+//  * ceil mapping of CDFPredictor.symbol_to_range (:98-110):
+//        a = ceil(lo*w/T), b = ceil(hi*w/T)            -> unfudged_range()
+//  * the fudge branch of CDFPredictor.fudged_dist (:83-93) in closed form.  The
+//    loop p_i = max(p_{i-1}+1, min(w-(V-1-i), floor(c_i*w/T))) equals
+//        f_i = i + max(1, min(w-V+1, floor(Xmax_i / T))),
+//        Xmax_i = max_{j<=i} (c_j*w - j*T)
+//    so a = f_{s-1}, b = f_s need one prefix max and one division   -> fudge_f()
+//  * decide_bit/emit_bit (:176-186) collapsed: the loop runs
+//        k = max(0, prec - bitlen(h-l))
+//    times and emits digits whose value as one integer is E = l >> (prec-k);
+//    then l' = (l mod 2^(prec-k)) << k, h' = l' + ((h-l+1) << k) - 1  -> renorm()
+//  * flush (:193-202) literally, with region_overlap (:59-61)          -> flush_digits()
+//
+// The output integer R = sum_k d_k 2^(L-1-k) (A_to_bin.encode :212-219 == bits())
+// is accumulated as two bit planes: A (the low k bits of each E, appended) and C
+// (E's carry bit, which lands on the last bit already written).  R = A + C + flush,
+// resolved by one backward big-integer add in the finish kernel.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace lac {
+
+typedef unsigned __int128 u128;
+typedef __int128 i128;
+
+struct RowStats {          // per (step, stream) row, written by the row-stats kernel
+    uint64_t lo;           // c_{s-1} = sum_{i<s} pmf_i
+    uint64_t hi;           // c_s
+    uint64_t tot;          // T = c_{V-1}; 0 marks a bad row (minp: 0 empty, 1 overflow)
+    uint64_t minp;         // smallest positive pmf entry
+};
+
+struct EncState {          // per stream, persistent across lac_encode calls
+    int64_t l, h;          // coder registers, 0 <= l < 2^(prec+1), h < 3*2^prec
+    uint64_t L;            // bits written to the planes so far
+    uint64_t wa, wc;       // plane words holding bit L-1 (not yet stored)
+    int64_t nsym;          // symbols encoded
+    int32_t err;           // sticky status (LAC_E_*)
+    int32_t nflush;        // flush digits (finish)
+    int64_t err_step;      // nsym at the failing symbol
+    int8_t flush[8];       // flush digits
+};
+
+struct DecState {
+    int64_t l, h, x;       // registers and the prec-bit value window
+    uint64_t pos;          // next bit to read
+    int64_t nsym;
+    int32_t err;
+    int32_t pad;
+    int64_t err_step;
+};
+
+__host__ __device__ inline int bitlen64(uint64_t x) { return x ? 64 - __builtin_clzll(x) : 0; }
+
+// floor(N / d) for d > 0 when the quotient is known to be < 2^63.  Two rounds of
+// float64 quotient estimates plus an exact 128-bit remainder correction: no
+// shift-subtract loop (the generic __int128 division is ~5k cycles on gfx950).
+__host__ __device__ inline uint64_t div_floor(u128 N, uint64_t d) {
+    const double two64 = 18446744073709551616.0;
+    const double dd = (double)d;
+    const double dn = (double)(uint64_t)(N >> 64) * two64 + (double)(uint64_t)N;
+    double qd = dn / dd;
+    uint64_t q = qd >= 9.2e18 ? (uint64_t)9.2e18 : (uint64_t)qd;
+    i128 r = (i128)(N - (u128)q * d);
+    const double rd = (double)(int64_t)(r >> 64) * two64 + (double)(uint64_t)r;
+    const int64_t adj = (int64_t)(rd / dd);
+    q += (uint64_t)adj;
+    r -= (i128)adj * (i128)d;
+    while (r < 0) { q -= 1; r += d; }
+    while (r >= (i128)d) { q += 1; r -= d; }
+    return q;
+}
+
+__host__ __device__ inline uint64_t div_ceil(u128 N, uint64_t d) {
+    return div_floor(N + (d - 1), d);
+}
+
+// CDFPredictor.fudged_dist test (arith_code.py:84): fudged iff T > w*minp.
+__host__ __device__ inline bool is_fudged(uint64_t T, uint64_t w, uint64_t minp) {
+    return (u128)T > (u128)w * minp;
+}
+
+// Unfudged ceil mapping (arith_code.py:107-109).
+__host__ __device__ inline void unfudged_range(uint64_t lo, uint64_t hi, uint64_t T, uint64_t w,
+                                               uint64_t *a, uint64_t *b) {
+    *a = lo ? div_ceil((u128)lo * w, T) : 0;
+    *b = div_ceil((u128)hi * w, T);
+}
+
+// X_j = c_j*w - j*T (signed), the quantity whose prefix max drives the fudge.
+__host__ __device__ inline i128 fudge_x(uint64_t c, int64_t j, uint64_t w, uint64_t T) {
+    return (i128)((u128)c * w) - (i128)((u128)(uint64_t)j * T);
+}
+
+// f_i = i + max(1, min(w-V+1, floor(xmax/T)))   (fudged_dist, closed form)
+__host__ __device__ inline uint64_t fudge_f(int64_t i, i128 xmax, uint64_t T, uint64_t w, int64_t V) {
+    const uint64_t cap = w - (uint64_t)V + 1;             // >= 2 since w > 2^(prec-1) >= V
+    uint64_t g;
+    if (xmax < (i128)2 * (i128)T) {
+        g = 1;                                            // floor(xmax/T) <= 1
+    } else {
+        const uint64_t m = div_floor((u128)xmax, T);      // <= w
+        g = m < cap ? m : cap;
+    }
+    return (uint64_t)i + g;
+}
+
+// Encoder renormalisation (decide_bit/emit_bit, arith_code.py:176-186) in O(1).
+// On return *k digits were emitted with integer value *E (< 2^(k+1)).
+__host__ __device__ inline void renorm(int64_t &l, int64_t &h, int prec, int *k, uint64_t *E) {
+    const int kk = prec - bitlen64((uint64_t)(h - l));
+    if (kk <= 0) { *k = 0; *E = 0; return; }
+    const int sh = prec - kk;
+    const uint64_t e = (uint64_t)l >> sh;
+    const int64_t w = h - l + 1;
+    l = (int64_t)(((uint64_t)l - (e << sh)) << kk);
+    h = l + (w << kk) - 1;
+    *k = kk;
+    *E = e;
+}
+
+__host__ __device__ inline int64_t floordiv_pos(int64_t a, int64_t b) {   // Python //, b > 0
+    int64_t q = a / b;
+    if ((a % b) != 0 && a < 0) q -= 1;
+    return q;
+}
+
+__host__ __device__ inline int64_t overlap(int64_t a, int64_t b, int64_t c, int64_t d) {
+    const int64_t hi = d < b ? d : b, lo = a > c ? a : c;
+    const int64_t r = hi - lo + 1;
+    return r > 0 ? r : 0;
+}
+
+// A_to_bin.flush (arith_code.py:193-202), literal.  Returns the digit count (<= 8
+// in practice: <= 2 observed), digits may be -1..3.  Returns -1 on overrun.
+__host__ __device__ inline int flush_digits(int64_t l, int64_t h, int prec, int8_t *out) {
+    const int64_t D = (int64_t)1 << prec, Hd = (int64_t)1 << (prec - 1);
+    int n = 0;
+    while (l > 0 || h + 1 < D) {
+        int64_t d = floordiv_pos(l, Hd);
+        if (overlap(l, h, d * Hd, (d + 1) * Hd) < overlap(l, h, (d + 1) * Hd, (d + 2) * Hd)) d += 1;
+        l = l * 2 - d * D;
+        h = h * 2 + 1 - d * D;
+        if (n >= 8) return -1;
+        out[n++] = (int8_t)d;
+    }
+    return n;
+}
+
+// Append one renorm's output to the planes held in registers.  `store(idx, wa, wc)`
+// receives every completed word.  Returns false on capacity overflow.
+template <typename Store>
+__host__ __device__ inline bool plane_append(uint64_t &L, uint64_t &wa, uint64_t &wc, int k, uint64_t E,
+                                             uint64_t cap_words, Store store) {
+    if (k <= 0) return true;
+    const uint64_t ehi = E >> k;
+    uint64_t elo = E & ((k == 64) ? ~0ull : ((1ull << k) - 1));
+    if (ehi) wc |= 1ull << (63 - ((L - 1) & 63));         // carry onto bit L-1 (L >= 1 here)
+    int rem = k;
+    while (rem > 0) {
+        if (L > 0 && (L & 63) == 0) {                     // bit L starts a new word
+            const uint64_t idx = (L >> 6) - 1;
+            if (idx >= cap_words) return false;
+            store(idx, wa, wc);
+            wa = 0;
+            wc = 0;
+        }
+        const int off = (int)(L & 63);
+        const int take = rem < 64 - off ? rem : 64 - off;
+        const uint64_t chunk = (elo >> (rem - take)) & ((take == 64) ? ~0ull : ((1ull << take) - 1));
+        wa |= chunk << (64 - off - take);
+        L += (uint64_t)take;
+        rem -= take;
+    }
+    return ((L - 1) >> 6) < cap_words;
+}
+
+__host__ __device__ inline uint64_t bswap64(uint64_t x) {
+    return __builtin_bswap64(x);
+}
+
+}  // namespace lac

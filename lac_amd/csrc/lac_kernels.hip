@@ -1,0 +1,1007 @@
+// lac_kernels.hip -- gfx950 kernels and the C-ABI (include/lac.h) of liblac.so.
+//
+// Encode of one lac_encode call is two kernels per chunk of <= 64 steps:
+//
+//   k_row_stats   one wave per (step, stream) row.  HBM-bound scan of the integer
+//                 pmf row (16-B coalesced loads, 8 in flight per lane) producing the
+//                 four scalars the reference's symbol_to_range needs
+//                 (arith_code.py:79-110): lo = c_{s-1}, hi = c_s, T = c_{V-1}, minp.
+//   k_encode      one wave per stream, sequential over the chunk's steps: the
+//                 range narrowing + renormalisation of A_to_bin (:169-192).  Lane i
+//                 prefetches step i's stats; rows that hit fudged_dist (:83-93) are
+//                 re-scanned by the whole wave (prefix max of c_j*w - j*T).
+//
+// lac_encode_finish runs k_finish (flush :193-202, carry resolution of bits()
+// :227-246, MSB-first byte packing of group_bits :336-347), one lane per stream.
+//
+// Decode (A_from_bin, :248-334) is k_decode_step: one workgroup per stream and
+// step.  Pass 1 streams the row into per-chunk sums held in LDS; wave 0 scans the
+// chunk sums, finds the chunk holding floor((x-l)*T/w), re-reads only that chunk
+// (L2-hot) and scans it to the symbol (val_to_symbol's bisect_right, :94-97).
+#include <hip/hip_runtime.h>
+
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "lac.h"
+#include "lac_core.h"
+
+using namespace lac;
+
+#define LAC_VERSION "lac-mi355x 0.1 (gfx950)"
+
+namespace {
+
+constexpr int kChunkSteps = 64;       // steps per encode launch pair (= lanes of a wave)
+constexpr int kWavesPerBlock = 4;     // 256-thread workgroups
+
+// ------------------------------------------------------------------ wave helpers
+__device__ inline uint32_t lane_id() { return __lane_id(); }
+
+__device__ inline uint64_t shfl_u64(uint64_t v, int src) {
+    const uint32_t lo = __shfl((int)(uint32_t)v, src), hi = __shfl((int)(uint32_t)(v >> 32), src);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ inline uint64_t shfl_xor_u64(uint64_t v, int m) {
+    const uint32_t lo = __shfl_xor((int)(uint32_t)v, m), hi = __shfl_xor((int)(uint32_t)(v >> 32), m);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ inline uint64_t shfl_up_u64(uint64_t v, int d) {
+    const uint32_t lo = __shfl_up((int)(uint32_t)v, d), hi = __shfl_up((int)(uint32_t)(v >> 32), d);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ inline i128 shfl_i128(i128 v, int src) {
+    const u128 u = (u128)v;
+    return (i128)(((u128)shfl_u64((uint64_t)(u >> 64), src) << 64) | shfl_u64((uint64_t)u, src));
+}
+__device__ inline i128 shfl_up_i128(i128 v, int d) {
+    const u128 u = (u128)v;
+    return (i128)(((u128)shfl_up_u64((uint64_t)(u >> 64), d) << 64) | shfl_up_u64((uint64_t)u, d));
+}
+__device__ inline i128 shfl_xor_i128(i128 v, int m) {
+    const u128 u = (u128)v;
+    return (i128)(((u128)shfl_xor_u64((uint64_t)(u >> 64), m) << 64) | shfl_xor_u64((uint64_t)u, m));
+}
+__device__ inline uint64_t readlane_u64(uint64_t v, int l) {
+    const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ inline uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += shfl_xor_u64(v, m);
+    return v;
+}
+__device__ inline uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) { const uint64_t o = shfl_xor_u64(v, m); v = o < v ? o : v; }
+    return v;
+}
+__device__ inline uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) { const uint64_t o = shfl_xor_u64(v, m); v = o > v ? o : v; }
+    return v;
+}
+__device__ inline uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) { const uint32_t o = (uint32_t)__shfl_xor((int)v, m); v = o < v ? o : v; }
+    return v;
+}
+__device__ inline i128 wave_max_i128(i128 v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) { const i128 o = shfl_xor_i128(v, m); v = o > v ? o : v; }
+    return v;
+}
+__device__ inline uint64_t wave_incl_scan_u64(uint64_t v) {
+    const int lane = (int)lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) { const uint64_t t = shfl_up_u64(v, d); if (lane >= d) v += t; }
+    return v;
+}
+__device__ inline i128 wave_incl_maxscan_i128(i128 v) {
+    const int lane = (int)lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) { const i128 t = shfl_up_i128(v, d); if (lane >= d && t > v) v = t; }
+    return v;
+}
+
+constexpr i128 kI128Min = (i128)((u128)1 << 127);
+
+// ------------------------------------------------------------------ row loads
+template <typename E, int VEC> struct VecT;
+template <> struct VecT<uint32_t, 4> { typedef uint32_t type __attribute__((ext_vector_type(4))); };
+template <> struct VecT<uint64_t, 2> { typedef uint64_t type __attribute__((ext_vector_type(2))); };
+template <> struct VecT<uint32_t, 1> { typedef uint32_t type; };
+template <> struct VecT<uint64_t, 1> { typedef uint64_t type; };
+
+template <typename E, int VEC>
+__device__ inline typename VecT<E, VEC>::type load_vec(const E *row, int64_t vi) {
+    typedef typename VecT<E, VEC>::type V;
+    return __builtin_nontemporal_load(reinterpret_cast<const V *>(row) + vi);
+}
+template <typename E, int VEC>
+__device__ inline E vget(const typename VecT<E, VEC>::type &v, int j) {
+    if constexpr (VEC == 1) { (void)j; return v; } else { return v[j]; }
+}
+
+// ------------------------------------------------------------------ k_row_stats
+// Wave-per-row scan: T = sum pmf, lo = sum_{i<s} pmf, minp = min positive pmf.
+// u32 rows accumulate in u64 (V < 2^32 keeps it exact); u64 rows split each entry
+// into 32-bit halves so a total >= 2^64 is detected instead of wrapping.
+template <typename E, int VEC>
+__global__ __launch_bounds__(256) void k_row_stats(const E *__restrict__ pmf, int64_t step_stride,
+                                                   int64_t stream_stride, const int32_t *__restrict__ sym,
+                                                   int64_t B, int64_t rows, int64_t V, int64_t t0,
+                                                   RowStats *__restrict__ out) {
+    const int lane = (int)lane_id();
+    const int64_t r = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (r >= rows) return;
+    const int64_t t = t0 + r / B, b = r % B;
+    const E *row = pmf + t * step_stride + b * stream_stride;
+    const int64_t s = sym[t * B + b];
+    const int64_t sc = s < 0 ? 0 : (s > V ? V : s);
+    const int64_t nvec = V / VEC, sfull = sc / VEC;
+    constexpr bool W = sizeof(E) == 8;
+    uint64_t tot = 0, lo = 0, tot_h = 0, lo_h = 0;         // *_h: high halves (u64 rows)
+    E mn = (E)~(E)0;                                      // min over (x - 1): 0 wraps to max
+    constexpr int U = 8;
+    int64_t vi = lane;
+    auto take = [&](const typename VecT<E, VEC>::type &x, int64_t v) {
+        uint64_t sl = 0, sh = 0;
+#pragma unroll
+        for (int j = 0; j < VEC; j++) {
+            const E e = vget<E, VEC>(x, j);
+            if constexpr (W) { sl += (uint32_t)e; sh += (uint64_t)e >> 32; } else { sl += e; }
+            const E m1 = e - 1;
+            mn = m1 < mn ? m1 : mn;
+        }
+        tot += sl;
+        tot_h += sh;
+        if (v < sfull) { lo += sl; lo_h += sh; }
+    };
+    for (; vi + 64 * (U - 1) < nvec; vi += 64 * U) {
+        typename VecT<E, VEC>::type x[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) x[u] = load_vec<E, VEC>(row, vi + 64 * u);
+#pragma unroll
+        for (int u = 0; u < U; u++) take(x[u], vi + 64 * u);
+    }
+    for (; vi < nvec; vi += 64) take(load_vec<E, VEC>(row, vi), vi);
+    tot = wave_sum_u64(tot);
+    lo = wave_sum_u64(lo);
+    if constexpr (W) {
+        tot_h = wave_sum_u64(tot_h);
+        lo_h = wave_sum_u64(lo_h);
+    }
+    uint64_t m;
+    if constexpr (W) m = wave_min_u64(mn); else m = wave_min_u32(mn);
+    if (lane == 0) {
+        RowStats st;
+        u128 T = (u128)tot + ((u128)tot_h << 32), L = (u128)lo + ((u128)lo_h << 32);
+        for (int64_t i = sfull * VEC; i < sc; i++) L += (uint64_t)row[i];   // partial vector below s
+        const bool bad_s = s < 0 || s >= V;
+        const u128 Hh = L + (bad_s ? 0 : (uint64_t)row[s]);
+        if (T >> 64) {
+            st.lo = st.hi = st.tot = 0;
+            st.minp = 1;                                  // total >= 2^64
+        } else {
+            st.lo = (uint64_t)L;
+            st.hi = (uint64_t)Hh;
+            st.tot = (uint64_t)T;
+            st.minp = T ? m + 1 : 0;
+        }
+        out[r] = st;
+    }
+}
+
+// ------------------------------------------------------------------ fudge scan
+// max_{j<n} (c_j*w - j*T) over the first n entries of a row, by one wave.
+template <typename E>
+__device__ i128 wave_xmax_prefix(const E *row, int64_t n, uint64_t w, uint64_t T) {
+    const int lane = (int)lane_id();
+    constexpr int VEC = 4;
+    i128 best = kI128Min;
+    uint64_t base = 0;
+    E x[VEC];
+    auto ld = [&](int64_t r0) {
+#pragma unroll
+        for (int j = 0; j < VEC; j++) {
+            const int64_t e = r0 + lane * VEC + j;
+            x[j] = e < n ? row[e] : (E)0;
+        }
+    };
+    ld(0);
+    for (int64_t r0 = 0; r0 < n; r0 += 64 * VEC) {
+        E cur[VEC];
+#pragma unroll
+        for (int j = 0; j < VEC; j++) cur[j] = x[j];
+        if (r0 + 64 * VEC < n) ld(r0 + 64 * VEC);                 // prefetch the next round
+        uint64_t ls = 0;
+#pragma unroll
+        for (int j = 0; j < VEC; j++) ls += (uint64_t)cur[j];
+        const uint64_t incl = wave_incl_scan_u64(ls);
+        uint64_t c = base + incl - ls;
+#pragma unroll
+        for (int j = 0; j < VEC; j++) {
+            const int64_t e = r0 + lane * VEC + j;
+            c += (uint64_t)cur[j];
+            if (e < n) {
+                const i128 X = fudge_x(c, e, w, T);
+                best = X > best ? X : best;
+            }
+        }
+        base += readlane_u64(incl, 63);
+    }
+    return wave_max_i128(best);
+}
+
+// ------------------------------------------------------------------ k_encode
+template <typename E>
+__global__ __launch_bounds__(256) void k_encode(const RowStats *__restrict__ stats, const int32_t *__restrict__ sym,
+                                                int64_t B, int64_t t0, int nsteps, const E *pmf,
+                                                int64_t step_stride, int64_t stream_stride, int64_t V, int prec,
+                                                EncState *states, uint64_t *planeA, uint64_t *planeC,
+                                                uint64_t cap_words, uint64_t *trace) {
+    const int lane = (int)lane_id();
+    const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (b >= B) return;
+    EncState st = states[b];
+    if (st.err || st.nflush >= 0) {
+        if (lane == 0 && !st.err && st.nflush >= 0) { st.err = LAC_E_STATE; st.err_step = st.nsym; states[b] = st; }
+        return;
+    }
+    RowStats my = {0, 0, 0, 0};
+    int32_t mys = 0;
+    if (lane < nsteps) {
+        my = stats[(int64_t)lane * B + b];
+        mys = sym[(t0 + lane) * B + b];
+    }
+    uint64_t *pa = planeA + (uint64_t)b * cap_words, *pc = planeC + (uint64_t)b * cap_words;
+    auto store = [&](uint64_t idx, uint64_t wa, uint64_t wc) {
+        if (lane == 0) { pa[idx] = wa; pc[idx] = wc; }
+    };
+    int64_t l = st.l, h = st.h;
+    for (int i = 0; i < nsteps; i++) {
+        const uint64_t lo = readlane_u64(my.lo, i), hi = readlane_u64(my.hi, i);
+        const uint64_t T = readlane_u64(my.tot, i), minp = readlane_u64(my.minp, i);
+        const int64_t s = __builtin_amdgcn_readlane(mys, i);
+        if (s < 0 || s >= V) { st.err = LAC_E_SYMBOL_RANGE; break; }
+        if (T == 0) { st.err = LAC_E_TABLE; break; }
+        const uint64_t w = (uint64_t)(h - l + 1);
+        uint64_t a, bb;
+        if (!is_fudged(T, w, minp)) {
+            unfudged_range(lo, hi, T, w, &a, &bb);
+        } else {                                              // CDFPredictor.fudged_dist
+            const E *row = pmf + (t0 + i) * step_stride + b * stream_stride;
+            const i128 xprev = s > 0 ? wave_xmax_prefix<E>(row, s, w, T) : kI128Min;
+            const i128 xs = fudge_x(hi, s, w, T);
+            a = s > 0 ? fudge_f(s - 1, xprev, T, w, V) : 0;
+            bb = fudge_f(s, xs > xprev ? xs : xprev, T, w, V);
+        }
+        if (a >= bb) { st.err = LAC_E_ZERO_WIDTH; break; }
+        h = l + (int64_t)bb - 1;
+        l = l + (int64_t)a;
+        int k;
+        uint64_t Ev;
+        renorm(l, h, prec, &k, &Ev);
+        if (trace && lane == 0) {
+            trace[2 * ((t0 + i) * B + b)] = Ev;
+            trace[2 * ((t0 + i) * B + b) + 1] = (uint64_t)k;
+        }
+        if (!plane_append(st.L, st.wa, st.wc, k, Ev, cap_words, store)) { st.err = LAC_E_CAPACITY; break; }
+        st.nsym++;
+    }
+    if (lane == 0) {
+        if (st.err) st.err_step = st.nsym;
+        if (st.L > 0 && ((st.L - 1) >> 6) < cap_words) { pa[(st.L - 1) >> 6] = st.wa; pc[(st.L - 1) >> 6] = st.wc; }
+        st.l = l;
+        st.h = h;
+        states[b] = st;
+    }
+}
+
+// ------------------------------------------------------------------ k_finish
+// flush + R = A + C + F (backward big-integer add) + big-endian byte packing, in place.
+__global__ __launch_bounds__(256) void k_finish(EncState *states, uint64_t *planeA, const uint64_t *planeC,
+                                                uint64_t cap_words, int64_t B, int prec, uint64_t *nbits) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    EncState st = states[b];
+    if (st.err || st.nflush >= 0) {
+        if (!st.err) nbits[b] = st.L;
+        else nbits[b] = 0;
+        return;
+    }
+    int8_t fd[8];
+    const int m = flush_digits(st.l, st.h, prec, fd);
+    if (m < 0) { st.err = LAC_E_CAPACITY; st.err_step = st.nsym; states[b] = st; nbits[b] = 0; return; }
+    int64_t F = 0;
+    for (int i = 0; i < m; i++) F = F * 2 + fd[i];
+    const uint64_t L = st.L, Lf = L + (uint64_t)m;
+    const uint64_t nwords = (Lf + 63) >> 6;
+    if (nwords > cap_words) { st.err = LAC_E_CAPACITY; st.err_step = st.nsym; states[b] = st; nbits[b] = 0; return; }
+    const int pad = (int)(nwords * 64 - Lf);
+    i128 carry = (i128)F * ((i128)1 << pad);
+    const int64_t last = L ? (int64_t)((L - 1) >> 6) : -1;
+    uint64_t *pa = planeA + (uint64_t)b * cap_words;
+    const uint64_t *pc = planeC + (uint64_t)b * cap_words;
+    for (int64_t i = (int64_t)nwords - 1; i >= 0; i--) {
+        const uint64_t a = i <= last ? pa[i] : 0, c = i <= last ? pc[i] : 0;
+        const i128 sm = (i128)(u128)a + (i128)(u128)c + carry;
+        pa[i] = bswap64((uint64_t)sm);
+        carry = sm >> 64;
+    }
+    if (carry != 0) st.err = LAC_E_ARG;                   // R >= 2^L: impossible for the reference
+    st.nflush = m;
+    for (int i = 0; i < 8; i++) st.flush[i] = i < m ? fd[i] : 0;
+    st.L = Lf;
+    states[b] = st;
+    nbits[b] = st.err ? 0 : Lf;
+}
+
+__global__ void k_enc_reset(EncState *states, int64_t B, int prec) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    EncState st;
+    memset(&st, 0, sizeof(st));
+    st.l = 0;
+    st.h = ((int64_t)1 << prec) - 1;
+    st.nflush = -1;
+    st.err_step = -1;
+    states[b] = st;
+}
+
+// ------------------------------------------------------------------ decode
+// Bits [pos, pos+k) of a big-endian byte stream, zeros past nbits (k <= 63).
+__device__ inline uint64_t read_bits(const uint8_t *bits, uint64_t nbits, uint64_t pos, int k) {
+    if (k <= 0 || pos >= nbits) return 0;
+    const uint64_t *wp = reinterpret_cast<const uint64_t *>(bits);
+    const uint64_t wi = pos >> 6;
+    const int off = (int)(pos & 63);
+    uint64_t v = bswap64(wp[wi]) << off;
+    if (off && (wi + 1) * 64 < nbits) v |= bswap64(wp[wi + 1]) >> (64 - off);
+    v >>= (64 - k);
+    if (pos + (uint64_t)k > nbits) {
+        const int drop = (int)(pos + (uint64_t)k - nbits);
+        v = (v >> drop) << drop;
+    }
+    return v;
+}
+
+__global__ void k_dec_init(DecState *states, int64_t B, int prec, const uint8_t *bits, uint64_t stride,
+                           const uint64_t *nbits) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    DecState st;
+    memset(&st, 0, sizeof(st));
+    st.l = 0;
+    st.h = ((int64_t)1 << prec) - 1;
+    st.x = (int64_t)read_bits(bits + b * stride, nbits[b], 0, prec);
+    st.pos = (uint64_t)prec;
+    st.err_step = -1;
+    states[b] = st;
+}
+
+// One decode step for every stream: grid = B workgroups of 256 threads.
+template <typename E, int VEC, int G>
+__global__ __launch_bounds__(256) void k_decode_step(const E *__restrict__ pmf, int64_t step_off,
+                                                     int64_t stream_stride, int64_t V, int prec,
+                                                     DecState *states, const uint8_t *bits, uint64_t stride,
+                                                     const uint64_t *nbits, int32_t *sym_out, int64_t B) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+    __shared__ uint64_t wmin[kWavesPerBlock];
+    __shared__ uint32_t wovf[kWavesPerBlock];
+    const int lane = (int)lane_id(), wave = threadIdx.x >> 6;
+    const int64_t b = blockIdx.x;
+    DecState st = states[b];
+    if (st.err) {
+        if (threadIdx.x == 0) sym_out[b] = -1;
+        return;
+    }
+    const E *row = pmf + step_off + b * stream_stride;
+    constexpr int64_t CH = 64 * VEC * G;                 // elements per chunk
+    const int64_t nvec = V / VEC, nch = (V + CH - 1) / CH;
+    uint64_t *csum = smem;
+    // ---- pass 1: chunk sums, minp (all waves)
+    uint64_t mn = ~0ull;
+    uint32_t ovf = 0;
+    for (int64_t c = wave; c < nch; c += kWavesPerBlock) {
+        uint64_t ls = 0;
+        typename VecT<E, VEC>::type x[G];
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            const int64_t vi = c * 64 * G + g * 64 + lane;
+            if (vi < nvec) x[g] = load_vec<E, VEC>(row, vi);
+            else x[g] = (typename VecT<E, VEC>::type)0;
+        }
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+#pragma unroll
+            for (int j = 0; j < VEC; j++) {
+                const uint64_t e = (uint64_t)vget<E, VEC>(x[g], j);
+                const uint64_t n2 = ls + e;
+                ovf |= n2 < ls;
+                ls = n2;
+                const uint64_t m1 = e - 1;
+                mn = m1 < mn ? m1 : mn;
+            }
+        }
+        // chunk total with overflow detection (u64 rows only can overflow)
+        uint64_t tsum = ls;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) {
+            const uint64_t o = shfl_xor_u64(tsum, m);
+            const uint64_t n2 = tsum + o;
+            ovf |= n2 < tsum;
+            tsum = n2;
+        }
+        if (lane == 0) csum[c] = tsum;
+    }
+    mn = wave_min_u64(mn);
+    ovf = (uint32_t)__any(ovf);
+    if (lane == 0) { wmin[wave] = mn; wovf[wave] = ovf; }
+    __syncthreads();
+    if (wave != 0) return;
+    // ---- wave 0: T, minp, chunk prefix
+    uint64_t m0 = wmin[0];
+    uint32_t anyovf = wovf[0];
+    for (int i = 1; i < kWavesPerBlock; i++) { m0 = wmin[i] < m0 ? wmin[i] : m0; anyovf |= wovf[i]; }
+    const int64_t per = (nch + 63) / 64;
+    const int64_t c0 = lane * per, c1 = (c0 + per < nch) ? c0 + per : nch;
+    uint64_t local = 0;
+    for (int64_t c = c0; c < c1; c++) {
+        const uint64_t n2 = local + csum[c];
+        anyovf |= n2 < local;
+        local = n2;
+    }
+    const uint64_t incl = wave_incl_scan_u64(local);
+    const uint64_t T = readlane_u64(incl, 63);
+    // total overflow: sum of lane partials wrapped
+    const uint64_t chk = wave_sum_u64(local);
+    uint32_t tovf = (uint32_t)__any(anyovf);
+    {
+        // detect wrap of the cross-lane total: compare u128 sum
+        u128 acc = (u128)local;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) {
+            const u128 o = ((u128)shfl_xor_u64((uint64_t)(acc >> 64), m) << 64) | shfl_xor_u64((uint64_t)acc, m);
+            acc += o;
+        }
+        tovf |= (uint32_t)((acc >> 64) != 0);
+    }
+    (void)chk;
+    int err = 0;
+    if (tovf || T == 0) err = LAC_E_TABLE;
+    const uint64_t minp = m0 + 1;
+    const int64_t l = st.l, h = st.h, x = st.x;
+    const uint64_t w = (uint64_t)(h - l + 1), v = (uint64_t)(x - l);
+    int64_t s = -1;
+    uint64_t a = 0, bb = 0;
+    if (x < l || x > h) err = LAC_E_DECODE_RANGE;             // corrupted state / bits
+    if (!err && !is_fudged(T, w, minp)) {
+        const uint64_t tgt = div_floor((u128)v * T, w);          // < T
+        // the chunk whose cumulative range holds tgt
+        uint64_t run = incl - local;
+        int64_t fc = -1;
+        uint64_t fbase = 0;
+        for (int64_t c = c0; c < c1; c++) {
+            const uint64_t nx = run + csum[c];
+            if (fc < 0 && run <= tgt && tgt < nx) { fc = c; fbase = run; }
+            run = nx;
+        }
+        const uint64_t mask = __ballot(fc >= 0);
+        const int src = mask ? __ffsll((unsigned long long)mask) - 1 : 0;
+        if (!mask) err = LAC_E_DECODE_RANGE;
+        const int64_t cidx = mask ? (int64_t)readlane_u64((uint64_t)fc, src) : 0;
+        uint64_t cb = readlane_u64(fbase, src);
+        uint64_t lo_c = cb, hi_c = ~0ull;
+        uint64_t cnt = 0;
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            const int64_t vi = cidx * 64 * G + g * 64 + lane;
+            typename VecT<E, VEC>::type xv;
+            if (vi < nvec) xv = load_vec<E, VEC>(row, vi);
+            else xv = (typename VecT<E, VEC>::type)0;
+            uint64_t loc[VEC], ls = 0;
+#pragma unroll
+            for (int j = 0; j < VEC; j++) { ls += (uint64_t)vget<E, VEC>(xv, j); loc[j] = ls; }
+            const uint64_t in = wave_incl_scan_u64(ls);
+            const uint64_t ex = cb + in - ls;
+#pragma unroll
+            for (int j = 0; j < VEC; j++) {
+                const uint64_t ce = ex + loc[j];
+                const bool valid = vi < nvec;
+                if (valid && ce <= tgt) { cnt++; lo_c = ce > lo_c ? ce : lo_c; }
+                if (valid && ce > tgt) hi_c = ce < hi_c ? ce : hi_c;
+            }
+            cb += readlane_u64(in, 63);
+        }
+        cnt = wave_sum_u64(cnt);
+        lo_c = wave_max_u64(lo_c);
+        hi_c = wave_min_u64(hi_c);
+        s = cidx * CH + (int64_t)cnt;
+        if (!err) unfudged_range(lo_c, hi_c, T, w, &a, &bb);
+    } else if (!err) {
+        // fudged: first i with f_i > v, walking the row once (fudged_dist closed form)
+        const uint64_t C = w - (uint64_t)V + 1;
+        uint64_t base = 0;
+        i128 xrun = kI128Min;
+        constexpr int FV = 4;
+        for (int64_t r0 = 0; r0 < V && s < 0; r0 += 64 * FV) {
+            E xe[FV];
+            uint64_t ls = 0;
+#pragma unroll
+            for (int j = 0; j < FV; j++) {
+                const int64_t e = r0 + lane * FV + j;
+                xe[j] = e < V ? row[e] : (E)0;
+                ls += (uint64_t)xe[j];
+            }
+            const uint64_t in = wave_incl_scan_u64(ls);
+            uint64_t c = base + in - ls;
+            i128 X[FV];
+            i128 lm = kI128Min;
+#pragma unroll
+            for (int j = 0; j < FV; j++) {
+                const int64_t e = r0 + lane * FV + j;
+                c += (uint64_t)xe[j];
+                X[j] = e < V ? fudge_x(c, e, w, T) : kI128Min;
+                lm = X[j] > lm ? X[j] : lm;
+            }
+            const i128 inm = wave_incl_maxscan_i128(lm);
+            i128 exm = shfl_up_i128(inm, 1);
+            if (lane == 0) exm = kI128Min;
+            i128 runm = exm > xrun ? exm : xrun;
+            int64_t myfail = -1;
+            i128 before = kI128Min, after = kI128Min;
+#pragma unroll
+            for (int j = 0; j < FV; j++) {
+                const int64_t e = r0 + lane * FV + j;
+                const i128 prev = runm;
+                runm = X[j] > runm ? X[j] : runm;
+                if (e < V && myfail < 0) {
+                    const int64_t rr = (int64_t)v - e;
+                    const bool le = rr >= 1 && ((uint64_t)rr >= C || runm < (i128)(rr + 1) * (i128)T);
+                    if (!le) { myfail = e; before = prev; after = runm; }
+                }
+            }
+            const uint64_t mask = __ballot(myfail >= 0);
+            if (mask) {
+                const int src = __ffsll((unsigned long long)mask) - 1;
+                s = (int64_t)readlane_u64((uint64_t)myfail, src);
+                const i128 xb = shfl_i128(before, src), xa = shfl_i128(after, src);
+                a = s > 0 ? fudge_f(s - 1, xb, T, w, V) : 0;
+                bb = fudge_f(s, xa, T, w, V);
+            }
+            base += readlane_u64(in, 63);
+            const i128 tm = shfl_i128(inm, 63);
+            xrun = tm > xrun ? tm : xrun;
+        }
+        if (s < 0) err = LAC_E_DECODE_RANGE;
+    }
+    if (!err && !((int64_t)(l + (int64_t)a) <= x && x <= l + (int64_t)bb - 1)) err = LAC_E_DECODE_RANGE;
+    if (lane == 0) {
+        if (err) {
+            st.err = err;
+            st.err_step = st.nsym;
+            sym_out[b] = -1;
+        } else {
+            int64_t nl = l + (int64_t)a, nh = l + (int64_t)bb - 1;
+            int k;
+            uint64_t Ev;
+            renorm(nl, nh, prec, &k, &Ev);
+            int64_t nx = x;
+            if (k > 0) {
+                const int sh = prec - k;
+                nx = (int64_t)((((uint64_t)x - (Ev << sh)) << k) | read_bits(bits + b * stride, nbits[b], st.pos, k));
+                st.pos += (uint64_t)k;
+            }
+            st.l = nl;
+            st.h = nh;
+            st.x = nx;
+            st.nsym++;
+            sym_out[b] = (int32_t)s;
+        }
+        states[b] = st;
+    }
+}
+
+}  // namespace
+
+// ====================================================================== C-ABI
+struct lac_ctx {
+    int device = 0, prec = 0, pmf_bits = 32;
+    int64_t V = 0, B = 0;
+    uint64_t cap_bits = 0, cap_words = 0;
+    RowStats *stats = nullptr;
+    EncState *enc = nullptr;
+    DecState *dec = nullptr;
+    uint64_t *planeA = nullptr, *planeC = nullptr, *nbits = nullptr;
+    const uint8_t *dbits = nullptr;
+    uint64_t dstride = 0;
+    const uint64_t *dnbits = nullptr;
+    int mode = 0;                       // 0 encode, 1 decode
+    // live kernel timing (lac_profile_enable): hipEvent pairs around launches
+    bool prof = false;
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev_used;   // kernel id, (start, stop)
+    size_t ev_next = 0;
+};
+
+enum { KID_ROW_STATS = 0, KID_ENCODE = 1, KID_FINISH = 2, KID_DECODE = 3, KID_COUNT = 4 };
+
+static hipEvent_t ev_get(lac_ctx *c) {
+    if (c->ev_next == c->ev_pool.size()) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        c->ev_pool.push_back(e);
+    }
+    return c->ev_pool[c->ev_next++];
+}
+
+// Brackets one launch with events on its stream when profiling is on.
+struct ProfScope {
+    lac_ctx *c;
+    int kid;
+    hipStream_t st;
+    hipEvent_t a = nullptr, b = nullptr;
+    ProfScope(lac_ctx *c_, int kid_, hipStream_t st_) : c(c_), kid(kid_), st(st_) {
+        if (c->prof) {
+            a = ev_get(c);
+            b = ev_get(c);
+            if (a && b) (void)hipEventRecord(a, st);
+        }
+    }
+    ~ProfScope() {
+        if (c->prof && a && b) {
+            (void)hipEventRecord(b, st);
+            c->ev_used.push_back({kid, {a, b}});
+        }
+    }
+};
+
+static thread_local std::string g_err;
+
+static int fail(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+static int fail(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIPCHK(x)                                                                          \
+    do {                                                                                   \
+        hipError_t e_ = (x);                                                               \
+        if (e_ != hipSuccess) return fail(LAC_E_HIP, "%s: %s", #x, hipGetErrorString(e_)); \
+    } while (0)
+
+#define CHECK_LAUNCH() HIPCHK(hipGetLastError())
+
+static inline hipStream_t S(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+template <typename E, int VEC>
+static int encode_impl(lac_ctx *c, const E *pmf, int64_t step_stride, int64_t stream_stride, const int32_t *sym,
+                       int64_t steps, uint64_t *trace, hipStream_t st) {
+    for (int64_t t0 = 0; t0 < steps; t0 += kChunkSteps) {
+        const int n = (int)((steps - t0) < kChunkSteps ? (steps - t0) : kChunkSteps);
+        const int64_t rows = (int64_t)n * c->B;
+        {
+        ProfScope ps(c, KID_ROW_STATS, st);
+        k_row_stats<E, VEC><<<(unsigned)((rows + kWavesPerBlock - 1) / kWavesPerBlock), 64 * kWavesPerBlock, 0, st>>>(
+            pmf, step_stride, stream_stride, sym, c->B, rows, c->V, t0, c->stats);
+        }
+        CHECK_LAUNCH();
+        {
+        ProfScope ps(c, KID_ENCODE, st);
+        k_encode<E><<<(unsigned)((c->B + kWavesPerBlock - 1) / kWavesPerBlock), 64 * kWavesPerBlock, 0, st>>>(
+            c->stats, sym, c->B, t0, n, pmf, step_stride, stream_stride, c->V, c->prec, c->enc, c->planeA,
+            c->planeC, c->cap_words, trace);
+        }
+        CHECK_LAUNCH();
+    }
+    return LAC_OK;
+}
+
+template <typename E, int VEC, int G>
+static int decode_launch(lac_ctx *c, const E *pmf, int64_t step_off, int64_t stream_stride, int32_t *out,
+                         hipStream_t st) {
+    constexpr int64_t CH = 64 * VEC * G;
+    const int64_t nch = (c->V + CH - 1) / CH;
+    const size_t lds = sizeof(uint64_t) * (size_t)nch;
+    if (lds > 64 * 1024) return fail(LAC_E_ARG, "vocab too large for the decode chunk table");
+    ProfScope ps(c, KID_DECODE, st);
+    k_decode_step<E, VEC, G><<<(unsigned)c->B, 64 * kWavesPerBlock, lds, st>>>(
+        pmf, step_off, stream_stride, c->V, c->prec, c->dec, c->dbits, c->dstride, c->dnbits, out, c->B);
+    CHECK_LAUNCH();
+    return LAC_OK;
+}
+
+static int decode_one(lac_ctx *c, const void *pmf, int64_t step_off, int64_t step_stride, int64_t stream_stride,
+                      int32_t *out, hipStream_t st) {
+    const uintptr_t p = (uintptr_t)pmf;
+    if (c->pmf_bits == 32) {
+        const bool vec = (p % 16 == 0) && c->V % 4 == 0 && step_stride % 4 == 0 && stream_stride % 4 == 0;
+        if (vec) return decode_launch<uint32_t, 4, 2>(c, (const uint32_t *)pmf, step_off, stream_stride, out, st);
+        return decode_launch<uint32_t, 1, 8>(c, (const uint32_t *)pmf, step_off, stream_stride, out, st);
+    }
+    const bool vec = (p % 16 == 0) && c->V % 2 == 0 && step_stride % 2 == 0 && stream_stride % 2 == 0;
+    if (vec) return decode_launch<uint64_t, 2, 4>(c, (const uint64_t *)pmf, step_off, stream_stride, out, st);
+    return decode_launch<uint64_t, 1, 8>(c, (const uint64_t *)pmf, step_off, stream_stride, out, st);
+}
+
+extern "C" {
+
+const char *lac_version(void) { return LAC_VERSION; }
+const char *lac_last_error(void) { return g_err.c_str(); }
+
+int lac_open(int device, int prec, int64_t vocab, int64_t streams, int pmf_bits, uint64_t capacity_bits,
+             lac_ctx **out) {
+    if (!out) return fail(LAC_E_ARG, "out is NULL");
+    *out = nullptr;
+    if (prec < 2 || prec > 61) return fail(LAC_E_PREC, "prec %d outside [2, 61]", prec);
+    if (vocab < 1 || vocab > (int64_t)1 << 31) return fail(LAC_E_ARG, "vocab %lld outside [1, 2^31]", (long long)vocab);
+    if (((int64_t)1 << (prec - 1)) < vocab)
+        return fail(LAC_E_PREC, "2^(prec-1) = %lld < vocab %lld (the reference coder cannot progress)",
+                    (long long)1 << (prec - 1), (long long)vocab);
+    if (streams < 1) return fail(LAC_E_ARG, "streams must be >= 1");
+    if (pmf_bits != 32 && pmf_bits != 64) return fail(LAC_E_ARG, "pmf_bits must be 32 or 64");
+    if (capacity_bits < 64) capacity_bits = 64;
+    HIPCHK(hipSetDevice(device));
+    lac_ctx *c = new lac_ctx;
+    c->device = device;
+    c->prec = prec;
+    c->pmf_bits = pmf_bits;
+    c->V = vocab;
+    c->B = streams;
+    c->cap_bits = capacity_bits;
+    c->cap_words = (capacity_bits + 63) / 64 + 1;
+    hipError_t e = hipSuccess;
+    e = e ? e : hipMalloc(&c->stats, sizeof(RowStats) * kChunkSteps * streams);
+    e = e ? e : hipMalloc(&c->enc, sizeof(EncState) * streams);
+    e = e ? e : hipMalloc(&c->dec, sizeof(DecState) * streams);
+    e = e ? e : hipMalloc(&c->planeA, sizeof(uint64_t) * (c->cap_words * streams + 1));
+    e = e ? e : hipMalloc(&c->planeC, sizeof(uint64_t) * (c->cap_words * streams + 1));
+    e = e ? e : hipMalloc(&c->nbits, sizeof(uint64_t) * streams);
+    if (e != hipSuccess) {
+        lac_close(c);
+        return fail(LAC_E_HIP, "hipMalloc: %s", hipGetErrorString(e));
+    }
+    HIPCHK(hipMemset(c->nbits, 0, sizeof(uint64_t) * streams));
+    int rc = lac_encode_reset(c, nullptr);
+    if (rc) { lac_close(c); return rc; }
+    HIPCHK(hipDeviceSynchronize());
+    *out = c;
+    return LAC_OK;
+}
+
+int lac_close(lac_ctx *c) {
+    if (!c) return LAC_OK;
+    (void)hipSetDevice(c->device);
+    (void)hipDeviceSynchronize();
+    (void)hipFree(c->stats);
+    (void)hipFree(c->enc);
+    (void)hipFree(c->dec);
+    (void)hipFree(c->planeA);
+    (void)hipFree(c->planeC);
+    (void)hipFree(c->nbits);
+    for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
+    delete c;
+    return LAC_OK;
+}
+
+int lac_encode_reset(lac_ctx *c, void *stream) {
+    if (!c) return fail(LAC_E_ARG, "ctx is NULL");
+    HIPCHK(hipSetDevice(c->device));
+    c->mode = 0;
+    k_enc_reset<<<(unsigned)((c->B + 255) / 256), 256, 0, S(stream)>>>(c->enc, c->B, c->prec);
+    CHECK_LAUNCH();
+    return LAC_OK;
+}
+
+int lac_encode(lac_ctx *c, const void *pmf_dev, int64_t step_stride, int64_t stream_stride, const int32_t *sym_dev,
+               int64_t steps, uint64_t *trace_dev, void *stream) {
+    if (!c || !pmf_dev || !sym_dev) return fail(LAC_E_ARG, "NULL argument");
+    if (steps < 0 || step_stride < 0 || stream_stride < 0) return fail(LAC_E_ARG, "negative size/stride");
+    if (steps == 0) return LAC_OK;
+    if (c->mode != 0) return fail(LAC_E_STATE, "context is decoding; call lac_encode_reset first");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = S(stream);
+    const uintptr_t p = (uintptr_t)pmf_dev;
+    if (c->pmf_bits == 32) {
+        const bool vec = (p % 16 == 0) && c->V % 4 == 0 && step_stride % 4 == 0 && stream_stride % 4 == 0;
+        return vec ? encode_impl<uint32_t, 4>(c, (const uint32_t *)pmf_dev, step_stride, stream_stride, sym_dev, steps,
+                                              trace_dev, st)
+                   : encode_impl<uint32_t, 1>(c, (const uint32_t *)pmf_dev, step_stride, stream_stride, sym_dev, steps,
+                                              trace_dev, st);
+    }
+    const bool vec = (p % 16 == 0) && c->V % 2 == 0 && step_stride % 2 == 0 && stream_stride % 2 == 0;
+    return vec ? encode_impl<uint64_t, 2>(c, (const uint64_t *)pmf_dev, step_stride, stream_stride, sym_dev, steps,
+                                          trace_dev, st)
+               : encode_impl<uint64_t, 1>(c, (const uint64_t *)pmf_dev, step_stride, stream_stride, sym_dev, steps,
+                                          trace_dev, st);
+}
+
+int lac_encode_finish(lac_ctx *c, void *stream) {
+    if (!c) return fail(LAC_E_ARG, "ctx is NULL");
+    if (c->mode != 0) return fail(LAC_E_STATE, "context is decoding");
+    HIPCHK(hipSetDevice(c->device));
+    ProfScope ps(c, KID_FINISH, S(stream));
+    k_finish<<<(unsigned)((c->B + 255) / 256), 256, 0, S(stream)>>>(c->enc, c->planeA, c->planeC, c->cap_words, c->B,
+                                                                   c->prec, c->nbits);
+    CHECK_LAUNCH();
+    return LAC_OK;
+}
+
+int lac_stream_status(lac_ctx *c, int32_t *err_host, int64_t *err_step_host, void *stream) {
+    if (!c) return fail(LAC_E_ARG, "ctx is NULL");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(S(stream)));
+    int first = LAC_OK;
+    if (c->mode == 0) {
+        std::vector<EncState> v(c->B);
+        HIPCHK(hipMemcpy(v.data(), c->enc, sizeof(EncState) * c->B, hipMemcpyDeviceToHost));
+        for (int64_t b = 0; b < c->B; b++) {
+            if (err_host) err_host[b] = v[b].err;
+            if (err_step_host) err_step_host[b] = v[b].err ? v[b].err_step : -1;
+            if (!first && v[b].err) first = v[b].err;
+        }
+    } else {
+        std::vector<DecState> v(c->B);
+        HIPCHK(hipMemcpy(v.data(), c->dec, sizeof(DecState) * c->B, hipMemcpyDeviceToHost));
+        for (int64_t b = 0; b < c->B; b++) {
+            if (err_host) err_host[b] = v[b].err;
+            if (err_step_host) err_step_host[b] = v[b].err ? v[b].err_step : -1;
+            if (!first && v[b].err) first = v[b].err;
+        }
+    }
+    if (first) fail(first, "a stream reported status %d", first);
+    return first;
+}
+
+int lac_encoded_lengths(lac_ctx *c, uint64_t *nbits_host, void *stream) {
+    if (!c || !nbits_host) return fail(LAC_E_ARG, "NULL argument");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(S(stream)));
+    HIPCHK(hipMemcpy(nbits_host, c->nbits, sizeof(uint64_t) * c->B, hipMemcpyDeviceToHost));
+    return LAC_OK;
+}
+
+int lac_encoded_device(lac_ctx *c, const uint8_t **bits_dev, uint64_t *stride_bytes, const uint64_t **nbits_dev) {
+    if (!c) return fail(LAC_E_ARG, "ctx is NULL");
+    if (bits_dev) *bits_dev = reinterpret_cast<const uint8_t *>(c->planeA);
+    if (stride_bytes) *stride_bytes = c->cap_words * 8;
+    if (nbits_dev) *nbits_dev = c->nbits;
+    return LAC_OK;
+}
+
+int lac_copy_bits(lac_ctx *c, uint8_t *dst, uint64_t dst_stride, void *stream) {
+    if (!c || !dst || dst_stride == 0) return fail(LAC_E_ARG, "bad argument");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(S(stream)));
+    const uint64_t src_stride = c->cap_words * 8;
+    const uint64_t width = dst_stride < src_stride ? dst_stride : src_stride;
+    HIPCHK(hipMemcpy2D(dst, dst_stride, c->planeA, src_stride, width, (size_t)c->B, hipMemcpyDeviceToHost));
+    return LAC_OK;
+}
+
+int lac_copy_bits_dev(lac_ctx *c, uint8_t *dst, uint64_t dst_stride, void *stream) {
+    if (!c || !dst || dst_stride == 0) return fail(LAC_E_ARG, "bad argument");
+    HIPCHK(hipSetDevice(c->device));
+    const uint64_t src_stride = c->cap_words * 8;
+    const uint64_t width = dst_stride < src_stride ? dst_stride : src_stride;
+    HIPCHK(hipMemcpy2DAsync(dst, dst_stride, c->planeA, src_stride, width, (size_t)c->B, hipMemcpyDeviceToDevice,
+                            S(stream)));
+    return LAC_OK;
+}
+
+int lac_copy_nbits_dev(lac_ctx *c, uint64_t *dst, void *stream) {
+    if (!c || !dst) return fail(LAC_E_ARG, "bad argument");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemcpyAsync(dst, c->nbits, sizeof(uint64_t) * c->B, hipMemcpyDeviceToDevice, S(stream)));
+    return LAC_OK;
+}
+
+int lac_encoder_registers(lac_ctx *c, int64_t *l_host, int64_t *h_host, void *stream) {
+    if (!c) return fail(LAC_E_ARG, "ctx is NULL");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(S(stream)));
+    std::vector<EncState> v(c->B);
+    HIPCHK(hipMemcpy(v.data(), c->enc, sizeof(EncState) * c->B, hipMemcpyDeviceToHost));
+    for (int64_t b = 0; b < c->B; b++) {
+        if (l_host) l_host[b] = v[b].l;
+        if (h_host) h_host[b] = v[b].h;
+    }
+    return LAC_OK;
+}
+
+int lac_flush_digits(lac_ctx *c, int8_t *digits_host, int32_t *count_host, void *stream) {
+    if (!c) return fail(LAC_E_ARG, "ctx is NULL");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(S(stream)));
+    std::vector<EncState> v(c->B);
+    HIPCHK(hipMemcpy(v.data(), c->enc, sizeof(EncState) * c->B, hipMemcpyDeviceToHost));
+    for (int64_t b = 0; b < c->B; b++) {
+        if (count_host) count_host[b] = v[b].nflush;
+        if (digits_host) memcpy(digits_host + 8 * b, v[b].flush, 8);
+    }
+    return LAC_OK;
+}
+
+int lac_decode_open(lac_ctx *c, const uint8_t *bits_dev, uint64_t stride_bytes, const uint64_t *nbits_dev,
+                    void *stream) {
+    if (!c) return fail(LAC_E_ARG, "ctx is NULL");
+    HIPCHK(hipSetDevice(c->device));
+    if (!bits_dev) {
+        bits_dev = reinterpret_cast<const uint8_t *>(c->planeA);
+        stride_bytes = c->cap_words * 8;
+        nbits_dev = c->nbits;
+    } else {
+        if (!nbits_dev) return fail(LAC_E_ARG, "nbits_dev is NULL");
+        if (stride_bytes % 8 || (uintptr_t)bits_dev % 8) return fail(LAC_E_ARG, "bit buffers must be 8-byte aligned");
+    }
+    c->dbits = bits_dev;
+    c->dstride = stride_bytes;
+    c->dnbits = nbits_dev;
+    c->mode = 1;
+    k_dec_init<<<(unsigned)((c->B + 255) / 256), 256, 0, S(stream)>>>(c->dec, c->B, c->prec, bits_dev, stride_bytes,
+                                                                      nbits_dev);
+    CHECK_LAUNCH();
+    return LAC_OK;
+}
+
+int lac_decode_step(lac_ctx *c, const void *pmf_dev, int64_t stream_stride, int32_t *sym_out_dev, void *stream) {
+    return lac_decode_steps(c, pmf_dev, 0, stream_stride, 1, sym_out_dev, stream);
+}
+
+int lac_decode_steps(lac_ctx *c, const void *pmf_dev, int64_t step_stride, int64_t stream_stride, int64_t steps,
+                     int32_t *sym_out_dev, void *stream) {
+    if (!c || !pmf_dev || !sym_out_dev) return fail(LAC_E_ARG, "NULL argument");
+    if (c->mode != 1) return fail(LAC_E_STATE, "call lac_decode_open first");
+    if (steps < 0 || step_stride < 0 || stream_stride < 0) return fail(LAC_E_ARG, "negative size/stride");
+    HIPCHK(hipSetDevice(c->device));
+    for (int64_t t = 0; t < steps; t++) {
+        const int rc = decode_one(c, pmf_dev, t * step_stride, step_stride, stream_stride, sym_out_dev + t * c->B,
+                                  S(stream));
+        if (rc) return rc;
+    }
+    return LAC_OK;
+}
+
+int lac_profile_enable(lac_ctx *c, int on) {
+    if (!c) return fail(LAC_E_ARG, "ctx is NULL");
+    c->prof = on != 0;
+    return LAC_OK;
+}
+
+int lac_profile_read(lac_ctx *c, double *ms_total, int64_t *launches, int reset) {
+    if (!c) return fail(LAC_E_ARG, "ctx is NULL");
+    HIPCHK(hipSetDevice(c->device));
+    double tot[KID_COUNT] = {0, 0, 0, 0};
+    int64_t cnt[KID_COUNT] = {0, 0, 0, 0};
+    for (auto &u : c->ev_used) {
+        HIPCHK(hipEventSynchronize(u.second.second));
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, u.second.first, u.second.second));
+        tot[u.first] += ms;
+        cnt[u.first] += 1;
+    }
+    for (int k = 0; k < KID_COUNT; k++) {
+        if (ms_total) ms_total[k] = tot[k];
+        if (launches) launches[k] = cnt[k];
+    }
+    if (reset) {
+        c->ev_used.clear();
+        c->ev_next = 0;
+    }
+    return LAC_OK;
+}
+
+}  // extern "C"

@@ -112,3 +112,39 @@ def make_batch(seed: int, steps: int, streams: int, V: int, kind: str = "logunif
             else:
                 sym[t, b] = splitmix64_int(row_key(seed ^ 0xABC, t, b)) % V
     return pmf, sym
+
+
+# ----------------------------------------------------------- device tables
+def softmax_tables(steps: int, streams: int, V: int, seed: int = 1234, device="cuda",
+                   sigma: float = 3.0, scale_bits: int = 31, out=None):
+    """Random-logit tables on the GPU (the BASELINE.json workload).
+
+    Per step t: logits = sigma * N(0, 1) from ``torch.Generator(device)`` seeded
+    ``seed + t``; pmf = max(1, floor(softmax * 2^scale_bits)) (scale_bits <= 31 ->
+    uint32 bit patterns in int32 storage, else int64 for the 2^60 llama scale of
+    llama_compress.py:29 with floor 2); symbols by inverse CDF of a seeded uniform.
+    Returns (pmf [steps, streams, V], sym int32 [steps, streams]).
+    """
+    import torch
+    wide = scale_bits > 31
+    dt = torch.int64 if wide else torch.int32
+    if out is None:
+        out = torch.empty((steps, streams, V), dtype=dt, device=device)
+    sym = torch.empty((steps, streams), dtype=torch.int32, device=device)
+    floor_v = 2 if wide else 1
+    for t in range(steps):
+        g = torch.Generator(device=device)
+        g.manual_seed(seed + t)
+        logits = torch.randn((streams, V), generator=g, device=device, dtype=torch.float32) * sigma
+        p = torch.softmax(logits.double(), dim=-1)
+        del logits
+        q = torch.clamp(torch.floor(p * float(1 << scale_bits)), min=floor_v).to(torch.int64)
+        del p
+        cdf = torch.cumsum(q, dim=-1)
+        tot = cdf[:, -1]
+        u = torch.rand((streams,), generator=g, device=device, dtype=torch.float64)
+        target = torch.minimum((u * tot.double()).floor().long(), tot - 1)
+        sym[t] = torch.searchsorted(cdf, target.unsqueeze(1), right=True).squeeze(1).to(torch.int32)
+        out[t] = q.to(dt)
+        del q, cdf
+    return out, sym

@@ -1,0 +1,92 @@
+// Host-side unit check of lac_amd/csrc/lac_core.h -- test infrastructure.
+//
+// Drives the same per-stream arithmetic the gfx950 kernels use (closed-form fudge,
+// float64-assisted exact division, O(1) renorm, A/C bit planes, backward carry
+// resolution) sequentially on the CPU, so tests can compare it with the oracle
+// before any GPU is involved.  The wave-parallel parts (row scans, chunk search)
+// are exercised only by the GPU parity tests.
+#include <stdint.h>
+#include <string.h>
+
+#include <vector>
+
+#include "lac_core.h"
+
+using namespace lac;
+
+extern "C" {
+
+uint64_t cc_div_floor(uint64_t nh, uint64_t nl, uint64_t d) { return div_floor(((u128)nh << 64) | nl, d); }
+
+// pmf rows [steps][V] (eb = 4 or 8 bytes), one stream.  Returns status, writes
+// MSB-first bytes and the bit count.
+int cc_encode(const void *pmf, int eb, int64_t V, int64_t steps, int64_t step_stride, const int32_t *syms, int prec,
+              uint8_t *out, uint64_t cap_bytes, uint64_t *nbits) {
+    const uint64_t cap_words = cap_bytes / 8;
+    std::vector<uint64_t> A(cap_words + 1, 0), Cc(cap_words + 1, 0);
+    int64_t l = 0, h = ((int64_t)1 << prec) - 1;
+    uint64_t L = 0, wa = 0, wc = 0;
+    auto store = [&](uint64_t idx, uint64_t a, uint64_t c) { A[idx] = a; Cc[idx] = c; };
+    for (int64_t t = 0; t < steps; t++) {
+        const char *row = (const char *)pmf + (size_t)(t * step_stride) * eb;
+        auto at = [&](int64_t i) -> uint64_t { return eb == 4 ? ((const uint32_t *)row)[i] : ((const uint64_t *)row)[i]; };
+        const int64_t s = syms[t];
+        if (s < 0 || s >= V) return -3;
+        u128 T = 0, lo = 0;
+        uint64_t minp = 0;
+        for (int64_t i = 0; i < V; i++) {
+            const uint64_t p = at(i);
+            if (i < s) lo += p;
+            T += p;
+            if (p && (!minp || p < minp)) minp = p;
+        }
+        if (T == 0 || (T >> 64)) return -5;
+        const uint64_t hi = (uint64_t)lo + at(s);
+        const uint64_t w = (uint64_t)(h - l + 1);
+        uint64_t a, b;
+        if (!is_fudged((uint64_t)T, w, minp)) {
+            unfudged_range((uint64_t)lo, hi, (uint64_t)T, w, &a, &b);
+        } else {
+            i128 xprev = (i128)((u128)1 << 127);
+            uint64_t c = 0;
+            for (int64_t j = 0; j < s; j++) {
+                c += at(j);
+                const i128 X = fudge_x(c, j, w, (uint64_t)T);
+                if (X > xprev) xprev = X;
+            }
+            const i128 xs = fudge_x(hi, s, w, (uint64_t)T);
+            a = s > 0 ? fudge_f(s - 1, xprev, (uint64_t)T, w, V) : 0;
+            b = fudge_f(s, xs > xprev ? xs : xprev, (uint64_t)T, w, V);
+        }
+        if (a >= b) return -4;
+        h = l + (int64_t)b - 1;
+        l = l + (int64_t)a;
+        int k;
+        uint64_t E;
+        renorm(l, h, prec, &k, &E);
+        if (!plane_append(L, wa, wc, k, E, cap_words, store)) return -7;
+    }
+    if (L > 0) { A[(L - 1) >> 6] = wa; Cc[(L - 1) >> 6] = wc; }
+    int8_t fd[8];
+    const int m = flush_digits(l, h, prec, fd);
+    if (m < 0) return -7;
+    int64_t F = 0;
+    for (int i = 0; i < m; i++) F = F * 2 + fd[i];
+    const uint64_t Lf = L + (uint64_t)m, nwords = (Lf + 63) >> 6;
+    if (nwords > cap_words) return -7;
+    const int pad = (int)(nwords * 64 - Lf);
+    i128 carry = (i128)F * ((i128)1 << pad);
+    const int64_t last = L ? (int64_t)((L - 1) >> 6) : -1;
+    for (int64_t i = (int64_t)nwords - 1; i >= 0; i--) {
+        const uint64_t av = i <= last ? A[i] : 0, cv = i <= last ? Cc[i] : 0;
+        const i128 sm = (i128)(u128)av + (i128)(u128)cv + carry;
+        const uint64_t o = bswap64((uint64_t)sm);
+        memcpy(out + 8 * i, &o, 8);
+        carry = sm >> 64;
+    }
+    if (carry != 0) return -1;
+    *nbits = Lf;
+    return 0;
+}
+
+}  // extern "C"

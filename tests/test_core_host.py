@@ -1,0 +1,87 @@
+"""Host check of the kernels' per-stream arithmetic (lac_core.h) against the oracle.
+
+Compiles tests/native/core_check.cpp (host code only) with hipcc; no GPU needed.
+"""
+import ctypes as C
+import os
+import random
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import REPO, load_golden
+from lac_amd import synth
+from oracle import oracle as coracle
+
+SO = os.path.join(REPO, "tests", "native", "libcorecheck.so")
+SRC = os.path.join(REPO, "tests", "native", "core_check.cpp")
+
+
+@pytest.fixture(scope="module")
+def core():
+    if not os.path.exists(SO) or os.path.getmtime(SO) < max(os.path.getmtime(SRC), os.path.getmtime(
+            os.path.join(REPO, "lac_amd", "csrc", "lac_core.h"))):
+        subprocess.run(["hipcc", "-O2", "-std=c++17", "-fPIC", "-shared", "-I", os.path.join(REPO, "lac_amd", "csrc"),
+                        SRC, "-o", SO], check=True)
+    lib = C.CDLL(SO)
+    lib.cc_div_floor.restype = C.c_uint64
+    lib.cc_div_floor.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64]
+    lib.cc_encode.restype = C.c_int
+    lib.cc_encode.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.c_int64, C.c_int64, C.c_void_p, C.c_int,
+                              C.c_void_p, C.c_uint64, C.c_void_p]
+    return lib
+
+
+def _enc(core, rows, syms, prec):
+    a = np.ascontiguousarray(rows)
+    s = np.ascontiguousarray(np.asarray(syms, dtype=np.int32))
+    cap = (len(s) * (prec + 2) + 256) // 8 * 8
+    out = np.zeros(cap, dtype=np.uint8)
+    nb = np.zeros(1, dtype=np.uint64)
+    stride = 0 if a.shape[0] == 1 else a.shape[1]
+    rc = core.cc_encode(a.ctypes.data, a.itemsize, a.shape[1], len(s), stride, s.ctypes.data, prec,
+                        out.ctypes.data, cap, nb.ctypes.data)
+    L = int(nb[0])
+    return rc, out[:(L + 7) // 8].tobytes(), L
+
+
+def test_div_floor_exact(core):
+    rng = random.Random(5)
+    for _ in range(20000):
+        d = rng.choice([1, 2, 3, rng.randrange(1, 1 << 20), rng.randrange(1, 1 << 47), rng.randrange(1, 1 << 64)])
+        q = rng.randrange(0, 1 << rng.choice([8, 32, 47, 61, 62]))
+        r = rng.randrange(0, d)
+        N = q * d + r
+        if N >> 128:
+            continue
+        assert core.cc_div_floor(N >> 64, N & ((1 << 64) - 1), d) == q
+
+
+def test_core_matches_golden(core):
+    for kind in ("static", "perstep"):
+        for c in load_golden("small_cases.json")[kind]:
+            if not c["syms"]:
+                continue
+            rows = np.array(c["rows"], dtype=np.uint32)
+            rc, data, L = _enc(core, rows, c["syms"], c["prec"])
+            assert rc == 0 and L == c["L"] and data.hex() == c["bytes"], c
+    for c in load_golden("gen_cases.json"):
+        rows = np.stack([synth.pmf_row(c["seed"], t, 0, c["V"], c["kind"], c["exp_range"]) for t in range(c["steps"])])
+        rc, data, L = _enc(core, rows, c["syms"], c["prec"])
+        assert rc == 0 and L == c["L"] and data.hex() == c["bytes"], c["name"]
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_core_random_vs_oracle(core, seed):
+    rng = random.Random(100 + seed)
+    for _ in range(60):
+        V = rng.choice([2, 3, 7, 64, 300, 1000])
+        prec = rng.randint(max(2, (V - 1).bit_length() + 1), 61)
+        kind = rng.choice(["loguniform", "zeros", "peaked", "flat", "llama64"])
+        steps = rng.randint(1, 40)
+        pmf, sym = synth.make_batch(rng.randrange(1 << 30), steps, 1, V, kind)
+        rows = pmf[:, 0, :]
+        want = coracle.encode(rows, sym[:, 0], prec)
+        rc, data, L = _enc(core, rows, sym[:, 0], prec)
+        assert rc == 0 and (data, L) == want[:2], (V, prec, kind)

@@ -1,0 +1,235 @@
+"""GPU parity: liblac.so (HIP, gfx950) vs the oracle and the reference's golden vectors.
+
+Every test calls the product through its C-ABI (lac_amd.batch -> liblac.so).
+Integer/byte work, so the bar is bit-exact everywhere.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+from conftest import load_golden
+from lac_amd import synth
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+def _coder(V, B, prec, bits=32, cap=1 << 16):
+    from lac_amd.batch import BatchCoder
+    return BatchCoder(V, B, prec=prec, pmf_bits=bits, capacity_bits=cap, device=DEV)
+
+
+def _dev_pmf(a):
+    """numpy uint32/uint64 -> int32/int64 device tensor with the same bits."""
+    a = np.ascontiguousarray(a)
+    view = a.view(np.int32) if a.dtype == np.uint32 else a.view(np.int64)
+    return torch.from_numpy(view).to(DEV)
+
+
+def _gpu_encode(pmf_np, sym_np, prec, trace=False):
+    steps, B, V = pmf_np.shape
+    bits = 64 if pmf_np.dtype == np.uint64 else 32
+    c = _coder(V, B, prec, bits, cap=steps * (prec + 2) + 256)
+    pmf = _dev_pmf(pmf_np)
+    sym = torch.from_numpy(np.ascontiguousarray(sym_np, dtype=np.int32)).to(DEV)
+    tr = torch.zeros((steps, B, 2), dtype=torch.int64, device=DEV) if trace else None
+    c.encode(pmf, sym, trace=tr)
+    c.finish()
+    data, n = c.to_bytes()
+    return c, pmf, data, n, tr
+
+
+def _digits_from_trace(tr, b):
+    from lac_amd.batch import digits_of
+    t = tr[:, b, :].cpu().numpy()
+    return [digits_of(int(E), int(k)) for E, k in t]
+
+
+# ---------------------------------------------------------------- golden vectors
+@pytest.mark.parametrize("case", load_golden("gen_cases.json"), ids=lambda c: c["name"])
+def test_golden_gen_case(case):
+    rows = np.stack([synth.pmf_row(case["seed"], t, 0, case["V"], case["kind"], case["exp_range"])
+                     for t in range(case["steps"])])
+    pmf = rows[:, None, :]
+    sym = np.asarray(case["syms"], dtype=np.int32)[:, None]
+    c, dpmf, data, n, tr = _gpu_encode(pmf, sym, case["prec"], trace=True)
+    assert int(n[0]) == case["L"] and data[0].hex() == case["bytes"]
+    assert _digits_from_trace(tr, 0) == case["trace"]
+    assert c.flush_digits()[0] == case["flush"]
+    c.decode_open()
+    out = c.decode(dpmf).cpu().numpy()[:, 0]
+    assert out.tolist() == case["syms"]
+    c.raise_on_error()
+
+
+def test_golden_small_cases():
+    for kind in ("static", "perstep"):
+        for c in load_golden("small_cases.json")[kind]:
+            if not c["syms"]:
+                continue
+            T = len(c["syms"])
+            rows = np.array(c["rows"], dtype=np.uint32)
+            rows = rows if rows.shape[0] == T else np.repeat(rows[:1], T, axis=0)
+            cd, dpmf, data, n, tr = _gpu_encode(rows[:, None, :], np.array(c["syms"])[:, None], c["prec"], trace=True)
+            assert int(n[0]) == c["L"] and data[0].hex() == c["bytes"], c
+            assert _digits_from_trace(tr, 0) == c["trace"]
+            assert cd.flush_digits()[0] == c["flush"]
+            cd.decode_open()
+            assert cd.decode(dpmf).cpu().numpy()[:, 0].tolist() == c["syms"]
+            cd.close()
+
+
+def test_kat1_identity_static_model():
+    """KAT-1 on the GPU: uniform-256 static table (stride 0), prec 48, 1 MiB -> identity."""
+    kat = load_golden("kat.json")["kat1"]
+    data = np.random.default_rng(0).integers(0, 256, kat["n"], dtype=np.uint8)
+    c = _coder(256, 1, 48, cap=kat["n"] * 8 + 4096)
+    row = torch.ones(256, dtype=torch.int32, device=DEV)
+    sym = torch.from_numpy(data.astype(np.int32)).to(DEV).view(-1, 1)
+    c.encode(row, sym)
+    c.finish()
+    out, n = c.to_bytes()
+    assert len(out[0]) == kat["out_len"] and hashlib.sha256(out[0]).hexdigest() == kat["out_sha256"]
+    c.decode_open()
+    dec = c.decode(row.view(1, 1, 256).expand(kat["n"], 1, 256)).cpu().numpy()[:, 0]
+    assert bytes(dec.astype(np.uint8)) == data.tobytes()
+
+
+# ---------------------------------------------------------------- batches vs oracle
+BATCH_CASES = [
+    # V, streams, steps, prec, kind
+    (256, 64, 40, 24, "loguniform"),
+    (1000, 96, 24, 48, "zeros"),
+    (1000, 64, 16, 16, "loguniform"),      # fudged rows
+    (300, 64, 32, 10, "flat"),             # mixed fudged / unfudged
+    (1001, 33, 12, 48, "peaked"),          # odd V: scalar load path
+    (3000, 40, 8, 61, "loguniform"),
+    (1000, 32, 12, 48, "llama64"),         # u64 tables, every row fudged
+    (32000, 16, 4, 48, "loguniform"),
+    (32000, 8, 3, 24, "loguniform"),       # fudged at full vocab
+]
+
+
+@pytest.mark.parametrize("V,B,steps,prec,kind", BATCH_CASES)
+def test_batch_vs_oracle(V, B, steps, prec, kind):
+    from oracle import oracle as coracle
+    pmf, sym = synth.make_batch(1000 + V + prec, steps, B, V, kind)
+    c, dpmf, data, n, tr = _gpu_encode(pmf, sym, prec)
+    out, nb, status, rc = coracle.encode_batch(pmf, sym, prec, nthreads=16)
+    assert rc == 0
+    for b in range(B):
+        assert int(n[b]) == int(nb[b]), b
+        assert data[b] == out[b, :(int(nb[b]) + 7) // 8].tobytes(), b
+    c.decode_open()
+    dec = c.decode(dpmf).cpu().numpy()
+    assert (dec == sym).all()
+    c.raise_on_error()
+
+
+def test_decode_external_bits_from_oracle():
+    """Decode bitstreams produced by the oracle (user-provided device buffers)."""
+    from oracle import oracle as coracle
+    V, B, steps, prec = 512, 48, 20, 32
+    pmf, sym = synth.make_batch(77, steps, B, V, "zeros")
+    out, nb, status, rc = coracle.encode_batch(pmf, sym, prec, nthreads=8)
+    stride = (out.shape[1] + 7) // 8 * 8
+    buf = np.zeros((B, stride), dtype=np.uint8)
+    buf[:, :out.shape[1]] = out
+    c = _coder(V, B, prec)
+    bits = torch.from_numpy(buf).to(DEV)
+    nbits = torch.from_numpy(nb.astype(np.int64)).to(DEV)
+    c.decode_open(bits, nbits)
+    dec = c.decode(_dev_pmf(pmf)).cpu().numpy()
+    assert (dec == sym).all()
+
+
+def test_incremental_encode_matches_one_shot():
+    """Several lac_encode calls (chunks not multiple of 64) == one call."""
+    V, B, steps, prec = 700, 20, 150, 40
+    pmf, sym = synth.make_batch(5, steps, B, V, "loguniform")
+    _, _, one, n1, _ = _gpu_encode(pmf, sym, prec)
+    c = _coder(V, B, prec, cap=steps * (prec + 2) + 256)
+    dp, ds = _dev_pmf(pmf), torch.from_numpy(sym).to(DEV)
+    for a, b in ((0, 1), (1, 70), (70, 71), (71, 150)):
+        c.encode(dp[a:b], ds[a:b].contiguous())
+    c.finish()
+    two, n2 = c.to_bytes()
+    assert (n1 == n2).all() and one == two
+
+
+# ---------------------------------------------------------------- headline shape
+def test_headline_shape_softmax_tables():
+    """V=32000, 4096 streams, random-softmax u32 tables: sampled oracle parity,
+    full round trip, and size-independent properties."""
+    from oracle import oracle as coracle
+    V, B, steps, prec = 32000, 4096, 3, 48
+    pmf, sym = synth.softmax_tables(steps, B, V, seed=1234, device=DEV)
+    c = _coder(V, B, prec, cap=steps * (prec + 2) + 256)
+    c.encode(pmf, sym)
+    c.finish()
+    data, n = c.to_bytes()
+    sample = list(range(0, B, 97)) + [B - 1]
+    sub = pmf[:, sample, :].cpu().numpy().view(np.uint32)
+    out, nb, status, rc = coracle.encode_batch(sub, sym[:, sample].cpu().numpy(), prec, nthreads=16)
+    assert rc == 0
+    for i, b in enumerate(sample):
+        assert data[b] == out[i, :(int(nb[i]) + 7) // 8].tobytes()
+    c.decode_open()
+    assert torch.equal(c.decode(pmf), sym)
+    # every stream ends in the group_bits format: padding bits are zero
+    for b in range(0, B, 7):
+        L = int(n[b])
+        if L % 8:
+            assert data[b][-1] & ((1 << (8 - L % 8)) - 1) == 0
+
+
+# ---------------------------------------------------------------- errors
+def test_error_symbol_range():
+    V, B = 16, 4
+    pmf = torch.ones((2, B, V), dtype=torch.int32, device=DEV)
+    sym = torch.zeros((2, B), dtype=torch.int32, device=DEV)
+    sym[1, 2] = V          # AssertionError('unknown symbol', V) in the reference
+    sym[0, 3] = -1
+    c = _coder(V, B, 16)
+    c.encode(pmf, sym)
+    rc, err, step = c.status()
+    assert rc != 0
+    assert err.tolist() == [0, 0, -3, -3] and step[2] == 1 and step[3] == 0
+
+
+def test_error_zero_width_and_table():
+    V, B = 8, 3
+    pmf = torch.ones((1, B, V), dtype=torch.int32, device=DEV)
+    pmf[0, 0, 5] = 0
+    pmf[0, 1, :] = 0
+    sym = torch.full((1, B), 5, dtype=torch.int32, device=DEV)
+    c = _coder(V, B, 16)
+    c.encode(pmf, sym)
+    rc, err, step = c.status()
+    assert err.tolist() == [-4, -5, 0]
+
+
+def test_error_capacity():
+    V, B, steps = 1000, 2, 200
+    pmf, sym = synth.make_batch(9, steps, B, V, "loguniform")
+    c = _coder(V, B, 48, cap=128)
+    c.encode(_dev_pmf(pmf), torch.from_numpy(sym).to(DEV))
+    rc, err, step = c.status()
+    assert (err == -7).all()
+
+
+def test_open_rejects_bad_prec():
+    from lac_amd._lib import LacError
+    with pytest.raises(LacError):
+        _coder(300, 1, 8)          # 2^(8-1) < 300: the reference coder hangs
+    with pytest.raises(LacError):
+        _coder(10, 1, 62)
