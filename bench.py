@@ -34,8 +34,8 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def read_traffic(cfg):
-    """HBM bytes per row_stats launch from the committed rocprofv3 PMC summary, if it matches."""
+def read_traffic(cfg, kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary, if it matches."""
     p = os.path.join(HERE, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
@@ -44,7 +44,7 @@ def read_traffic(cfg):
         return None
     keys = ("vocab", "streams", "tokens", "pmf_bits")
     if all(d.get(k) == cfg.get(k) for k in keys):
-        return d.get("row_stats_bytes_per_launch")
+        return d.get("bytes_per_launch", {}).get(kernel)
     return None
 
 
@@ -61,6 +61,7 @@ def main():
     ap.add_argument("--cpu-baseline", default="on", choices=("on", "off"))
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-streams", type=int, default=0, help="oracle sample streams (0 = all)")
+    ap.add_argument("--path", default="auto", choices=("auto", "split", "fused"), help="encode kernel path")
     args = ap.parse_args()
 
     import numpy as np
@@ -90,10 +91,11 @@ def main():
         f"in {time.time() - t_gen:.1f}s")
     coder = BatchCoder(V, B, prec=P, pmf_bits=args.pmf_bits, capacity_bits=T * (P + 2) + 256, device=dev)
 
+    if args.path != "auto":
+        coder.set_path(args.path)
+
     def job():
-        coder.reset()
-        coder.encode(pmf, sym)
-        coder.finish()
+        coder.encode_job(pmf, sym)
         if world > 1:
             return gather_bitstreams(coder.bits_tensor(), coder.nbits_tensor())
         return None
@@ -120,8 +122,8 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     import ctypes as C
-    ms = (C.c_double * 4)()
-    cnt = (C.c_int64 * 4)()
+    ms = (C.c_double * 8)()
+    cnt = (C.c_int64 * 8)()
     coder.lib.lac_profile_read(coder.ctx, C.cast(ms, C.c_void_p), C.cast(cnt, C.c_void_p), 1)
 
     # ---------------- checks, outside the timed region
@@ -160,10 +162,12 @@ def main():
         parity["bits_per_symbol"] = avg_bits
 
     if rank == 0:
-        units = T * B                                       # symbols per row_stats launch (T <= 64)
-        rs_launch_ms = ms[0] / max(cnt[0], 1)
+        kid = 4 if cnt[4] else 0                            # encode_fused, else row_stats
+        kname = "k_encode_fused" if kid == 4 else "k_row_stats"
+        units = T * B                                       # symbols per launch (split path: T <= 64)
+        rs_launch_ms = ms[kid] / max(cnt[kid], 1)
         alg_bytes = units * (V * ebytes + 4)
-        achieved = alg_bytes / (rs_launch_ms * 1e-3) / 1e9 if cnt[0] else None
+        achieved = alg_bytes / (rs_launch_ms * 1e-3) / 1e9 if cnt[kid] else None
         cfg = {"workload": f"c3: vocab={V}, {B} streams/GPU, {T} symbols/stream per job, prec={P}, "
                            f"uint{args.pmf_bits} pmf rows",
                "vocab": V, "streams": B, "tokens": T, "prec": P, "pmf_bits": args.pmf_bits,
@@ -178,10 +182,12 @@ def main():
             "config": cfg,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-                         "traffic": read_traffic(cfg), "kernel": "k_row_stats",
-                         "kernel_ms_per_launch": rs_launch_ms, "launches": int(cnt[0]),
+                         "traffic": read_traffic(cfg, kname), "kernel": kname,
+                         "kernel_ms_per_launch": rs_launch_ms, "launches": int(cnt[kid]),
                          "bytes_per_launch": alg_bytes,
-                         "other_kernels_ms_per_step": {"encode": ms[1] / args.steps, "finish": ms[2] / args.steps}},
+                         "kernel_ms_per_step": {n: ms[i] / args.steps for n, i in
+                                                (("row_stats", 0), ("encode", 1), ("finish", 2), ("encode_fused", 4))
+                                                if cnt[i]}},
             "cpu_baseline": cpu,
             "parity": parity,
         }

@@ -62,6 +62,16 @@ enum {
     LAC_E_STATE = -9
 };
 
+enum {                       /* lac_set_option */
+    LAC_OPT_ENCODE_PATH = 1,       /* LAC_PATH_*: which encode kernels run */
+    LAC_OPT_FUSED_MIN_STREAMS = 2  /* AUTO picks the fused kernel from this many streams (2048) */
+};
+enum {
+    LAC_PATH_AUTO = 0,             /* fused if streams >= fused_min_streams, else split */
+    LAC_PATH_SPLIT = 1,            /* row-stats kernel over all (step, stream) rows + coder kernel */
+    LAC_PATH_FUSED = 2             /* one wave per stream: row scan + coder in one kernel */
+};
+
 /* Library identification and the last error message of this thread. */
 const char *lac_version(void);
 const char *lac_last_error(void);
@@ -74,6 +84,9 @@ int lac_open(int device, int prec, int64_t vocab, int64_t streams, int pmf_bits,
              uint64_t capacity_bits, lac_ctx **out);
 int lac_close(lac_ctx *ctx);
 
+/* Tune a context (LAC_OPT_*); results are identical on every path. */
+int lac_set_option(lac_ctx *ctx, int option, int64_t value);
+
 /* Reset every stream to l = 0, h = 2^prec - 1 with an empty output. */
 int lac_encode_reset(lac_ctx *ctx, void *stream);
 
@@ -85,6 +98,13 @@ int lac_encode_reset(lac_ctx *ctx, void *stream);
  * the rest 0/1).  Asynchronous on `stream`. */
 int lac_encode(lac_ctx *ctx, const void *pmf_dev, int64_t step_stride, int64_t stream_stride,
                const int32_t *sym_dev, int64_t steps, uint64_t *trace_dev, void *stream);
+
+/* One whole job in one call: reset every stream, encode `steps` symbols (as
+ * lac_encode), flush and pack (as lac_encode_finish).  The batched counterpart
+ * of bytes(group_bits(AC(...).to_bin.bits(symbols))) (arith_code.py:207-246,
+ * :401-420).  At >= 2048 streams this is a single kernel launch. */
+int lac_encode_job(lac_ctx *ctx, const void *pmf_dev, int64_t step_stride, int64_t stream_stride,
+                   const int32_t *sym_dev, int64_t steps, uint64_t *trace_dev, void *stream);
 
 /* Flush every stream and resolve carries into packed bytes (asynchronous). */
 int lac_encode_finish(lac_ctx *ctx, void *stream);
@@ -137,10 +157,11 @@ int lac_decode_steps(lac_ctx *ctx, const void *pmf_dev, int64_t step_stride, int
 
 /* Live kernel timing: with profiling on, every kernel launch is bracketed by
  * hipEvents recorded on its own stream.  lac_profile_read synchronises and
- * returns, per kernel id (0 row_stats, 1 encode, 2 finish, 3 decode_step),
- * the summed device milliseconds and the launch count; reset != 0 clears. */
+ * returns, per kernel id (0 row_stats, 1 encode, 2 finish, 3 decode_step,
+ * 4 encode_fused; 8 slots), the summed device milliseconds and the launch
+ * count; reset != 0 clears. */
 int lac_profile_enable(lac_ctx *ctx, int on);
-int lac_profile_read(lac_ctx *ctx, double *ms_total /*[4]*/, int64_t *launches /*[4]*/, int reset);
+int lac_profile_read(lac_ctx *ctx, double *ms_total /*[8]*/, int64_t *launches /*[8]*/, int reset);
 
 #ifdef __cplusplus
 }

@@ -40,6 +40,8 @@ PROTOTYPES = [
     ("lac_close", _i, [_vp]),
     ("lac_encode_reset", _i, [_vp, _vp]),
     ("lac_encode", _i, [_vp, _vp, _i64, _i64, _vp, _i64, _vp, _vp]),
+    ("lac_encode_job", _i, [_vp, _vp, _i64, _i64, _vp, _i64, _vp, _vp]),
+    ("lac_set_option", _i, [_vp, _i, _i64]),
     ("lac_encode_finish", _i, [_vp, _vp]),
     ("lac_stream_status", _i, [_vp, _vp, _vp, _vp]),
     ("lac_encoded_lengths", _i, [_vp, _vp, _vp]),
@@ -56,7 +58,10 @@ PROTOTYPES = [
     ("lac_profile_read", _i, [_vp, _vp, _vp, _i]),
 ]
 
-KERNEL_IDS = {"row_stats": 0, "encode": 1, "finish": 2, "decode_step": 3}
+KERNEL_IDS = {"row_stats": 0, "encode": 1, "finish": 2, "decode_step": 3, "encode_fused": 4}
+LAC_OPT_ENCODE_PATH = 1
+LAC_OPT_FUSED_MIN_STREAMS = 2
+LAC_PATH_AUTO, LAC_PATH_SPLIT, LAC_PATH_FUSED = 0, 1, 2
 
 
 class LacLibraryError(RuntimeError):

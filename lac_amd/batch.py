@@ -106,15 +106,7 @@ class BatchCoder:
         check(self.lib.lac_encode_reset(self.ctx, self._stream))
         self._finished = False
 
-    def encode(self, pmf, sym, trace=None):
-        """Encode sym[t, b] with row pmf[t, b, :] (or pmf[b, :] / pmf[:] broadcast).
-
-        ``pmf`` [steps, streams, V], [streams, V] (steps == 1), [V] (a static
-        row for every step and stream) or [steps, 1, V] / [1, streams, V] with
-        stride-0 broadcasting via ``expand``.  ``sym`` int32 [steps, streams].
-        ``trace`` (optional int64 device tensor [steps, streams, 2]) receives
-        per symbol {E, k} -- its raw digits.
-        """
+    def _encode_args(self, pmf, sym, trace):
         torch = _torch()
         self._check_pmf(pmf)
         if sym.dtype != torch.int32 or sym.device != self.device:
@@ -139,8 +131,31 @@ class BatchCoder:
             if trace.dtype != torch.int64 or trace.numel() != steps * self.streams * 2 or not trace.is_contiguous():
                 raise ValueError("trace must be a contiguous int64 tensor [steps, streams, 2]")
             tp = C.c_void_p(trace.data_ptr())
-        check(self.lib.lac_encode(self.ctx, C.c_void_p(pmf.data_ptr()), step_stride, stream_stride,
-                                  C.c_void_p(sym.data_ptr()), steps, tp, self._stream))
+        self._keep = (pmf, sym)
+        return (self.ctx, C.c_void_p(pmf.data_ptr()), step_stride, stream_stride, C.c_void_p(sym.data_ptr()),
+                steps, tp, self._stream)
+
+    def encode(self, pmf, sym, trace=None):
+        """Encode sym[t, b] with row pmf[t, b, :] (or pmf[b, :] / pmf[:] broadcast).
+
+        ``pmf`` [steps, streams, V], [streams, V] (steps == 1), [V] (a static
+        row for every step and stream) or [steps, 1, V] / [1, streams, V] with
+        stride-0 broadcasting via ``expand``.  ``sym`` int32 [steps, streams].
+        ``trace`` (optional int64 device tensor [steps, streams, 2]) receives
+        per symbol {E, k} -- its raw digits.  Streams continue from where the
+        previous call left them.
+        """
+        check(self.lib.lac_encode(*self._encode_args(pmf, sym, trace)))
+
+    def encode_job(self, pmf, sym, trace=None):
+        """reset + encode + finish in one call (one kernel at >= 2048 streams)."""
+        check(self.lib.lac_encode_job(*self._encode_args(pmf, sym, trace)))
+        self._finished = True
+
+    def set_path(self, path):
+        """'auto', 'split' or 'fused' encode kernels (bit-identical results)."""
+        v = {"auto": _lib.LAC_PATH_AUTO, "split": _lib.LAC_PATH_SPLIT, "fused": _lib.LAC_PATH_FUSED}[path]
+        check(self.lib.lac_set_option(self.ctx, _lib.LAC_OPT_ENCODE_PATH, v))
 
     def finish(self):
         check(self.lib.lac_encode_finish(self.ctx, self._stream))

@@ -59,10 +59,6 @@ __device__ inline i128 shfl_i128(i128 v, int src) {
     const u128 u = (u128)v;
     return (i128)(((u128)shfl_u64((uint64_t)(u >> 64), src) << 64) | shfl_u64((uint64_t)u, src));
 }
-__device__ inline i128 shfl_up_i128(i128 v, int d) {
-    const u128 u = (u128)v;
-    return (i128)(((u128)shfl_up_u64((uint64_t)(u >> 64), d) << 64) | shfl_up_u64((uint64_t)u, d));
-}
 __device__ inline i128 shfl_xor_i128(i128 v, int m) {
     const u128 u = (u128)v;
     return (i128)(((u128)shfl_xor_u64((uint64_t)(u >> 64), m) << 64) | shfl_xor_u64((uint64_t)u, m));
@@ -103,13 +99,6 @@ __device__ inline uint64_t wave_incl_scan_u64(uint64_t v) {
     for (int d = 1; d < 64; d <<= 1) { const uint64_t t = shfl_up_u64(v, d); if (lane >= d) v += t; }
     return v;
 }
-__device__ inline i128 wave_incl_maxscan_i128(i128 v) {
-    const int lane = (int)lane_id();
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) { const i128 t = shfl_up_i128(v, d); if (lane >= d && t > v) v = t; }
-    return v;
-}
-
 constexpr i128 kI128Min = (i128)((u128)1 << 127);
 
 // ------------------------------------------------------------------ row loads
@@ -129,28 +118,27 @@ __device__ inline E vget(const typename VecT<E, VEC>::type &v, int j) {
     if constexpr (VEC == 1) { (void)j; return v; } else { return v[j]; }
 }
 
-// ------------------------------------------------------------------ k_row_stats
-// Wave-per-row scan: T = sum pmf, lo = sum_{i<s} pmf, minp = min positive pmf.
+// ------------------------------------------------------------------ row reduction
+// One wave scans a pmf row: T = sum pmf, lo = sum_{i<s} pmf, ps = pmf[s],
+// minp = smallest positive entry (CDFPredictor.minp, arith_code.py:79-82) -- the
+// only per-row quantities symbol_to_range (:98-110) needs when unfudged.
 // u32 rows accumulate in u64 (V < 2^32 keeps it exact); u64 rows split each entry
 // into 32-bit halves so a total >= 2^64 is detected instead of wrapping.
+struct RowSums {
+    u128 T, lo;
+    uint64_t ps, minp;
+};
+
 template <typename E, int VEC>
-__global__ __launch_bounds__(256) void k_row_stats(const E *__restrict__ pmf, int64_t step_stride,
-                                                   int64_t stream_stride, const int32_t *__restrict__ sym,
-                                                   int64_t B, int64_t rows, int64_t V, int64_t t0,
-                                                   RowStats *__restrict__ out) {
+__device__ inline RowSums row_reduce(const E *row, int64_t V, int64_t s) {
     const int lane = (int)lane_id();
-    const int64_t r = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-    if (r >= rows) return;
-    const int64_t t = t0 + r / B, b = r % B;
-    const E *row = pmf + t * step_stride + b * stream_stride;
-    const int64_t s = sym[t * B + b];
     const int64_t sc = s < 0 ? 0 : (s > V ? V : s);
     const int64_t nvec = V / VEC, sfull = sc / VEC;
+    const int sr = (int)(sc - sfull * VEC);
     constexpr bool W = sizeof(E) == 8;
-    uint64_t tot = 0, lo = 0, tot_h = 0, lo_h = 0;         // *_h: high halves (u64 rows)
-    E mn = (E)~(E)0;                                      // min over (x - 1): 0 wraps to max
+    uint64_t tot = 0, lo = 0, tot_h = 0, lo_h = 0, ps = 0;     // *_h: high halves (u64 rows)
+    E mn = (E)~(E)0;                                          // min over (x - 1): 0 wraps to max
     constexpr int U = 8;
-    int64_t vi = lane;
     auto take = [&](const typename VecT<E, VEC>::type &x, int64_t v) {
         uint64_t sl = 0, sh = 0;
 #pragma unroll
@@ -163,7 +151,18 @@ __global__ __launch_bounds__(256) void k_row_stats(const E *__restrict__ pmf, in
         tot += sl;
         tot_h += sh;
         if (v < sfull) { lo += sl; lo_h += sh; }
+        if (v == sfull) {                                     // the vector holding symbol s
+#pragma unroll
+            for (int j = 0; j < VEC; j++) {
+                const E e = vget<E, VEC>(x, j);
+                if (j < sr) {
+                    if constexpr (W) { lo += (uint32_t)e; lo_h += (uint64_t)e >> 32; } else { lo += e; }
+                }
+                if (j == sr) ps = (uint64_t)e;
+            }
+        }
     };
+    int64_t vi = lane;
     for (; vi + 64 * (U - 1) < nvec; vi += 64 * U) {
         typename VecT<E, VEC>::type x[U];
 #pragma unroll
@@ -172,37 +171,28 @@ __global__ __launch_bounds__(256) void k_row_stats(const E *__restrict__ pmf, in
         for (int u = 0; u < U; u++) take(x[u], vi + 64 * u);
     }
     for (; vi < nvec; vi += 64) take(load_vec<E, VEC>(row, vi), vi);
+    RowSums r;
     tot = wave_sum_u64(tot);
     lo = wave_sum_u64(lo);
+    ps = wave_sum_u64(ps);
     if constexpr (W) {
         tot_h = wave_sum_u64(tot_h);
         lo_h = wave_sum_u64(lo_h);
+        r.minp = wave_min_u64(mn) + 1;
+    } else {
+        r.minp = (uint64_t)wave_min_u32(mn) + 1;
     }
-    uint64_t m;
-    if constexpr (W) m = wave_min_u64(mn); else m = wave_min_u32(mn);
-    if (lane == 0) {
-        RowStats st;
-        u128 T = (u128)tot + ((u128)tot_h << 32), L = (u128)lo + ((u128)lo_h << 32);
-        for (int64_t i = sfull * VEC; i < sc; i++) L += (uint64_t)row[i];   // partial vector below s
-        const bool bad_s = s < 0 || s >= V;
-        const u128 Hh = L + (bad_s ? 0 : (uint64_t)row[s]);
-        if (T >> 64) {
-            st.lo = st.hi = st.tot = 0;
-            st.minp = 1;                                  // total >= 2^64
-        } else {
-            st.lo = (uint64_t)L;
-            st.hi = (uint64_t)Hh;
-            st.tot = (uint64_t)T;
-            st.minp = T ? m + 1 : 0;
-        }
-        out[r] = st;
-    }
+    r.T = (u128)tot + ((u128)tot_h << 32);
+    r.lo = (u128)lo + ((u128)lo_h << 32);
+    r.ps = ps;
+    return r;
 }
 
 // ------------------------------------------------------------------ fudge scan
-// max_{j<n} (c_j*w - j*T) over the first n entries of a row, by one wave.
+// max_{j<n} (c_j*w - j*T) over the first n entries of a row, by one wave;
+// *csum (optional) receives c_{n-1}.
 template <typename E>
-__device__ i128 wave_xmax_prefix(const E *row, int64_t n, uint64_t w, uint64_t T) {
+__device__ i128 wave_xmax_prefix(const E *row, int64_t n, uint64_t w, uint64_t T, uint64_t *csum = nullptr) {
     const int lane = (int)lane_id();
     constexpr int VEC = 4;
     i128 best = kI128Min;
@@ -237,10 +227,126 @@ __device__ i128 wave_xmax_prefix(const E *row, int64_t n, uint64_t w, uint64_t T
         }
         base += readlane_u64(incl, 63);
     }
+    if (csum) *csum = base;
     return wave_max_i128(best);
 }
 
-// ------------------------------------------------------------------ k_encode
+// ------------------------------------------------------------------ coder step
+// receive_symbol + decide_bit/emit_bit loop of A_to_bin (arith_code.py:169-192)
+// for one stream, executed uniformly by its wave.  Returns false (st.err set)
+// on a coder error.
+template <typename E>
+__device__ inline bool coder_step(EncState &st, int64_t &l, int64_t &h, uint64_t lo, uint64_t hi, uint64_t T,
+                                  uint64_t minp, int64_t s, const E *row, int64_t V, int prec, uint64_t *pa,
+                                  uint64_t *pc, uint64_t cap_words, uint64_t *trace_slot, int lane) {
+    if (s < 0 || s >= V) { st.err = LAC_E_SYMBOL_RANGE; return false; }   // arith_code.py:100-101
+    if (T == 0) { st.err = LAC_E_TABLE; return false; }
+    const uint64_t w = (uint64_t)(h - l + 1);
+    uint64_t a, bb;
+    if (!is_fudged(T, w, minp)) {
+        unfudged_range(lo, hi, T, w, &a, &bb);
+    } else {                                                  // CDFPredictor.fudged_dist
+        const i128 xprev = s > 0 ? wave_xmax_prefix<E>(row, s, w, T) : kI128Min;
+        const i128 xs = fudge_x(hi, s, w, T);
+        a = s > 0 ? fudge_f(s - 1, xprev, T, w, V) : 0;
+        bb = fudge_f(s, xs > xprev ? xs : xprev, T, w, V);
+    }
+    if (a >= bb) { st.err = LAC_E_ZERO_WIDTH; return false; }   // the reference hangs here
+    h = l + (int64_t)bb - 1;
+    l = l + (int64_t)a;
+    int k;
+    uint64_t Ev;
+    renorm(l, h, prec, &k, &Ev);
+    if (trace_slot && lane == 0) { trace_slot[0] = Ev; trace_slot[1] = (uint64_t)k; }
+    auto store = [&](uint64_t idx, uint64_t wa, uint64_t wc) {
+        if (lane == 0) { pa[idx] = wa; pc[idx] = wc; }
+    };
+    if (!plane_append(st.L, st.wa, st.wc, k, Ev, cap_words, store)) { st.err = LAC_E_CAPACITY; return false; }
+    st.nsym++;
+    return true;
+}
+
+__device__ inline void store_state(EncState &st, int64_t l, int64_t h, uint64_t *pa, uint64_t *pc,
+                                   uint64_t cap_words, EncState *slot) {
+    if (st.err) st.err_step = st.nsym;
+    if (st.L > 0 && ((st.L - 1) >> 6) < cap_words) { pa[(st.L - 1) >> 6] = st.wa; pc[(st.L - 1) >> 6] = st.wc; }
+    st.l = l;
+    st.h = h;
+    *slot = st;
+}
+
+__host__ __device__ inline EncState fresh_state(int prec) {
+    EncState st;
+    memset(&st, 0, sizeof(st));
+    st.l = 0;
+    st.h = ((int64_t)1 << prec) - 1;
+    st.nflush = -1;
+    st.err_step = -1;
+    return st;
+}
+
+// flush (arith_code.py:193-202) + R = A + C + F by a backward big-integer add +
+// big-endian bytes (bits() :227-246, group_bits :336-347), in place.  One lane.
+__device__ inline void finish_stream(EncState &st, uint64_t *pa, const uint64_t *pc, uint64_t cap_words, int prec,
+                                     uint64_t *nbits_slot) {
+    if (st.err || st.nflush >= 0) {
+        *nbits_slot = st.err ? 0 : st.L;
+        return;
+    }
+    int8_t fd[8];
+    const int m = flush_digits(st.l, st.h, prec, fd);
+    if (m < 0) { st.err = LAC_E_CAPACITY; st.err_step = st.nsym; *nbits_slot = 0; return; }
+    int64_t F = 0;
+    for (int i = 0; i < m; i++) F = F * 2 + fd[i];
+    const uint64_t L = st.L, Lf = L + (uint64_t)m;
+    const uint64_t nwords = (Lf + 63) >> 6;
+    if (nwords > cap_words) { st.err = LAC_E_CAPACITY; st.err_step = st.nsym; *nbits_slot = 0; return; }
+    const int pad = (int)(nwords * 64 - Lf);
+    i128 carry = (i128)F * ((i128)1 << pad);
+    const int64_t last = L ? (int64_t)((L - 1) >> 6) : -1;
+    for (int64_t i = (int64_t)nwords - 1; i >= 0; i--) {
+        const uint64_t a = i <= last ? pa[i] : 0, c = i <= last ? pc[i] : 0;
+        const i128 sm = (i128)(u128)a + (i128)(u128)c + carry;
+        pa[i] = bswap64((uint64_t)sm);
+        carry = sm >> 64;
+    }
+    if (carry != 0) st.err = LAC_E_ARG;                   // R >= 2^L: impossible for the reference
+    st.nflush = m;
+    for (int i = 0; i < 8; i++) st.flush[i] = i < m ? fd[i] : 0;
+    st.L = Lf;
+    *nbits_slot = st.err ? 0 : Lf;
+}
+
+// ------------------------------------------------------------------ split path
+// k_row_stats: one wave per (step, stream) row -> RowStats.  Fully parallel over
+// steps x streams: the path for small stream counts.
+template <typename E, int VEC>
+__global__ __launch_bounds__(256) void k_row_stats(const E *__restrict__ pmf, int64_t step_stride,
+                                                   int64_t stream_stride, const int32_t *__restrict__ sym,
+                                                   int64_t B, int64_t rows, int64_t V, int64_t t0,
+                                                   RowStats *__restrict__ out) {
+    const int lane = (int)lane_id();
+    const int64_t r = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (r >= rows) return;
+    const int64_t t = t0 + r / B, b = r % B;
+    const RowSums rs = row_reduce<E, VEC>(pmf + t * step_stride + b * stream_stride, V, sym[t * B + b]);
+    if (lane == 0) {
+        RowStats st;
+        if (rs.T >> 64) {
+            st.lo = st.hi = st.tot = 0;
+            st.minp = 1;                                  // total >= 2^64
+        } else {
+            st.lo = (uint64_t)rs.lo;
+            st.hi = (uint64_t)rs.lo + rs.ps;
+            st.tot = (uint64_t)rs.T;
+            st.minp = rs.T ? rs.minp : 0;
+        }
+        out[r] = st;
+    }
+}
+
+// k_encode: one wave per stream over a chunk of <= 64 steps; lane i prefetches
+// step i's RowStats.
 template <typename E>
 __global__ __launch_bounds__(256) void k_encode(const RowStats *__restrict__ stats, const int32_t *__restrict__ sym,
                                                 int64_t B, int64_t t0, int nsteps, const E *pmf,
@@ -262,98 +368,80 @@ __global__ __launch_bounds__(256) void k_encode(const RowStats *__restrict__ sta
         mys = sym[(t0 + lane) * B + b];
     }
     uint64_t *pa = planeA + (uint64_t)b * cap_words, *pc = planeC + (uint64_t)b * cap_words;
-    auto store = [&](uint64_t idx, uint64_t wa, uint64_t wc) {
-        if (lane == 0) { pa[idx] = wa; pc[idx] = wc; }
-    };
     int64_t l = st.l, h = st.h;
     for (int i = 0; i < nsteps; i++) {
         const uint64_t lo = readlane_u64(my.lo, i), hi = readlane_u64(my.hi, i);
         const uint64_t T = readlane_u64(my.tot, i), minp = readlane_u64(my.minp, i);
         const int64_t s = __builtin_amdgcn_readlane(mys, i);
-        if (s < 0 || s >= V) { st.err = LAC_E_SYMBOL_RANGE; break; }
-        if (T == 0) { st.err = LAC_E_TABLE; break; }
-        const uint64_t w = (uint64_t)(h - l + 1);
-        uint64_t a, bb;
-        if (!is_fudged(T, w, minp)) {
-            unfudged_range(lo, hi, T, w, &a, &bb);
-        } else {                                              // CDFPredictor.fudged_dist
-            const E *row = pmf + (t0 + i) * step_stride + b * stream_stride;
-            const i128 xprev = s > 0 ? wave_xmax_prefix<E>(row, s, w, T) : kI128Min;
-            const i128 xs = fudge_x(hi, s, w, T);
-            a = s > 0 ? fudge_f(s - 1, xprev, T, w, V) : 0;
-            bb = fudge_f(s, xs > xprev ? xs : xprev, T, w, V);
+        const E *row = pmf + (t0 + i) * step_stride + b * stream_stride;
+        if (!coder_step<E>(st, l, h, lo, hi, T, minp, s, row, V, prec, pa, pc, cap_words,
+                           trace ? trace + 2 * ((t0 + i) * B + b) : nullptr, lane))
+            break;
+    }
+    if (lane == 0) store_state(st, l, h, pa, pc, cap_words, &states[b]);
+}
+
+// ------------------------------------------------------------------ fused path
+// k_encode_fused: one wave owns one stream for the whole call.  Per step it scans
+// the row (HBM-bound) and applies the range update in registers, so no per-row
+// statistics round-trip through HBM and no second launch; with kReset/kFinish
+// the stream is also initialised and flushed + packed in the same launch.  With
+// >= 2048 streams there are >= 8 waves per CU streaming rows, which hides each
+// wave's short serial coder step behind the others' loads.
+enum { kReset = 1, kFinish = 2 };
+
+template <typename E, int VEC>
+__global__ __launch_bounds__(256) void k_encode_fused(const E *__restrict__ pmf, int64_t step_stride,
+                                                      int64_t stream_stride, const int32_t *__restrict__ sym,
+                                                      int64_t B, int64_t t0, int64_t nsteps, int64_t V, int prec,
+                                                      EncState *states, uint64_t *planeA, uint64_t *planeC,
+                                                      uint64_t cap_words, uint64_t *trace, uint64_t *nbits, int flags) {
+    const int lane = (int)lane_id();
+    const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (b >= B) return;
+    EncState st = (flags & kReset) ? fresh_state(prec) : states[b];
+    uint64_t *pa = planeA + (uint64_t)b * cap_words, *pc = planeC + (uint64_t)b * cap_words;
+    if (st.err || st.nflush >= 0) {
+        if (!st.err && st.nflush >= 0 && nsteps > 0) { st.err = LAC_E_STATE; st.err_step = st.nsym; }
+        if (lane == 0) {
+            states[b] = st;
+            if (flags & kFinish) nbits[b] = st.err ? 0 : st.L;
         }
-        if (a >= bb) { st.err = LAC_E_ZERO_WIDTH; break; }
-        h = l + (int64_t)bb - 1;
-        l = l + (int64_t)a;
-        int k;
-        uint64_t Ev;
-        renorm(l, h, prec, &k, &Ev);
-        if (trace && lane == 0) {
-            trace[2 * ((t0 + i) * B + b)] = Ev;
-            trace[2 * ((t0 + i) * B + b) + 1] = (uint64_t)k;
-        }
-        if (!plane_append(st.L, st.wa, st.wc, k, Ev, cap_words, store)) { st.err = LAC_E_CAPACITY; break; }
-        st.nsym++;
+        return;
+    }
+    int64_t l = st.l, h = st.h;
+    for (int64_t i = 0; i < nsteps; i++) {
+        const int64_t t = t0 + i;
+        const E *row = pmf + t * step_stride + b * stream_stride;
+        const int64_t s = sym[t * B + b];
+        const RowSums rs = row_reduce<E, VEC>(row, V, s);
+        if (rs.T >> 64) { st.err = LAC_E_TABLE; break; }
+        const uint64_t lo = (uint64_t)rs.lo;
+        if (!coder_step<E>(st, l, h, lo, lo + rs.ps, (uint64_t)rs.T, rs.minp, s, row, V, prec, pa, pc, cap_words,
+                           trace ? trace + 2 * (t * B + b) : nullptr, lane))
+            break;
     }
     if (lane == 0) {
-        if (st.err) st.err_step = st.nsym;
-        if (st.L > 0 && ((st.L - 1) >> 6) < cap_words) { pa[(st.L - 1) >> 6] = st.wa; pc[(st.L - 1) >> 6] = st.wc; }
-        st.l = l;
-        st.h = h;
+        store_state(st, l, h, pa, pc, cap_words, &st);
+        if (flags & kFinish) finish_stream(st, pa, pc, cap_words, prec, &nbits[b]);
         states[b] = st;
     }
 }
 
 // ------------------------------------------------------------------ k_finish
-// flush + R = A + C + F (backward big-integer add) + big-endian byte packing, in place.
 __global__ __launch_bounds__(256) void k_finish(EncState *states, uint64_t *planeA, const uint64_t *planeC,
                                                 uint64_t cap_words, int64_t B, int prec, uint64_t *nbits) {
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= B) return;
     EncState st = states[b];
-    if (st.err || st.nflush >= 0) {
-        if (!st.err) nbits[b] = st.L;
-        else nbits[b] = 0;
-        return;
-    }
-    int8_t fd[8];
-    const int m = flush_digits(st.l, st.h, prec, fd);
-    if (m < 0) { st.err = LAC_E_CAPACITY; st.err_step = st.nsym; states[b] = st; nbits[b] = 0; return; }
-    int64_t F = 0;
-    for (int i = 0; i < m; i++) F = F * 2 + fd[i];
-    const uint64_t L = st.L, Lf = L + (uint64_t)m;
-    const uint64_t nwords = (Lf + 63) >> 6;
-    if (nwords > cap_words) { st.err = LAC_E_CAPACITY; st.err_step = st.nsym; states[b] = st; nbits[b] = 0; return; }
-    const int pad = (int)(nwords * 64 - Lf);
-    i128 carry = (i128)F * ((i128)1 << pad);
-    const int64_t last = L ? (int64_t)((L - 1) >> 6) : -1;
-    uint64_t *pa = planeA + (uint64_t)b * cap_words;
-    const uint64_t *pc = planeC + (uint64_t)b * cap_words;
-    for (int64_t i = (int64_t)nwords - 1; i >= 0; i--) {
-        const uint64_t a = i <= last ? pa[i] : 0, c = i <= last ? pc[i] : 0;
-        const i128 sm = (i128)(u128)a + (i128)(u128)c + carry;
-        pa[i] = bswap64((uint64_t)sm);
-        carry = sm >> 64;
-    }
-    if (carry != 0) st.err = LAC_E_ARG;                   // R >= 2^L: impossible for the reference
-    st.nflush = m;
-    for (int i = 0; i < 8; i++) st.flush[i] = i < m ? fd[i] : 0;
-    st.L = Lf;
+    finish_stream(st, planeA + (uint64_t)b * cap_words, planeC + (uint64_t)b * cap_words, cap_words, prec, &nbits[b]);
     states[b] = st;
-    nbits[b] = st.err ? 0 : Lf;
 }
 
 __global__ void k_enc_reset(EncState *states, int64_t B, int prec) {
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= B) return;
-    EncState st;
-    memset(&st, 0, sizeof(st));
-    st.l = 0;
-    st.h = ((int64_t)1 << prec) - 1;
-    st.nflush = -1;
-    st.err_step = -1;
-    states[b] = st;
+    states[b] = fresh_state(prec);
 }
 
 // ------------------------------------------------------------------ decode
@@ -527,12 +615,15 @@ __global__ __launch_bounds__(256) void k_decode_step(const E *__restrict__ pmf, 
         s = cidx * CH + (int64_t)cnt;
         if (!err) unfudged_range(lo_c, hi_c, T, w, &a, &bb);
     } else if (!err) {
-        // fudged: first i with f_i > v, walking the row once (fudged_dist closed form)
+        // fudged (fudged_dist closed form).  f is strictly increasing and
+        // f_e = e + g(Xmax_e) with g monotone, so f_e > v  <=>  some j <= e has
+        // e > v - g(X_j); the first such e is  s = min_j max(j, v + 1 - g(X_j)),
+        // a plain min-reduction over the row (no ordered scan of the maxima).
         const uint64_t C = w - (uint64_t)V + 1;
         uint64_t base = 0;
-        i128 xrun = kI128Min;
+        int64_t best = V;
         constexpr int FV = 4;
-        for (int64_t r0 = 0; r0 < V && s < 0; r0 += 64 * FV) {
+        for (int64_t r0 = 0; r0 < V; r0 += 64 * FV) {
             E xe[FV];
             uint64_t ls = 0;
 #pragma unroll
@@ -543,43 +634,35 @@ __global__ __launch_bounds__(256) void k_decode_step(const E *__restrict__ pmf, 
             }
             const uint64_t in = wave_incl_scan_u64(ls);
             uint64_t c = base + in - ls;
-            i128 X[FV];
-            i128 lm = kI128Min;
 #pragma unroll
             for (int j = 0; j < FV; j++) {
                 const int64_t e = r0 + lane * FV + j;
                 c += (uint64_t)xe[j];
-                X[j] = e < V ? fudge_x(c, e, w, T) : kI128Min;
-                lm = X[j] > lm ? X[j] : lm;
-            }
-            const i128 inm = wave_incl_maxscan_i128(lm);
-            i128 exm = shfl_up_i128(inm, 1);
-            if (lane == 0) exm = kI128Min;
-            i128 runm = exm > xrun ? exm : xrun;
-            int64_t myfail = -1;
-            i128 before = kI128Min, after = kI128Min;
-#pragma unroll
-            for (int j = 0; j < FV; j++) {
-                const int64_t e = r0 + lane * FV + j;
-                const i128 prev = runm;
-                runm = X[j] > runm ? X[j] : runm;
-                if (e < V && myfail < 0) {
-                    const int64_t rr = (int64_t)v - e;
-                    const bool le = rr >= 1 && ((uint64_t)rr >= C || runm < (i128)(rr + 1) * (i128)T);
-                    if (!le) { myfail = e; before = prev; after = runm; }
+                if (e < V) {
+                    const i128 X = fudge_x(c, e, w, T);
+                    uint64_t g = 1;
+                    if (X >= (i128)2 * (i128)T) {
+                        const uint64_t m = div_floor((u128)X, T);
+                        g = m < C ? m : C;
+                    }
+                    int64_t cand = (int64_t)v + 1 - (int64_t)g;
+                    cand = cand > e ? cand : e;
+                    best = cand < best ? cand : best;
                 }
             }
-            const uint64_t mask = __ballot(myfail >= 0);
-            if (mask) {
-                const int src = __ffsll((unsigned long long)mask) - 1;
-                s = (int64_t)readlane_u64((uint64_t)myfail, src);
-                const i128 xb = shfl_i128(before, src), xa = shfl_i128(after, src);
-                a = s > 0 ? fudge_f(s - 1, xb, T, w, V) : 0;
-                bb = fudge_f(s, xa, T, w, V);
-            }
             base += readlane_u64(in, 63);
-            const i128 tm = shfl_i128(inm, 63);
-            xrun = tm > xrun ? tm : xrun;
+            const int64_t wb = (int64_t)wave_min_u64((uint64_t)best);
+            if (wb < r0 + 64 * FV) break;                      // later j cannot beat it
+        }
+        s = (int64_t)wave_min_u64((uint64_t)best);
+        if (s >= 0 && s < V) {
+            uint64_t cprev = 0;
+            const i128 xprev = s > 0 ? wave_xmax_prefix<E>(row, s, w, T, &cprev) : kI128Min;
+            const i128 xs = fudge_x(cprev + (uint64_t)row[s], s, w, T);
+            a = s > 0 ? fudge_f(s - 1, xprev, T, w, V) : 0;
+            bb = fudge_f(s, xs > xprev ? xs : xprev, T, w, V);
+        } else {
+            s = -1;
         }
         if (s < 0) err = LAC_E_DECODE_RANGE;
     }
@@ -625,6 +708,8 @@ struct lac_ctx {
     uint64_t dstride = 0;
     const uint64_t *dnbits = nullptr;
     int mode = 0;                       // 0 encode, 1 decode
+    int path = LAC_PATH_AUTO;           // encode kernel path (lac_set_option)
+    int64_t fused_min_streams = 2048;   // AUTO: fused kernel from this many streams
     // live kernel timing (lac_profile_enable): hipEvent pairs around launches
     bool prof = false;
     std::vector<hipEvent_t> ev_pool;
@@ -632,7 +717,7 @@ struct lac_ctx {
     size_t ev_next = 0;
 };
 
-enum { KID_ROW_STATS = 0, KID_ENCODE = 1, KID_FINISH = 2, KID_DECODE = 3, KID_COUNT = 4 };
+enum { KID_ROW_STATS = 0, KID_ENCODE = 1, KID_FINISH = 2, KID_DECODE = 3, KID_FUSED = 4, KID_COUNT = 8 };
 
 static hipEvent_t ev_get(lac_ctx *c) {
     if (c->ev_next == c->ev_pool.size()) {
@@ -689,25 +774,68 @@ static inline hipStream_t S(void *s) { return reinterpret_cast<hipStream_t>(s); 
 
 template <typename E, int VEC>
 static int encode_impl(lac_ctx *c, const E *pmf, int64_t step_stride, int64_t stream_stride, const int32_t *sym,
-                       int64_t steps, uint64_t *trace, hipStream_t st) {
+                       int64_t steps, uint64_t *trace, hipStream_t st, int flags) {
+    const unsigned blocks = (unsigned)((c->B + kWavesPerBlock - 1) / kWavesPerBlock);
+    const bool fused = c->path == LAC_PATH_FUSED || (c->path == LAC_PATH_AUTO && c->B >= c->fused_min_streams);
+    if (fused) {
+        ProfScope ps(c, KID_FUSED, st);
+        k_encode_fused<E, VEC><<<blocks, 64 * kWavesPerBlock, 0, st>>>(
+            pmf, step_stride, stream_stride, sym, c->B, 0, steps, c->V, c->prec, c->enc, c->planeA, c->planeC,
+            c->cap_words, trace, c->nbits, flags);
+        CHECK_LAUNCH();
+        return LAC_OK;
+    }
+    if (flags & kReset) {
+        k_enc_reset<<<(unsigned)((c->B + 255) / 256), 256, 0, st>>>(c->enc, c->B, c->prec);
+        CHECK_LAUNCH();
+    }
     for (int64_t t0 = 0; t0 < steps; t0 += kChunkSteps) {
         const int n = (int)((steps - t0) < kChunkSteps ? (steps - t0) : kChunkSteps);
         const int64_t rows = (int64_t)n * c->B;
         {
-        ProfScope ps(c, KID_ROW_STATS, st);
-        k_row_stats<E, VEC><<<(unsigned)((rows + kWavesPerBlock - 1) / kWavesPerBlock), 64 * kWavesPerBlock, 0, st>>>(
-            pmf, step_stride, stream_stride, sym, c->B, rows, c->V, t0, c->stats);
+            ProfScope ps(c, KID_ROW_STATS, st);
+            k_row_stats<E, VEC><<<(unsigned)((rows + kWavesPerBlock - 1) / kWavesPerBlock), 64 * kWavesPerBlock, 0,
+                                  st>>>(pmf, step_stride, stream_stride, sym, c->B, rows, c->V, t0, c->stats);
         }
         CHECK_LAUNCH();
         {
-        ProfScope ps(c, KID_ENCODE, st);
-        k_encode<E><<<(unsigned)((c->B + kWavesPerBlock - 1) / kWavesPerBlock), 64 * kWavesPerBlock, 0, st>>>(
-            c->stats, sym, c->B, t0, n, pmf, step_stride, stream_stride, c->V, c->prec, c->enc, c->planeA,
-            c->planeC, c->cap_words, trace);
+            ProfScope ps(c, KID_ENCODE, st);
+            k_encode<E><<<blocks, 64 * kWavesPerBlock, 0, st>>>(c->stats, sym, c->B, t0, n, pmf, step_stride,
+                                                                stream_stride, c->V, c->prec, c->enc, c->planeA,
+                                                                c->planeC, c->cap_words, trace);
         }
         CHECK_LAUNCH();
     }
+    if (flags & kFinish) {
+        ProfScope ps(c, KID_FINISH, st);
+        k_finish<<<(unsigned)((c->B + 255) / 256), 256, 0, st>>>(c->enc, c->planeA, c->planeC, c->cap_words, c->B,
+                                                                 c->prec, c->nbits);
+        CHECK_LAUNCH();
+    }
     return LAC_OK;
+}
+
+static int encode_dispatch(lac_ctx *c, const void *pmf_dev, int64_t step_stride, int64_t stream_stride,
+                           const int32_t *sym_dev, int64_t steps, uint64_t *trace_dev, void *stream, int flags) {
+    if (!c || !pmf_dev || !sym_dev) return fail(LAC_E_ARG, "NULL argument");
+    if (steps < 0 || step_stride < 0 || stream_stride < 0) return fail(LAC_E_ARG, "negative size/stride");
+    if (steps == 0 && !flags) return LAC_OK;
+    HIPCHK(hipSetDevice(c->device));
+    c->mode = 0;
+    hipStream_t st = S(stream);
+    const uintptr_t p = (uintptr_t)pmf_dev;
+    if (c->pmf_bits == 32) {
+        const bool vec = (p % 16 == 0) && c->V % 4 == 0 && step_stride % 4 == 0 && stream_stride % 4 == 0;
+        return vec ? encode_impl<uint32_t, 4>(c, (const uint32_t *)pmf_dev, step_stride, stream_stride, sym_dev, steps,
+                                              trace_dev, st, flags)
+                   : encode_impl<uint32_t, 1>(c, (const uint32_t *)pmf_dev, step_stride, stream_stride, sym_dev, steps,
+                                              trace_dev, st, flags);
+    }
+    const bool vec = (p % 16 == 0) && c->V % 2 == 0 && step_stride % 2 == 0 && stream_stride % 2 == 0;
+    return vec ? encode_impl<uint64_t, 2>(c, (const uint64_t *)pmf_dev, step_stride, stream_stride, sym_dev, steps,
+                                          trace_dev, st, flags)
+               : encode_impl<uint64_t, 1>(c, (const uint64_t *)pmf_dev, step_stride, stream_stride, sym_dev, steps,
+                                          trace_dev, st, flags);
 }
 
 template <typename E, int VEC, int G>
@@ -808,25 +936,30 @@ int lac_encode_reset(lac_ctx *c, void *stream) {
 
 int lac_encode(lac_ctx *c, const void *pmf_dev, int64_t step_stride, int64_t stream_stride, const int32_t *sym_dev,
                int64_t steps, uint64_t *trace_dev, void *stream) {
-    if (!c || !pmf_dev || !sym_dev) return fail(LAC_E_ARG, "NULL argument");
-    if (steps < 0 || step_stride < 0 || stream_stride < 0) return fail(LAC_E_ARG, "negative size/stride");
-    if (steps == 0) return LAC_OK;
-    if (c->mode != 0) return fail(LAC_E_STATE, "context is decoding; call lac_encode_reset first");
-    HIPCHK(hipSetDevice(c->device));
-    hipStream_t st = S(stream);
-    const uintptr_t p = (uintptr_t)pmf_dev;
-    if (c->pmf_bits == 32) {
-        const bool vec = (p % 16 == 0) && c->V % 4 == 0 && step_stride % 4 == 0 && stream_stride % 4 == 0;
-        return vec ? encode_impl<uint32_t, 4>(c, (const uint32_t *)pmf_dev, step_stride, stream_stride, sym_dev, steps,
-                                              trace_dev, st)
-                   : encode_impl<uint32_t, 1>(c, (const uint32_t *)pmf_dev, step_stride, stream_stride, sym_dev, steps,
-                                              trace_dev, st);
+    if (c && c->mode != 0) return fail(LAC_E_STATE, "context is decoding; call lac_encode_reset first");
+    return encode_dispatch(c, pmf_dev, step_stride, stream_stride, sym_dev, steps, trace_dev, stream, 0);
+}
+
+int lac_encode_job(lac_ctx *c, const void *pmf_dev, int64_t step_stride, int64_t stream_stride,
+                   const int32_t *sym_dev, int64_t steps, uint64_t *trace_dev, void *stream) {
+    return encode_dispatch(c, pmf_dev, step_stride, stream_stride, sym_dev, steps, trace_dev, stream,
+                           kReset | kFinish);
+}
+
+int lac_set_option(lac_ctx *c, int option, int64_t value) {
+    if (!c) return fail(LAC_E_ARG, "ctx is NULL");
+    switch (option) {
+    case LAC_OPT_ENCODE_PATH:
+        if (value < LAC_PATH_AUTO || value > LAC_PATH_FUSED) return fail(LAC_E_ARG, "bad encode path %lld", (long long)value);
+        c->path = (int)value;
+        return LAC_OK;
+    case LAC_OPT_FUSED_MIN_STREAMS:
+        if (value < 1) return fail(LAC_E_ARG, "fused_min_streams must be >= 1");
+        c->fused_min_streams = value;
+        return LAC_OK;
+    default:
+        return fail(LAC_E_ARG, "unknown option %d", option);
     }
-    const bool vec = (p % 16 == 0) && c->V % 2 == 0 && step_stride % 2 == 0 && stream_stride % 2 == 0;
-    return vec ? encode_impl<uint64_t, 2>(c, (const uint64_t *)pmf_dev, step_stride, stream_stride, sym_dev, steps,
-                                          trace_dev, st)
-               : encode_impl<uint64_t, 1>(c, (const uint64_t *)pmf_dev, step_stride, stream_stride, sym_dev, steps,
-                                          trace_dev, st);
 }
 
 int lac_encode_finish(lac_ctx *c, void *stream) {
@@ -984,8 +1117,8 @@ int lac_profile_enable(lac_ctx *c, int on) {
 int lac_profile_read(lac_ctx *c, double *ms_total, int64_t *launches, int reset) {
     if (!c) return fail(LAC_E_ARG, "ctx is NULL");
     HIPCHK(hipSetDevice(c->device));
-    double tot[KID_COUNT] = {0, 0, 0, 0};
-    int64_t cnt[KID_COUNT] = {0, 0, 0, 0};
+    double tot[KID_COUNT] = {0};
+    int64_t cnt[KID_COUNT] = {0};
     for (auto &u : c->ev_used) {
         HIPCHK(hipEventSynchronize(u.second.second));
         float ms = 0;

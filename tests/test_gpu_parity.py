@@ -35,15 +35,19 @@ def _dev_pmf(a):
     return torch.from_numpy(view).to(DEV)
 
 
-def _gpu_encode(pmf_np, sym_np, prec, trace=False):
+def _gpu_encode(pmf_np, sym_np, prec, trace=False, path="auto", job=False):
     steps, B, V = pmf_np.shape
     bits = 64 if pmf_np.dtype == np.uint64 else 32
     c = _coder(V, B, prec, bits, cap=steps * (prec + 2) + 256)
+    c.set_path(path)
     pmf = _dev_pmf(pmf_np)
     sym = torch.from_numpy(np.ascontiguousarray(sym_np, dtype=np.int32)).to(DEV)
     tr = torch.zeros((steps, B, 2), dtype=torch.int64, device=DEV) if trace else None
-    c.encode(pmf, sym, trace=tr)
-    c.finish()
+    if job:
+        c.encode_job(pmf, sym, trace=tr)
+    else:
+        c.encode(pmf, sym, trace=tr)
+        c.finish()
     data, n = c.to_bytes()
     return c, pmf, data, n, tr
 
@@ -55,13 +59,14 @@ def _digits_from_trace(tr, b):
 
 
 # ---------------------------------------------------------------- golden vectors
+@pytest.mark.parametrize("path", ["split", "fused"])
 @pytest.mark.parametrize("case", load_golden("gen_cases.json"), ids=lambda c: c["name"])
-def test_golden_gen_case(case):
+def test_golden_gen_case(case, path):
     rows = np.stack([synth.pmf_row(case["seed"], t, 0, case["V"], case["kind"], case["exp_range"])
                      for t in range(case["steps"])])
     pmf = rows[:, None, :]
     sym = np.asarray(case["syms"], dtype=np.int32)[:, None]
-    c, dpmf, data, n, tr = _gpu_encode(pmf, sym, case["prec"], trace=True)
+    c, dpmf, data, n, tr = _gpu_encode(pmf, sym, case["prec"], trace=True, path=path)
     assert int(n[0]) == case["L"] and data[0].hex() == case["bytes"]
     assert _digits_from_trace(tr, 0) == case["trace"]
     assert c.flush_digits()[0] == case["flush"]
@@ -71,7 +76,8 @@ def test_golden_gen_case(case):
     c.raise_on_error()
 
 
-def test_golden_small_cases():
+@pytest.mark.parametrize("path", ["split", "fused"])
+def test_golden_small_cases(path):
     for kind in ("static", "perstep"):
         for c in load_golden("small_cases.json")[kind]:
             if not c["syms"]:
@@ -79,7 +85,8 @@ def test_golden_small_cases():
             T = len(c["syms"])
             rows = np.array(c["rows"], dtype=np.uint32)
             rows = rows if rows.shape[0] == T else np.repeat(rows[:1], T, axis=0)
-            cd, dpmf, data, n, tr = _gpu_encode(rows[:, None, :], np.array(c["syms"])[:, None], c["prec"], trace=True)
+            cd, dpmf, data, n, tr = _gpu_encode(rows[:, None, :], np.array(c["syms"])[:, None], c["prec"], trace=True,
+                                                path=path)
             assert int(n[0]) == c["L"] and data[0].hex() == c["bytes"], c
             assert _digits_from_trace(tr, 0) == c["trace"]
             assert cd.flush_digits()[0] == c["flush"]
@@ -119,11 +126,12 @@ BATCH_CASES = [
 ]
 
 
+@pytest.mark.parametrize("path,job", [("split", False), ("fused", False), ("fused", True), ("split", True)])
 @pytest.mark.parametrize("V,B,steps,prec,kind", BATCH_CASES)
-def test_batch_vs_oracle(V, B, steps, prec, kind):
+def test_batch_vs_oracle(V, B, steps, prec, kind, path, job):
     from oracle import oracle as coracle
     pmf, sym = synth.make_batch(1000 + V + prec, steps, B, V, kind)
-    c, dpmf, data, n, tr = _gpu_encode(pmf, sym, prec)
+    c, dpmf, data, n, tr = _gpu_encode(pmf, sym, prec, path=path, job=job)
     out, nb, status, rc = coracle.encode_batch(pmf, sym, prec, nthreads=16)
     assert rc == 0
     for b in range(B):
@@ -174,9 +182,14 @@ def test_headline_shape_softmax_tables():
     V, B, steps, prec = 32000, 4096, 3, 48
     pmf, sym = synth.softmax_tables(steps, B, V, seed=1234, device=DEV)
     c = _coder(V, B, prec, cap=steps * (prec + 2) + 256)
-    c.encode(pmf, sym)
-    c.finish()
+    c.encode_job(pmf, sym)                 # AUTO: fused kernel at 4096 streams
     data, n = c.to_bytes()
+    c2 = _coder(V, B, prec, cap=steps * (prec + 2) + 256)
+    c2.set_path("split")
+    c2.encode(pmf, sym)
+    c2.finish()
+    assert c2.to_bytes()[0] == data
+    c2.close()
     sample = list(range(0, B, 97)) + [B - 1]
     sub = pmf[:, sample, :].cpu().numpy().view(np.uint32)
     out, nb, status, rc = coracle.encode_batch(sub, sym[:, sample].cpu().numpy(), prec, nthreads=16)
@@ -193,35 +206,41 @@ def test_headline_shape_softmax_tables():
 
 
 # ---------------------------------------------------------------- errors
-def test_error_symbol_range():
+@pytest.mark.parametrize("path", ["split", "fused"])
+def test_error_symbol_range(path):
     V, B = 16, 4
     pmf = torch.ones((2, B, V), dtype=torch.int32, device=DEV)
     sym = torch.zeros((2, B), dtype=torch.int32, device=DEV)
     sym[1, 2] = V          # AssertionError('unknown symbol', V) in the reference
     sym[0, 3] = -1
     c = _coder(V, B, 16)
+    c.set_path(path)
     c.encode(pmf, sym)
     rc, err, step = c.status()
     assert rc != 0
     assert err.tolist() == [0, 0, -3, -3] and step[2] == 1 and step[3] == 0
 
 
-def test_error_zero_width_and_table():
+@pytest.mark.parametrize("path", ["split", "fused"])
+def test_error_zero_width_and_table(path):
     V, B = 8, 3
     pmf = torch.ones((1, B, V), dtype=torch.int32, device=DEV)
     pmf[0, 0, 5] = 0
     pmf[0, 1, :] = 0
     sym = torch.full((1, B), 5, dtype=torch.int32, device=DEV)
     c = _coder(V, B, 16)
+    c.set_path(path)
     c.encode(pmf, sym)
     rc, err, step = c.status()
     assert err.tolist() == [-4, -5, 0]
 
 
-def test_error_capacity():
+@pytest.mark.parametrize("path", ["split", "fused"])
+def test_error_capacity(path):
     V, B, steps = 1000, 2, 200
     pmf, sym = synth.make_batch(9, steps, B, V, "loguniform")
     c = _coder(V, B, 48, cap=128)
+    c.set_path(path)
     c.encode(_dev_pmf(pmf), torch.from_numpy(sym).to(DEV))
     rc, err, step = c.status()
     assert (err == -7).all()
