@@ -64,7 +64,19 @@ enum {
 
 enum {                       /* lac_set_option */
     LAC_OPT_ENCODE_PATH = 1,       /* LAC_PATH_*: which encode kernels run */
-    LAC_OPT_FUSED_MIN_STREAMS = 2  /* AUTO picks the fused kernel from this many streams (2048) */
+    LAC_OPT_FUSED_MIN_STREAMS = 2, /* AUTO picks the fused kernel from this many streams (2048) */
+    LAC_OPT_MAPPING = 3,           /* LAC_MAP_*: how a symbol's CDF range maps onto [l, h] */
+    LAC_OPT_TERMINATION = 4        /* LAC_TERM_*: how a stream is closed */
+};
+enum {
+    LAC_MAP_CEIL = 0,              /* CDFPredictor.symbol_to_range + fudged_dist (arith_code.py:83-110) */
+    LAC_MAP_FLOOR = 1              /* Predictor.symbol_to_range (arith_code.py:69-70) and
+                                      ACSampler's Region.map (arithmetic_coding.py:160-168) */
+};
+enum {
+    LAC_TERM_FLUSH = 0,            /* A_to_bin.flush (arith_code.py:193-202) */
+    LAC_TERM_ACSAMPLER = 1         /* ACSampler.flush_compress: step(1,2,3) + carry flush
+                                      (arithmetic_coding.py:50-56) */
 };
 enum {
     LAC_PATH_AUTO = 0,             /* fused if streams >= fused_min_streams, else split */

@@ -62,6 +62,10 @@ KERNEL_IDS = {"row_stats": 0, "encode": 1, "finish": 2, "decode_step": 3, "encod
 LAC_OPT_ENCODE_PATH = 1
 LAC_OPT_FUSED_MIN_STREAMS = 2
 LAC_PATH_AUTO, LAC_PATH_SPLIT, LAC_PATH_FUSED = 0, 1, 2
+LAC_OPT_MAPPING = 3
+LAC_OPT_TERMINATION = 4
+LAC_MAP_CEIL, LAC_MAP_FLOOR = 0, 1
+LAC_TERM_FLUSH, LAC_TERM_ACSAMPLER = 0, 1
 
 
 class LacLibraryError(RuntimeError):

@@ -152,6 +152,16 @@ class BatchCoder:
         check(self.lib.lac_encode_job(*self._encode_args(pmf, sym, trace)))
         self._finished = True
 
+    def set_mapping(self, mapping):
+        """'ceil' (CDFPredictor, default) or 'floor' (Predictor / ACSampler Region.map)."""
+        v = {"ceil": _lib.LAC_MAP_CEIL, "floor": _lib.LAC_MAP_FLOOR}[mapping]
+        check(self.lib.lac_set_option(self.ctx, _lib.LAC_OPT_MAPPING, v))
+
+    def set_termination(self, term):
+        """'flush' (A_to_bin.flush, default) or 'acsampler' (ACSampler.flush_compress)."""
+        v = {"flush": _lib.LAC_TERM_FLUSH, "acsampler": _lib.LAC_TERM_ACSAMPLER}[term]
+        check(self.lib.lac_set_option(self.ctx, _lib.LAC_OPT_TERMINATION, v))
+
     def set_path(self, path):
         """'auto', 'split' or 'fused' encode kernels (bit-identical results)."""
         v = {"auto": _lib.LAC_PATH_AUTO, "split": _lib.LAC_PATH_SPLIT, "fused": _lib.LAC_PATH_FUSED}[path]

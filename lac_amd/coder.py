@@ -157,13 +157,12 @@ def _row_of(predictor):
 
 
 def _is_uniform(predictor):
-    return getattr(predictor, "dist", None) is None and hasattr(predictor, "n") and \
-        type(predictor).symbol_to_range is Predictor.symbol_to_range or \
-        (type(predictor).__name__ == "Predictor" and hasattr(predictor, "n") and not hasattr(predictor, "dist"))
-
-
-def _uniform_row(n):
-    return np.ones(int(n), dtype=np.uint64)
+    """A table-less Predictor(n) with the base class's floor mapping (arith_code.py:64-74)."""
+    if getattr(predictor, "dist", None) is not None or not hasattr(predictor, "n"):
+        return False
+    stv = getattr(type(predictor), "symbol_to_range", None)
+    return stv is Predictor.symbol_to_range or (type(predictor).__name__ == "Predictor"
+                                                 and type(predictor).__module__ != __name__)
 
 
 def _raise_for(code, sym=None):
@@ -177,16 +176,17 @@ def _raise_for(code, sym=None):
 
 
 class _Tables:
-    """Collects per-step rows from a predictor, calling accept() like the coder does."""
+    """Per-step rows from a predictor.  A uniform Predictor(n) becomes a row of n
+    ones coded with the floor mapping (Predictor.symbol_to_range, :69-70)."""
 
     def __init__(self, predictor):
         self.p = predictor
         self.uniform = _is_uniform(predictor)
-        if self.uniform:
-            raise TypeError("the uniform Predictor uses a floor mapping that the GPU coder does not run; use "
-                            "CDFPredictor(list(range(1, n + 1))) for a uniform table")
+        self.mapping = "floor" if self.uniform else "ceil"
 
     def row(self):
+        if self.uniform:
+            return np.ones(int(self.p.n), dtype=np.uint64)
         return _row_of(self.p)
 
 
@@ -210,10 +210,10 @@ class A_to_bin:
         need = (self.emitted_bits + (steps_hint + 2) * (self.precision + 2) + 256)
         if self._coder is None or self._V != V or self._coder.capacity_bits < need:
             if self._coder is not None and self.emitted_bits:
-                raise RuntimeError("table size changed mid-stream")
-            import torch  # noqa: F401
+                raise RuntimeError("table size or capacity changed mid-stream; use run() for long inputs")
             self._coder = BatchCoder(V, 1, prec=self.precision, pmf_bits=64,
                                      capacity_bits=max(need * 2, 1 << 12))
+            self._coder.set_mapping(_Tables(self.predictor).mapping)
             self._V = V
 
     def _encode_rows(self, rows, syms, trace=True):
@@ -266,9 +266,8 @@ class A_to_bin:
 
     def flush(self):
         if self._coder is None:
-            self._ensure(1 if self._V is None else self._V)
-            if self._V is None:
-                return
+            tab = _Tables(self.predictor)
+            self._ensure(len(tab.row()))
         self._coder.finish()
         rc, err, step = self._coder.status()
         if rc:
@@ -365,6 +364,7 @@ class A_from_bin:
             V = len(row)
             if coder is None:
                 coder = BatchCoder(V, 1, prec=self.precision, pmf_bits=64, capacity_bits=max(nbits, 64) + 64)
+                coder.set_mapping(tab.mapping)
                 stride = ((len(data) + 7) // 8 + 1) * 8
                 buf = np.zeros((1, stride), dtype=np.uint8)
                 buf[0, :len(data)] = np.frombuffer(data, dtype=np.uint8)

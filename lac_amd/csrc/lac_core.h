@@ -92,6 +92,15 @@ __host__ __device__ inline void unfudged_range(uint64_t lo, uint64_t hi, uint64_
     *b = div_ceil((u128)hi * w, T);
 }
 
+// Floor mapping of Predictor.symbol_to_range (arith_code.py:69-70) and of
+// ACSampler's Region.map/step (arithmetic_coding.py:160-168):
+// a = floor(lo*w/T), b = floor(hi*w/T).  No fudge exists on these paths.
+__host__ __device__ inline void floor_range(uint64_t lo, uint64_t hi, uint64_t T, uint64_t w,
+                                            uint64_t *a, uint64_t *b) {
+    *a = lo ? div_floor((u128)lo * w, T) : 0;
+    *b = div_floor((u128)hi * w, T);
+}
+
 // X_j = c_j*w - j*T (signed), the quantity whose prefix max drives the fudge.
 __host__ __device__ inline i128 fudge_x(uint64_t c, int64_t j, uint64_t w, uint64_t T) {
     return (i128)((u128)c * w) - (i128)((u128)(uint64_t)j * T);

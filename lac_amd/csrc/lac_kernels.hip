@@ -238,12 +238,14 @@ __device__ i128 wave_xmax_prefix(const E *row, int64_t n, uint64_t w, uint64_t T
 template <typename E>
 __device__ inline bool coder_step(EncState &st, int64_t &l, int64_t &h, uint64_t lo, uint64_t hi, uint64_t T,
                                   uint64_t minp, int64_t s, const E *row, int64_t V, int prec, uint64_t *pa,
-                                  uint64_t *pc, uint64_t cap_words, uint64_t *trace_slot, int lane) {
+                                  uint64_t *pc, uint64_t cap_words, uint64_t *trace_slot, int lane, int mapping) {
     if (s < 0 || s >= V) { st.err = LAC_E_SYMBOL_RANGE; return false; }   // arith_code.py:100-101
     if (T == 0) { st.err = LAC_E_TABLE; return false; }
     const uint64_t w = (uint64_t)(h - l + 1);
     uint64_t a, bb;
-    if (!is_fudged(T, w, minp)) {
+    if (mapping == LAC_MAP_FLOOR) {
+        floor_range(lo, hi, T, w, &a, &bb);
+    } else if (!is_fudged(T, w, minp)) {
         unfudged_range(lo, hi, T, w, &a, &bb);
     } else {                                                  // CDFPredictor.fudged_dist
         const i128 xprev = s > 0 ? wave_xmax_prefix<E>(row, s, w, T) : kI128Min;
@@ -287,15 +289,31 @@ __host__ __device__ inline EncState fresh_state(int prec) {
 
 // flush (arith_code.py:193-202) + R = A + C + F by a backward big-integer add +
 // big-endian bytes (bits() :227-246, group_bits :336-347), in place.  One lane.
-__device__ inline void finish_stream(EncState &st, uint64_t *pa, const uint64_t *pc, uint64_t cap_words, int prec,
-                                     uint64_t *nbits_slot) {
+__device__ inline void finish_stream(EncState &st, uint64_t *pa, uint64_t *pc, uint64_t cap_words, int prec,
+                                     uint64_t *nbits_slot, int term) {
     if (st.err || st.nflush >= 0) {
         *nbits_slot = st.err ? 0 : st.L;
         return;
     }
     int8_t fd[8];
-    const int m = flush_digits(st.l, st.h, prec, fd);
-    if (m < 0) { st.err = LAC_E_CAPACITY; st.err_step = st.nsym; *nbits_slot = 0; return; }
+    int m = 0;
+    if (term == LAC_TERM_ACSAMPLER) {
+        // ACSampler.flush_compress (arithmetic_coding.py:50-56): Region.step(1, 2, 3)
+        // then the CarryBuffer drains -- one more floor-mapped narrowing, no digits.
+        const int64_t span = st.h - st.l + 1;
+        int64_t l2 = st.l + span / 3, h2 = st.l + (2 * span) / 3 - 1;
+        int k;
+        uint64_t Ev;
+        renorm(l2, h2, prec, &k, &Ev);
+        auto store = [&](uint64_t idx, uint64_t wa, uint64_t wc) { pa[idx] = wa; pc[idx] = wc; };
+        if (!plane_append(st.L, st.wa, st.wc, k, Ev, cap_words, store)) {
+            st.err = LAC_E_CAPACITY; st.err_step = st.nsym; *nbits_slot = 0; return;
+        }
+        if (st.L > 0) { pa[(st.L - 1) >> 6] = st.wa; pc[(st.L - 1) >> 6] = st.wc; }
+    } else {
+        m = flush_digits(st.l, st.h, prec, fd);
+        if (m < 0) { st.err = LAC_E_CAPACITY; st.err_step = st.nsym; *nbits_slot = 0; return; }
+    }
     int64_t F = 0;
     for (int i = 0; i < m; i++) F = F * 2 + fd[i];
     const uint64_t L = st.L, Lf = L + (uint64_t)m;
@@ -352,7 +370,7 @@ __global__ __launch_bounds__(256) void k_encode(const RowStats *__restrict__ sta
                                                 int64_t B, int64_t t0, int nsteps, const E *pmf,
                                                 int64_t step_stride, int64_t stream_stride, int64_t V, int prec,
                                                 EncState *states, uint64_t *planeA, uint64_t *planeC,
-                                                uint64_t cap_words, uint64_t *trace) {
+                                                uint64_t cap_words, uint64_t *trace, int mapping) {
     const int lane = (int)lane_id();
     const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
     if (b >= B) return;
@@ -375,7 +393,7 @@ __global__ __launch_bounds__(256) void k_encode(const RowStats *__restrict__ sta
         const int64_t s = __builtin_amdgcn_readlane(mys, i);
         const E *row = pmf + (t0 + i) * step_stride + b * stream_stride;
         if (!coder_step<E>(st, l, h, lo, hi, T, minp, s, row, V, prec, pa, pc, cap_words,
-                           trace ? trace + 2 * ((t0 + i) * B + b) : nullptr, lane))
+                           trace ? trace + 2 * ((t0 + i) * B + b) : nullptr, lane, mapping))
             break;
     }
     if (lane == 0) store_state(st, l, h, pa, pc, cap_words, &states[b]);
@@ -395,7 +413,8 @@ __global__ __launch_bounds__(256) void k_encode_fused(const E *__restrict__ pmf,
                                                       int64_t stream_stride, const int32_t *__restrict__ sym,
                                                       int64_t B, int64_t t0, int64_t nsteps, int64_t V, int prec,
                                                       EncState *states, uint64_t *planeA, uint64_t *planeC,
-                                                      uint64_t cap_words, uint64_t *trace, uint64_t *nbits, int flags) {
+                                                      uint64_t cap_words, uint64_t *trace, uint64_t *nbits, int flags,
+                                                      int mapping, int term) {
     const int lane = (int)lane_id();
     const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
     if (b >= B) return;
@@ -418,23 +437,24 @@ __global__ __launch_bounds__(256) void k_encode_fused(const E *__restrict__ pmf,
         if (rs.T >> 64) { st.err = LAC_E_TABLE; break; }
         const uint64_t lo = (uint64_t)rs.lo;
         if (!coder_step<E>(st, l, h, lo, lo + rs.ps, (uint64_t)rs.T, rs.minp, s, row, V, prec, pa, pc, cap_words,
-                           trace ? trace + 2 * (t * B + b) : nullptr, lane))
+                           trace ? trace + 2 * (t * B + b) : nullptr, lane, mapping))
             break;
     }
     if (lane == 0) {
         store_state(st, l, h, pa, pc, cap_words, &st);
-        if (flags & kFinish) finish_stream(st, pa, pc, cap_words, prec, &nbits[b]);
+        if (flags & kFinish) finish_stream(st, pa, pc, cap_words, prec, &nbits[b], term);
         states[b] = st;
     }
 }
 
 // ------------------------------------------------------------------ k_finish
-__global__ __launch_bounds__(256) void k_finish(EncState *states, uint64_t *planeA, const uint64_t *planeC,
-                                                uint64_t cap_words, int64_t B, int prec, uint64_t *nbits) {
+__global__ __launch_bounds__(256) void k_finish(EncState *states, uint64_t *planeA, uint64_t *planeC,
+                                                uint64_t cap_words, int64_t B, int prec, uint64_t *nbits, int term) {
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= B) return;
     EncState st = states[b];
-    finish_stream(st, planeA + (uint64_t)b * cap_words, planeC + (uint64_t)b * cap_words, cap_words, prec, &nbits[b]);
+    finish_stream(st, planeA + (uint64_t)b * cap_words, planeC + (uint64_t)b * cap_words, cap_words, prec, &nbits[b],
+                  term);
     states[b] = st;
 }
 
@@ -480,7 +500,7 @@ template <typename E, int VEC, int G>
 __global__ __launch_bounds__(256) void k_decode_step(const E *__restrict__ pmf, int64_t step_off,
                                                      int64_t stream_stride, int64_t V, int prec,
                                                      DecState *states, const uint8_t *bits, uint64_t stride,
-                                                     const uint64_t *nbits, int32_t *sym_out, int64_t B) {
+                                                     const uint64_t *nbits, int32_t *sym_out, int64_t B, int mapping) {
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
     __shared__ uint64_t wmin[kWavesPerBlock];
     __shared__ uint32_t wovf[kWavesPerBlock];
@@ -571,7 +591,7 @@ __global__ __launch_bounds__(256) void k_decode_step(const E *__restrict__ pmf, 
     int64_t s = -1;
     uint64_t a = 0, bb = 0;
     if (x < l || x > h) err = LAC_E_DECODE_RANGE;             // corrupted state / bits
-    if (!err && !is_fudged(T, w, minp)) {
+    if (!err && (mapping == LAC_MAP_FLOOR || !is_fudged(T, w, minp))) {
         const uint64_t tgt = div_floor((u128)v * T, w);          // < T
         // the chunk whose cumulative range holds tgt
         uint64_t run = incl - local;
@@ -613,7 +633,10 @@ __global__ __launch_bounds__(256) void k_decode_step(const E *__restrict__ pmf, 
         lo_c = wave_max_u64(lo_c);
         hi_c = wave_min_u64(hi_c);
         s = cidx * CH + (int64_t)cnt;
-        if (!err) unfudged_range(lo_c, hi_c, T, w, &a, &bb);
+        if (!err) {
+            if (mapping == LAC_MAP_FLOOR) floor_range(lo_c, hi_c, T, w, &a, &bb);
+            else unfudged_range(lo_c, hi_c, T, w, &a, &bb);
+        }
     } else if (!err) {
         // fudged (fudged_dist closed form).  f is strictly increasing and
         // f_e = e + g(Xmax_e) with g monotone, so f_e > v  <=>  some j <= e has
@@ -710,6 +733,8 @@ struct lac_ctx {
     int mode = 0;                       // 0 encode, 1 decode
     int path = LAC_PATH_AUTO;           // encode kernel path (lac_set_option)
     int64_t fused_min_streams = 2048;   // AUTO: fused kernel from this many streams
+    int mapping = LAC_MAP_CEIL;         // symbol_to_range flavour (lac_set_option)
+    int term = LAC_TERM_FLUSH;          // stream termination flavour
     // live kernel timing (lac_profile_enable): hipEvent pairs around launches
     bool prof = false;
     std::vector<hipEvent_t> ev_pool;
@@ -781,7 +806,7 @@ static int encode_impl(lac_ctx *c, const E *pmf, int64_t step_stride, int64_t st
         ProfScope ps(c, KID_FUSED, st);
         k_encode_fused<E, VEC><<<blocks, 64 * kWavesPerBlock, 0, st>>>(
             pmf, step_stride, stream_stride, sym, c->B, 0, steps, c->V, c->prec, c->enc, c->planeA, c->planeC,
-            c->cap_words, trace, c->nbits, flags);
+            c->cap_words, trace, c->nbits, flags, c->mapping, c->term);
         CHECK_LAUNCH();
         return LAC_OK;
     }
@@ -802,14 +827,14 @@ static int encode_impl(lac_ctx *c, const E *pmf, int64_t step_stride, int64_t st
             ProfScope ps(c, KID_ENCODE, st);
             k_encode<E><<<blocks, 64 * kWavesPerBlock, 0, st>>>(c->stats, sym, c->B, t0, n, pmf, step_stride,
                                                                 stream_stride, c->V, c->prec, c->enc, c->planeA,
-                                                                c->planeC, c->cap_words, trace);
+                                                                c->planeC, c->cap_words, trace, c->mapping);
         }
         CHECK_LAUNCH();
     }
     if (flags & kFinish) {
         ProfScope ps(c, KID_FINISH, st);
         k_finish<<<(unsigned)((c->B + 255) / 256), 256, 0, st>>>(c->enc, c->planeA, c->planeC, c->cap_words, c->B,
-                                                                 c->prec, c->nbits);
+                                                                 c->prec, c->nbits, c->term);
         CHECK_LAUNCH();
     }
     return LAC_OK;
@@ -847,7 +872,7 @@ static int decode_launch(lac_ctx *c, const E *pmf, int64_t step_off, int64_t str
     if (lds > 64 * 1024) return fail(LAC_E_ARG, "vocab too large for the decode chunk table");
     ProfScope ps(c, KID_DECODE, st);
     k_decode_step<E, VEC, G><<<(unsigned)c->B, 64 * kWavesPerBlock, lds, st>>>(
-        pmf, step_off, stream_stride, c->V, c->prec, c->dec, c->dbits, c->dstride, c->dnbits, out, c->B);
+        pmf, step_off, stream_stride, c->V, c->prec, c->dec, c->dbits, c->dstride, c->dnbits, out, c->B, c->mapping);
     CHECK_LAUNCH();
     return LAC_OK;
 }
@@ -957,6 +982,14 @@ int lac_set_option(lac_ctx *c, int option, int64_t value) {
         if (value < 1) return fail(LAC_E_ARG, "fused_min_streams must be >= 1");
         c->fused_min_streams = value;
         return LAC_OK;
+    case LAC_OPT_MAPPING:
+        if (value != LAC_MAP_CEIL && value != LAC_MAP_FLOOR) return fail(LAC_E_ARG, "bad mapping");
+        c->mapping = (int)value;
+        return LAC_OK;
+    case LAC_OPT_TERMINATION:
+        if (value != LAC_TERM_FLUSH && value != LAC_TERM_ACSAMPLER) return fail(LAC_E_ARG, "bad termination");
+        c->term = (int)value;
+        return LAC_OK;
     default:
         return fail(LAC_E_ARG, "unknown option %d", option);
     }
@@ -968,7 +1001,7 @@ int lac_encode_finish(lac_ctx *c, void *stream) {
     HIPCHK(hipSetDevice(c->device));
     ProfScope ps(c, KID_FINISH, S(stream));
     k_finish<<<(unsigned)((c->B + 255) / 256), 256, 0, S(stream)>>>(c->enc, c->planeA, c->planeC, c->cap_words, c->B,
-                                                                   c->prec, c->nbits);
+                                                                   c->prec, c->nbits, c->term);
     CHECK_LAUNCH();
     return LAC_OK;
 }

@@ -1,0 +1,158 @@
+"""The reference-shaped API (lac_amd.coder / lac_amd.sampler) on the GPU, against
+vectors the reference produced (tests/golden)."""
+import hashlib
+
+import numpy as np
+import pytest
+
+from conftest import load_golden
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+MISC = load_golden("misc.json")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+def test_ternary_docstring_example():
+    """AC() = uniform ternary Predictor at prec 16 (arith_code.py:15-52, :143-145)."""
+    from lac_amd.coder import AC
+    t = MISC["ternary"]
+    ac = AC()
+    assert list(ac.to_bin.run([1, 1, 2])) == t["digits"]
+    assert list(ac.to_bin.encode([1, 1, 2])) == t["encode"]
+    assert list(ac.to_bin.bits([1, 1, 2])) == t["bits"]
+    assert list(ac.from_bin.run(t["bits"], stop=0, n=3)) == t["decoded"]
+
+
+def test_step_and_call_match_run():
+    from lac_amd.coder import AC, CDFPredictor
+    c = [c for c in load_golden("small_cases.json")["static"] if len(c["syms"]) >= 4][0]
+    ac = AC(CDFPredictor(list(np.cumsum(c["rows"][0]).tolist())), c["prec"])
+    enc = ac.to_bin
+    steps = [enc(s) for s in c["syms"]]
+    assert [list(x) for x in steps] == c["trace"]
+    assert list(enc(None)) == c["flush"]
+
+
+@pytest.mark.parametrize("kind", ["static", "perstep"])
+def test_cdfpredictor_against_golden(kind):
+    """CDFPredictor / Replay-style predictors through AC, for 40 reference cases."""
+    from lac_amd.coder import AC, CDFPredictor, group_bits, measure_compress
+
+    class Replay(CDFPredictor):
+        def __init__(self, rows):
+            self.rows, self.i = rows, 0
+            self._load()
+
+        def _load(self):
+            self.dist = np.cumsum(self.rows[min(self.i, len(self.rows) - 1)]).tolist()
+            self.minp = min(x for x in self.rows[min(self.i, len(self.rows) - 1)] if x > 0)
+
+        def accept(self, s):
+            self.i += 1
+            self._load()
+
+        def copy(self):
+            return Replay(self.rows)
+
+    cases = [c for c in load_golden("small_cases.json")[kind] if c["syms"]][:40]
+    for c in cases:
+        ac = AC(Replay(c["rows"]), c["prec"])
+        R, L = ac.to_bin.encode(c["syms"])
+        assert L == c["L"]
+        data = measure_compress(ac.to_bin, iter(c["syms"]), print_every_inp=0)
+        assert data.hex() == c["bytes"]
+        bits = list(ac.to_bin.bits(c["syms"]))
+        assert bytes(group_bits(iter(bits))).hex() == c["bytes"]
+        assert list(ac.from_bin.run(bits, stop=0, n=len(c["syms"]))) == c["syms"]
+
+
+def test_probpredictor_subclass_adaptive():
+    """An adaptive ProbPredictor (counts of past symbols) round-trips and matches the oracle."""
+    from lac_amd.coder import AC, ProbPredictor
+    from oracle import restate
+
+    class Counts(ProbPredictor):
+        def __init__(self, n, counts=None):
+            super().__init__(n)
+            self.counts = list(counts) if counts else [1] * n
+
+        def prob(self, s):
+            return self.counts[s] * 1000 + 1
+
+        def accept(self, s):
+            self.counts[s] += 1
+            super().accept(s)
+
+        def copy(self):
+            return Counts(self.n, self.counts)
+
+    rng = np.random.default_rng(4)
+    syms = rng.integers(0, 7, 300).tolist()
+    ac = AC(Counts(7), 24)
+    bits = list(ac.to_bin.bits(syms))
+    p = Counts(7)
+    rows = []
+    for s in syms:
+        rows.append([p.prob(i) for i in range(7)])
+        p.accept(s)
+    want, L = restate.encode_bytes(rows, syms, 24)
+    assert len(bits) == L and bytes(restate.group_bits(bits)) == want
+    assert list(ac.from_bin.run(bits, stop=0, n=len(syms))) == syms
+
+
+def test_symbol_range_raises_like_reference():
+    from lac_amd.coder import AC, CDFPredictor
+    ac = AC(CDFPredictor([1, 3, 6, 10]), 16)
+    with pytest.raises(AssertionError) as e:
+        list(ac.to_bin.run([0, 4]))
+    assert e.value.args[0] == "unknown symbol" and e.value.args[1] == 4
+
+
+def test_acsampler_small_sampler_api():
+    """ACSampler(48) loop over np.ones(256), 1000 bytes."""
+    from lac_amd.sampler import ACSampler, packbits
+    k = MISC["acsampler_small"]
+    data = np.random.default_rng(0).integers(0, 256, k["n"], dtype=np.uint8)
+    out = bytearray()
+    s = ACSampler(48)
+    s.compress_tokens = iter(data.tolist())
+    s.compress_output = packbits(out.append)
+
+    def done():
+        s.on_compress_done = None
+        s.flush_compress()
+        s.compress_output.flush()
+        s.compress_output = None
+    s.on_compress_done = done
+    while not s.compress_done:
+        s.sample(np.ones(256))
+    assert bytes(out).hex() == k["out_hex"]
+
+
+def test_acsampler_nonuniform_golden():
+    from lac_amd.sampler import encode_acsampler
+    for c in MISC["acsampler_nonuniform"]:
+        cdf = np.array(c["cdf"], dtype=np.uint64)
+        pmf = np.concatenate([cdf[:1], np.diff(cdf)])
+        bits = encode_acsampler([pmf] * len(c["tokens"]), c["tokens"], 48)
+        assert "".join(map(str, bits)) == c["bits"]
+
+
+def test_kat2_acsampler_gpu():
+    """KAT-2: ACSampler uniform-256 encode of 1 MiB = input || 0x00 (reference-verified hash)."""
+    from lac_amd.sampler import encode_acsampler
+    from oracle import restate
+    kat = load_golden("kat.json")["kat2"]
+    data = np.random.default_rng(0).integers(0, 256, kat["n"], dtype=np.uint8)
+    cdf = restate.acsampler_cdf(np.ones(256))
+    pmf = np.concatenate([cdf[:1], np.diff(cdf)]).astype(np.uint64)
+    bits = encode_acsampler([pmf] * kat["n"], data.tolist(), 48)
+    out = bytes(restate.group_bits(bits))
+    assert len(out) == kat["out_len"] and hashlib.sha256(out).hexdigest() == kat["out_sha256"]
