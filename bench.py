@@ -64,6 +64,8 @@ def main():
     ap.add_argument("--path", default="auto", choices=("auto", "split", "fused"), help="encode kernel path")
     args = ap.parse_args()
 
+    import ctypes as C
+
     import numpy as np
     import torch
 
@@ -121,7 +123,6 @@ def main():
         tt = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
-    import ctypes as C
     ms = (C.c_double * 8)()
     cnt = (C.c_int64 * 8)()
     coder.lib.lac_profile_read(coder.ctx, C.cast(ms, C.c_void_p), C.cast(cnt, C.c_void_p), 1)
@@ -130,7 +131,24 @@ def main():
     rc, err, err_step = coder.status()
     data, nbits = coder.to_bytes() if rc == 0 else ([], None)
     coder.decode_open()
+    dec = coder.decode(pmf)                                # warm
+    torch.cuda.synchronize()
+    coder.lib.lac_profile_read(coder.ctx, None, None, 1)
+    coder.lib.lac_profile_enable(coder.ctx, 1)
+    d0 = time.perf_counter()
+    coder.decode_open()
     dec = coder.decode(pmf)
+    torch.cuda.synchronize()
+    d1 = time.perf_counter()
+    coder.lib.lac_profile_enable(coder.ctx, 0)
+    dms = (C.c_double * 8)()
+    dcnt = (C.c_int64 * 8)()
+    coder.lib.lac_profile_read(coder.ctx, C.cast(dms, C.c_void_p), C.cast(dcnt, C.c_void_p), 1)
+    dkid = 5 if dcnt[5] else 3                            # decode_wave (one launch per call) or decode_step
+    dstep_ms = dms[dkid] / (T if dkid == 5 else max(dcnt[dkid], 1))
+    decode_info = {"symbols_per_s": B * T / (d1 - d0), "kernel": "k_decode_wave" if dkid == 5 else "k_decode_step",
+                   "kernel_ms_per_step": dstep_ms,
+                   "achieved_GBps": B * (V * ebytes + 4) / (dstep_ms * 1e-3) / 1e9 if dcnt[dkid] else None}
     round_trip = bool(torch.equal(dec, sym)) and rc == 0
     if dist:
         ok = torch.tensor([1 if round_trip else 0], device=dev)
@@ -138,7 +156,7 @@ def main():
         round_trip = bool(ok.item())
 
     cpu = None
-    parity = {"round_trip_all_streams": round_trip, "stream_status_ok": rc == 0}
+    parity = {"round_trip_all_streams": round_trip, "stream_status_ok": rc == 0, "decode": decode_info}
     if rank == 0:
         from oracle import oracle as coracle
         S = B if (args.cpu_streams <= 0 or args.cpu_streams > B) else args.cpu_streams
@@ -164,7 +182,7 @@ def main():
     if rank == 0:
         kid = 4 if cnt[4] else 0                            # encode_fused, else row_stats
         kname = "k_encode_fused" if kid == 4 else "k_row_stats"
-        units = T * B                                       # symbols per launch (split path: T <= 64)
+        units = T * B * args.steps / max(cnt[kid], 1)       # symbols per launch of that kernel
         rs_launch_ms = ms[kid] / max(cnt[kid], 1)
         alg_bytes = units * (V * ebytes + 4)
         achieved = alg_bytes / (rs_launch_ms * 1e-3) / 1e9 if cnt[kid] else None

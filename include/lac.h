@@ -66,7 +66,10 @@ enum {                       /* lac_set_option */
     LAC_OPT_ENCODE_PATH = 1,       /* LAC_PATH_*: which encode kernels run */
     LAC_OPT_FUSED_MIN_STREAMS = 2, /* AUTO picks the fused kernel from this many streams (2048) */
     LAC_OPT_MAPPING = 3,           /* LAC_MAP_*: how a symbol's CDF range maps onto [l, h] */
-    LAC_OPT_TERMINATION = 4        /* LAC_TERM_*: how a stream is closed */
+    LAC_OPT_TERMINATION = 4,       /* LAC_TERM_*: how a stream is closed */
+    LAC_OPT_DECODE_PATH = 5        /* LAC_PATH_*: SPLIT = one 4-wave workgroup per stream and step,
+                                      FUSED = one wave per stream, all steps of a call in one launch;
+                                      AUTO = FUSED from 1024 streams */
 };
 enum {
     LAC_MAP_CEIL = 0,              /* CDFPredictor.symbol_to_range + fudged_dist (arith_code.py:83-110) */
@@ -167,10 +170,15 @@ int lac_decode_step(lac_ctx *ctx, const void *pmf_dev, int64_t stream_stride,
 int lac_decode_steps(lac_ctx *ctx, const void *pmf_dev, int64_t step_stride, int64_t stream_stride,
                      int64_t steps, int32_t *sym_out_dev, void *stream);
 
+/* Synchronise; ndet_host[streams] = how many leading decoded symbols the
+ * available bits determine, i.e. how many symbols the reference's bit-serial
+ * A_from_bin.run(bits, stop=0) emits (arith_code.py:268-299, :322-326). */
+int lac_decode_determined(lac_ctx *ctx, int64_t *ndet_host, void *stream);
+
 /* Live kernel timing: with profiling on, every kernel launch is bracketed by
  * hipEvents recorded on its own stream.  lac_profile_read synchronises and
  * returns, per kernel id (0 row_stats, 1 encode, 2 finish, 3 decode_step,
- * 4 encode_fused; 8 slots), the summed device milliseconds and the launch
+ * 4 encode_fused, 5 decode_wave; 8 slots), the summed device milliseconds and the launch
  * count; reset != 0 clears. */
 int lac_profile_enable(lac_ctx *ctx, int on);
 int lac_profile_read(lac_ctx *ctx, double *ms_total /*[8]*/, int64_t *launches /*[8]*/, int reset);

@@ -11,7 +11,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liblac.so")
+LIB_PATH = os.environ.get("LAC_LIB") or os.path.join(HERE, "liblac.so")   # LAC_LIB: tuning variants only
 
 LAC_OK = 0
 LAC_E_ARG = -1
@@ -54,16 +54,18 @@ PROTOTYPES = [
     ("lac_decode_open", _i, [_vp, _vp, _u64, _vp, _vp]),
     ("lac_decode_step", _i, [_vp, _vp, _i64, _vp, _vp]),
     ("lac_decode_steps", _i, [_vp, _vp, _i64, _i64, _i64, _vp, _vp]),
+    ("lac_decode_determined", _i, [_vp, _vp, _vp]),
     ("lac_profile_enable", _i, [_vp, _i]),
     ("lac_profile_read", _i, [_vp, _vp, _vp, _i]),
 ]
 
-KERNEL_IDS = {"row_stats": 0, "encode": 1, "finish": 2, "decode_step": 3, "encode_fused": 4}
+KERNEL_IDS = {"row_stats": 0, "encode": 1, "finish": 2, "decode_step": 3, "encode_fused": 4, "decode_wave": 5}
 LAC_OPT_ENCODE_PATH = 1
 LAC_OPT_FUSED_MIN_STREAMS = 2
 LAC_PATH_AUTO, LAC_PATH_SPLIT, LAC_PATH_FUSED = 0, 1, 2
 LAC_OPT_MAPPING = 3
 LAC_OPT_TERMINATION = 4
+LAC_OPT_DECODE_PATH = 5
 LAC_MAP_CEIL, LAC_MAP_FLOOR = 0, 1
 LAC_TERM_FLUSH, LAC_TERM_ACSAMPLER = 0, 1
 

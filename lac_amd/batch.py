@@ -162,6 +162,11 @@ class BatchCoder:
         v = {"flush": _lib.LAC_TERM_FLUSH, "acsampler": _lib.LAC_TERM_ACSAMPLER}[term]
         check(self.lib.lac_set_option(self.ctx, _lib.LAC_OPT_TERMINATION, v))
 
+    def set_decode_path(self, path):
+        """'auto', 'split' (one workgroup per stream per step) or 'fused' (one wave per stream, one launch)."""
+        v = {"auto": _lib.LAC_PATH_AUTO, "split": _lib.LAC_PATH_SPLIT, "fused": _lib.LAC_PATH_FUSED}[path]
+        check(self.lib.lac_set_option(self.ctx, _lib.LAC_OPT_DECODE_PATH, v))
+
     def set_path(self, path):
         """'auto', 'split' or 'fused' encode kernels (bit-identical results)."""
         v = {"auto": _lib.LAC_PATH_AUTO, "split": _lib.LAC_PATH_SPLIT, "fused": _lib.LAC_PATH_FUSED}[path]
@@ -247,6 +252,13 @@ class BatchCoder:
         self._dec_keep = (bits, nbits)                        # borrowed by the library
         check(self.lib.lac_decode_open(self.ctx, C.c_void_p(bits.data_ptr()), bits.stride(0),
                                        C.c_void_p(nbits.data_ptr()), self._stream))
+
+    def determined(self):
+        """Per stream: leading decoded symbols fixed by the available bits (the
+        count the reference's A_from_bin.run(bits, stop=0) emits)."""
+        n = np.zeros(self.streams, dtype=np.int64)
+        check(self.lib.lac_decode_determined(self.ctx, n.ctypes.data_as(C.c_void_p), self._stream))
+        return n
 
     def decode(self, pmf, out=None):
         """Decode one symbol per stream per step; pmf as in :meth:`encode`."""

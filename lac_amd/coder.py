@@ -341,25 +341,34 @@ class A_from_bin:
         self.denom = 1 << prec
         self.decision = 1 << (prec - 1)
 
-    def run(self, bits, stop=1, n=None):
-        if n is None:
-            raise TypeError("A_from_bin.run needs n= (the symbol count): lac bitstreams do not store it")
+    def run(self, bits, stop=1, n=None, max_symbols=1 << 24):
+        """Decode ``bits`` (an iterable of 0/1).
+
+        With ``n`` given: exactly n symbols (reads zero bits past the end).
+        Without: every symbol the bits determine -- the count the reference's
+        bit-serial ``run(bits, stop=0)`` emits (arith_code.py:268-299, 322-326).
+        ``stop=1`` does not run the reference's heuristic flush (:300-317),
+        which raises on about a fifth of valid streams (SURVEY.md finding 5).
+        """
         bl = [int(b) for b in bits]
         data = bytes(group_bits(iter(bl)))
-        return iter(self._decode_bytes(data, len(bl), n))
+        return iter(self._decode_bytes(data, len(bl), n, max_symbols))
+
+    def step(self, bit):
+        raise NotImplementedError("bit-at-a-time decoding is not provided; decode whole streams with run()")
 
     def decode(self, bits, length, stop=1, n=None):
-        if n is None:
-            raise TypeError("A_from_bin.decode needs n= (the symbol count)")
+        """A_from_bin.decode(int, length) -- arith_code.py:327-334."""
         bl = [(bits >> (length - 1 - i)) & 1 for i in range(length)]
         return self.run(bl, stop, n)
 
-    def _decode_bytes(self, data, nbits, n):
+    def _decode_bytes(self, data, nbits, n, max_symbols=1 << 24):
         import torch
         tab = _Tables(self.predictor)
         out = []
         coder = None
-        for i in range(n):
+        limit = n if n is not None else max_symbols
+        for i in range(limit):
             row = tab.row()
             V = len(row)
             if coder is None:
@@ -375,7 +384,11 @@ class A_from_bin:
             s = int(coder.decode(pmf).cpu()[0, 0])
             if s < 0:
                 rc, err, step = coder.status()
+                if n is None:
+                    break
                 _raise_for(int(err[0]) or _lib.LAC_E_DECODE_RANGE)
+            if n is None and int(coder.determined()[0]) <= i:
+                break                                   # the bits do not determine symbol i
             out.append(s)
             self.predictor.accept(s)
         if coder is not None:

@@ -47,12 +47,13 @@ struct EncState {          // per stream, persistent across lac_encode calls
 };
 
 struct DecState {
-    int64_t l, h, x;       // registers and the prec-bit value window
+    int64_t l, h, x;       // registers and the prec-bit value window (bits past the end read as 0)
     uint64_t pos;          // next bit to read
     int64_t nsym;
     int32_t err;
-    int32_t pad;
+    int32_t det;           // 1 while every symbol so far was determined by the available bits
     int64_t err_step;
+    int64_t ndet;          // leading symbols A_from_bin.run(bits, stop=0) emits (arith_code.py:268-299)
 };
 
 __host__ __device__ inline int bitlen64(uint64_t x) { return x ? 64 - __builtin_clzll(x) : 0; }

@@ -35,6 +35,15 @@ using namespace lac;
 
 #define LAC_VERSION "lac-mi355x 0.1 (gfx950)"
 
+// Row-scan tuning (tools/tune_encode.sh builds variants): vectors in flight per
+// lane, and nontemporal (read-once) vs default cache policy on the row loads.
+#ifndef LAC_UNROLL
+#define LAC_UNROLL 8
+#endif
+#ifndef LAC_NT
+#define LAC_NT 1
+#endif
+
 namespace {
 
 constexpr int kChunkSteps = 64;       // steps per encode launch pair (= lanes of a wave)
@@ -93,6 +102,12 @@ __device__ inline i128 wave_max_i128(i128 v) {
     for (int m = 32; m >= 1; m >>= 1) { const i128 o = shfl_xor_i128(v, m); v = o > v ? o : v; }
     return v;
 }
+__device__ inline u128 wave_sum_u128(u128 v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1)
+        v += ((u128)shfl_xor_u64((uint64_t)(v >> 64), m) << 64) | shfl_xor_u64((uint64_t)v, m);
+    return v;
+}
 __device__ inline uint64_t wave_incl_scan_u64(uint64_t v) {
     const int lane = (int)lane_id();
 #pragma unroll
@@ -111,7 +126,11 @@ template <> struct VecT<uint64_t, 1> { typedef uint64_t type; };
 template <typename E, int VEC>
 __device__ inline typename VecT<E, VEC>::type load_vec(const E *row, int64_t vi) {
     typedef typename VecT<E, VEC>::type V;
+#if LAC_NT
     return __builtin_nontemporal_load(reinterpret_cast<const V *>(row) + vi);
+#else
+    return reinterpret_cast<const V *>(row)[vi];
+#endif
 }
 template <typename E, int VEC>
 __device__ inline E vget(const typename VecT<E, VEC>::type &v, int j) {
@@ -138,7 +157,7 @@ __device__ inline RowSums row_reduce(const E *row, int64_t V, int64_t s) {
     constexpr bool W = sizeof(E) == 8;
     uint64_t tot = 0, lo = 0, tot_h = 0, lo_h = 0, ps = 0;     // *_h: high halves (u64 rows)
     E mn = (E)~(E)0;                                          // min over (x - 1): 0 wraps to max
-    constexpr int U = 8;
+    constexpr int U = LAC_UNROLL;
     auto take = [&](const typename VecT<E, VEC>::type &x, int64_t v) {
         uint64_t sl = 0, sh = 0;
 #pragma unroll
@@ -170,7 +189,14 @@ __device__ inline RowSums row_reduce(const E *row, int64_t V, int64_t s) {
 #pragma unroll
         for (int u = 0; u < U; u++) take(x[u], vi + 64 * u);
     }
-    for (; vi < nvec; vi += 64) take(load_vec<E, VEC>(row, vi), vi);
+    if (vi < nvec) {                      // one predicated tail group; zero vectors add nothing
+        typename VecT<E, VEC>::type x[U];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            x[u] = (vi + 64 * u < nvec) ? load_vec<E, VEC>(row, vi + 64 * u) : (typename VecT<E, VEC>::type)0;
+#pragma unroll
+        for (int u = 0; u < U; u++) take(x[u], vi + 64 * u);
+    }
     RowSums r;
     tot = wave_sum_u64(tot);
     lo = wave_sum_u64(lo);
@@ -492,10 +518,167 @@ __global__ void k_dec_init(DecState *states, int64_t B, int prec, const uint8_t 
     st.x = (int64_t)read_bits(bits + b * stride, nbits[b], 0, prec);
     st.pos = (uint64_t)prec;
     st.err_step = -1;
+    st.det = 1;
+    st.ndet = 0;
     states[b] = st;
 }
 
 // One decode step for every stream: grid = B workgroups of 256 threads.
+// ---- decode building blocks (one wave; all values wave-uniform unless noted)
+
+// Re-scan one chunk (vectors cv0 + 64*g + lane, g < G) from cumulative base cb:
+// count of entries with c_i <= tgt, and the bracketing c_{s-1}, c_s.
+template <typename E, int VEC>
+__device__ inline void scan_chunk(const E *row, int64_t nvec, int64_t cv0, int G, uint64_t cb, uint64_t tgt,
+                                  uint64_t *cnt_out, uint64_t *lo_out, uint64_t *hi_out) {
+    const int lane = (int)lane_id();
+    uint64_t lo_c = cb, hi_c = ~0ull, cnt = 0;
+    for (int g = 0; g < G; g++) {
+        const int64_t vi = cv0 + (int64_t)g * 64 + lane;
+        typename VecT<E, VEC>::type xv;
+        if (vi < nvec) xv = load_vec<E, VEC>(row, vi);
+        else xv = (typename VecT<E, VEC>::type)0;
+        uint64_t loc[VEC], ls = 0;
+#pragma unroll
+        for (int j = 0; j < VEC; j++) { ls += (uint64_t)vget<E, VEC>(xv, j); loc[j] = ls; }
+        const uint64_t in = wave_incl_scan_u64(ls);
+        const uint64_t ex = cb + in - ls;
+#pragma unroll
+        for (int j = 0; j < VEC; j++) {
+            const uint64_t ce = ex + loc[j];
+            const bool valid = vi < nvec;
+            if (valid && ce <= tgt) { cnt++; lo_c = ce > lo_c ? ce : lo_c; }
+            if (valid && ce > tgt) hi_c = ce < hi_c ? ce : hi_c;
+        }
+        cb += readlane_u64(in, 63);
+        if (cb > tgt) break;                                  // later entries all exceed tgt
+    }
+    *cnt_out = wave_sum_u64(cnt);
+    *lo_out = wave_max_u64(lo_c);
+    *hi_out = wave_min_u64(hi_c);
+}
+
+// Fudged val_to_symbol + symbol_to_range (fudged_dist closed form).  f is
+// strictly increasing and f_e = e + g(Xmax_e) with g monotone, so f_e > v  <=>
+// some j <= e has e > v - g(X_j); the first such e is
+//     s = min_j max(j, v + 1 - g(X_j)),
+// a plain min-reduction over the row (no ordered scan of the maxima).
+template <typename E>
+__device__ inline int decode_fudged(const E *row, int64_t V, uint64_t w, uint64_t v, uint64_t T, int64_t *s_out,
+                                    uint64_t *a, uint64_t *bb) {
+    const int lane = (int)lane_id();
+    const uint64_t C = w - (uint64_t)V + 1;
+    uint64_t base = 0;
+    int64_t best = V;
+    constexpr int FV = 4;
+    for (int64_t r0 = 0; r0 < V; r0 += 64 * FV) {
+        E xe[FV];
+        uint64_t ls = 0;
+#pragma unroll
+        for (int j = 0; j < FV; j++) {
+            const int64_t e = r0 + lane * FV + j;
+            xe[j] = e < V ? row[e] : (E)0;
+            ls += (uint64_t)xe[j];
+        }
+        const uint64_t in = wave_incl_scan_u64(ls);
+        uint64_t c = base + in - ls;
+#pragma unroll
+        for (int j = 0; j < FV; j++) {
+            const int64_t e = r0 + lane * FV + j;
+            c += (uint64_t)xe[j];
+            if (e < V) {
+                const i128 X = fudge_x(c, e, w, T);
+                uint64_t g = 1;
+                if (X >= (i128)2 * (i128)T) {
+                    const uint64_t m = div_floor((u128)X, T);
+                    g = m < C ? m : C;
+                }
+                int64_t cand = (int64_t)v + 1 - (int64_t)g;
+                cand = cand > e ? cand : e;
+                best = cand < best ? cand : best;
+            }
+        }
+        base += readlane_u64(in, 63);
+        const int64_t wb = (int64_t)wave_min_u64((uint64_t)best);
+        if (wb < r0 + 64 * FV) break;                      // later j cannot beat it
+    }
+    const int64_t s = (int64_t)wave_min_u64((uint64_t)best);
+    if (s < 0 || s >= V) return LAC_E_DECODE_RANGE;
+    uint64_t cprev = 0;
+    const i128 xprev = s > 0 ? wave_xmax_prefix<E>(row, s, w, T, &cprev) : kI128Min;
+    const i128 xs = fudge_x(cprev + (uint64_t)row[s], s, w, T);
+    *a = s > 0 ? fudge_f(s - 1, xprev, T, w, V) : 0;
+    *bb = fudge_f(s, xs > xprev ? xs : xprev, T, w, V);
+    *s_out = s;
+    return 0;
+}
+
+// Narrow to symbol s and renormalise, pulling k fresh bits into x
+// (emit_symbol + emit_bit, arith_code.py:274-291, value form).
+__device__ inline int decode_advance(DecState &st, uint64_t a, uint64_t bb, const uint8_t *bits, uint64_t nbits,
+                                     int prec) {
+    const int64_t l = st.l, x = st.x;
+    if (!((l + (int64_t)a) <= x && x <= l + (int64_t)bb - 1)) return LAC_E_DECODE_RANGE;  // :277-278
+    int64_t nl = l + (int64_t)a, nh = l + (int64_t)bb - 1;
+    int k;
+    uint64_t Ev;
+    renorm(nl, nh, prec, &k, &Ev);
+    int64_t nx = x;
+    if (k > 0) {
+        const int sh = prec - k;
+        nx = (int64_t)((((uint64_t)x - (Ev << sh)) << k) | read_bits(bits, nbits, st.pos, k));
+        st.pos += (uint64_t)k;
+    }
+    st.l = nl;
+    st.h = nh;
+    st.x = nx;
+    st.nsym++;
+    return 0;
+}
+
+// Everything after the row's totals are known: val_to_symbol + symbol_to_range
+// + advance.  `find_chunk(tgt, &cv0, &G, &cb)` locates the chunk holding tgt.
+template <typename E, int VEC, typename FindChunk>
+__device__ inline int decode_symbol(DecState &st, const E *row, int64_t V, uint64_t T, uint64_t minp, int prec,
+                                    int mapping, const uint8_t *bits, uint64_t nbits, FindChunk find_chunk,
+                                    int64_t *s_out) {
+    const int64_t l = st.l, h = st.h, x = st.x;
+    if (x < l || x > h) return LAC_E_DECODE_RANGE;            // corrupted state / bits
+    const uint64_t w = (uint64_t)(h - l + 1), v = (uint64_t)(x - l);
+    int64_t s = -1;
+    uint64_t a = 0, bb = 0;
+    // The reference decoder holds [lb, hb]: the bits read so far padded with 0s
+    // and with 1s.  x is the 0-padded end; the 1-padded end adds 2^u - 1 where u
+    // counts window bits past the end of the stream.  A symbol is "determined"
+    // (decide_symbol's ls == hs, arith_code.py:268-273) iff both ends map to it.
+    const uint64_t past = st.pos > nbits ? st.pos - nbits : 0;
+    const int u = past < (uint64_t)prec ? (int)past : prec;
+    const uint64_t vhi = v + ((1ull << u) - 1);
+    bool det;
+    if (mapping == LAC_MAP_FLOOR || !is_fudged(T, w, minp)) {
+        const uint64_t tgt = div_floor((u128)v * T, w);       // < T
+        int64_t cv0;
+        int G;
+        uint64_t cb;
+        if (!find_chunk(tgt, &cv0, &G, &cb)) return LAC_E_DECODE_RANGE;
+        uint64_t cnt, lo_c, hi_c;
+        scan_chunk<E, VEC>(row, V / VEC, cv0, G, cb, tgt, &cnt, &lo_c, &hi_c);
+        s = cv0 * VEC + (int64_t)cnt;
+        if (mapping == LAC_MAP_FLOOR) floor_range(lo_c, hi_c, T, w, &a, &bb);
+        else unfudged_range(lo_c, hi_c, T, w, &a, &bb);
+        det = vhi < w && div_floor((u128)vhi * T, w) < hi_c;  // bisect_right(cdf, t_hi) == s
+    } else {
+        const int e = decode_fudged<E>(row, V, w, v, T, &s, &a, &bb);
+        if (e) return e;
+        det = vhi < bb;                                       // f_s > v_hi
+    }
+    if (st.det && det) st.ndet++;
+    else st.det = 0;
+    *s_out = s;
+    return decode_advance(st, a, bb, bits, nbits, prec);
+}
+
+// One decode step for every stream, 4 waves per stream (small stream counts).
 template <typename E, int VEC, int G>
 __global__ __launch_bounds__(256) void k_decode_step(const E *__restrict__ pmf, int64_t step_off,
                                                      int64_t stream_stride, int64_t V, int prec,
@@ -539,7 +722,6 @@ __global__ __launch_bounds__(256) void k_decode_step(const E *__restrict__ pmf, 
                 mn = m1 < mn ? m1 : mn;
             }
         }
-        // chunk total with overflow detection (u64 rows only can overflow)
         uint64_t tsum = ls;
 #pragma unroll
         for (int m = 32; m >= 1; m >>= 1) {
@@ -561,159 +743,136 @@ __global__ __launch_bounds__(256) void k_decode_step(const E *__restrict__ pmf, 
     for (int i = 1; i < kWavesPerBlock; i++) { m0 = wmin[i] < m0 ? wmin[i] : m0; anyovf |= wovf[i]; }
     const int64_t per = (nch + 63) / 64;
     const int64_t c0 = lane * per, c1 = (c0 + per < nch) ? c0 + per : nch;
-    uint64_t local = 0;
-    for (int64_t c = c0; c < c1; c++) {
-        const uint64_t n2 = local + csum[c];
-        anyovf |= n2 < local;
-        local = n2;
-    }
-    const uint64_t incl = wave_incl_scan_u64(local);
-    const uint64_t T = readlane_u64(incl, 63);
-    // total overflow: sum of lane partials wrapped
-    const uint64_t chk = wave_sum_u64(local);
-    uint32_t tovf = (uint32_t)__any(anyovf);
-    {
-        // detect wrap of the cross-lane total: compare u128 sum
-        u128 acc = (u128)local;
-#pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) {
-            const u128 o = ((u128)shfl_xor_u64((uint64_t)(acc >> 64), m) << 64) | shfl_xor_u64((uint64_t)acc, m);
-            acc += o;
-        }
-        tovf |= (uint32_t)((acc >> 64) != 0);
-    }
-    (void)chk;
+    u128 local = 0;
+    for (int64_t c = c0; c < c1; c++) local += csum[c];
+    const u128 tot = wave_sum_u128(local);
+    const uint64_t incl = wave_incl_scan_u64((uint64_t)local);
     int err = 0;
-    if (tovf || T == 0) err = LAC_E_TABLE;
-    const uint64_t minp = m0 + 1;
-    const int64_t l = st.l, h = st.h, x = st.x;
-    const uint64_t w = (uint64_t)(h - l + 1), v = (uint64_t)(x - l);
+    if (__any(anyovf) || (tot >> 64) || tot == 0) err = LAC_E_TABLE;
     int64_t s = -1;
-    uint64_t a = 0, bb = 0;
-    if (x < l || x > h) err = LAC_E_DECODE_RANGE;             // corrupted state / bits
-    if (!err && (mapping == LAC_MAP_FLOOR || !is_fudged(T, w, minp))) {
-        const uint64_t tgt = div_floor((u128)v * T, w);          // < T
-        // the chunk whose cumulative range holds tgt
-        uint64_t run = incl - local;
-        int64_t fc = -1;
-        uint64_t fbase = 0;
-        for (int64_t c = c0; c < c1; c++) {
-            const uint64_t nx = run + csum[c];
-            if (fc < 0 && run <= tgt && tgt < nx) { fc = c; fbase = run; }
-            run = nx;
-        }
-        const uint64_t mask = __ballot(fc >= 0);
-        const int src = mask ? __ffsll((unsigned long long)mask) - 1 : 0;
-        if (!mask) err = LAC_E_DECODE_RANGE;
-        const int64_t cidx = mask ? (int64_t)readlane_u64((uint64_t)fc, src) : 0;
-        uint64_t cb = readlane_u64(fbase, src);
-        uint64_t lo_c = cb, hi_c = ~0ull;
-        uint64_t cnt = 0;
-#pragma unroll
-        for (int g = 0; g < G; g++) {
-            const int64_t vi = cidx * 64 * G + g * 64 + lane;
-            typename VecT<E, VEC>::type xv;
-            if (vi < nvec) xv = load_vec<E, VEC>(row, vi);
-            else xv = (typename VecT<E, VEC>::type)0;
-            uint64_t loc[VEC], ls = 0;
-#pragma unroll
-            for (int j = 0; j < VEC; j++) { ls += (uint64_t)vget<E, VEC>(xv, j); loc[j] = ls; }
-            const uint64_t in = wave_incl_scan_u64(ls);
-            const uint64_t ex = cb + in - ls;
-#pragma unroll
-            for (int j = 0; j < VEC; j++) {
-                const uint64_t ce = ex + loc[j];
-                const bool valid = vi < nvec;
-                if (valid && ce <= tgt) { cnt++; lo_c = ce > lo_c ? ce : lo_c; }
-                if (valid && ce > tgt) hi_c = ce < hi_c ? ce : hi_c;
+    if (!err) {
+        auto find_chunk = [&](uint64_t tgt, int64_t *cv0, int *g, uint64_t *cb) {
+            uint64_t run = incl - (uint64_t)local;
+            int64_t fc = -1;
+            uint64_t fbase = 0;
+            for (int64_t c = c0; c < c1; c++) {
+                const uint64_t nx = run + csum[c];
+                if (fc < 0 && run <= tgt && tgt < nx) { fc = c; fbase = run; }
+                run = nx;
             }
-            cb += readlane_u64(in, 63);
-        }
-        cnt = wave_sum_u64(cnt);
-        lo_c = wave_max_u64(lo_c);
-        hi_c = wave_min_u64(hi_c);
-        s = cidx * CH + (int64_t)cnt;
-        if (!err) {
-            if (mapping == LAC_MAP_FLOOR) floor_range(lo_c, hi_c, T, w, &a, &bb);
-            else unfudged_range(lo_c, hi_c, T, w, &a, &bb);
-        }
-    } else if (!err) {
-        // fudged (fudged_dist closed form).  f is strictly increasing and
-        // f_e = e + g(Xmax_e) with g monotone, so f_e > v  <=>  some j <= e has
-        // e > v - g(X_j); the first such e is  s = min_j max(j, v + 1 - g(X_j)),
-        // a plain min-reduction over the row (no ordered scan of the maxima).
-        const uint64_t C = w - (uint64_t)V + 1;
-        uint64_t base = 0;
-        int64_t best = V;
-        constexpr int FV = 4;
-        for (int64_t r0 = 0; r0 < V; r0 += 64 * FV) {
-            E xe[FV];
-            uint64_t ls = 0;
-#pragma unroll
-            for (int j = 0; j < FV; j++) {
-                const int64_t e = r0 + lane * FV + j;
-                xe[j] = e < V ? row[e] : (E)0;
-                ls += (uint64_t)xe[j];
-            }
-            const uint64_t in = wave_incl_scan_u64(ls);
-            uint64_t c = base + in - ls;
-#pragma unroll
-            for (int j = 0; j < FV; j++) {
-                const int64_t e = r0 + lane * FV + j;
-                c += (uint64_t)xe[j];
-                if (e < V) {
-                    const i128 X = fudge_x(c, e, w, T);
-                    uint64_t g = 1;
-                    if (X >= (i128)2 * (i128)T) {
-                        const uint64_t m = div_floor((u128)X, T);
-                        g = m < C ? m : C;
-                    }
-                    int64_t cand = (int64_t)v + 1 - (int64_t)g;
-                    cand = cand > e ? cand : e;
-                    best = cand < best ? cand : best;
-                }
-            }
-            base += readlane_u64(in, 63);
-            const int64_t wb = (int64_t)wave_min_u64((uint64_t)best);
-            if (wb < r0 + 64 * FV) break;                      // later j cannot beat it
-        }
-        s = (int64_t)wave_min_u64((uint64_t)best);
-        if (s >= 0 && s < V) {
-            uint64_t cprev = 0;
-            const i128 xprev = s > 0 ? wave_xmax_prefix<E>(row, s, w, T, &cprev) : kI128Min;
-            const i128 xs = fudge_x(cprev + (uint64_t)row[s], s, w, T);
-            a = s > 0 ? fudge_f(s - 1, xprev, T, w, V) : 0;
-            bb = fudge_f(s, xs > xprev ? xs : xprev, T, w, V);
-        } else {
-            s = -1;
-        }
-        if (s < 0) err = LAC_E_DECODE_RANGE;
+            const uint64_t mask = __ballot(fc >= 0);
+            if (!mask) return false;
+            const int src = __ffsll((unsigned long long)mask) - 1;
+            *cv0 = (int64_t)readlane_u64((uint64_t)fc, src) * 64 * G;
+            *g = G;
+            *cb = readlane_u64(fbase, src);
+            return true;
+        };
+        err = decode_symbol<E, VEC>(st, row, V, (uint64_t)tot, m0 + 1, prec, mapping, bits + b * stride, nbits[b],
+                                    find_chunk, &s);
     }
-    if (!err && !((int64_t)(l + (int64_t)a) <= x && x <= l + (int64_t)bb - 1)) err = LAC_E_DECODE_RANGE;
     if (lane == 0) {
         if (err) {
             st.err = err;
             st.err_step = st.nsym;
-            sym_out[b] = -1;
-        } else {
-            int64_t nl = l + (int64_t)a, nh = l + (int64_t)bb - 1;
-            int k;
-            uint64_t Ev;
-            renorm(nl, nh, prec, &k, &Ev);
-            int64_t nx = x;
-            if (k > 0) {
-                const int sh = prec - k;
-                nx = (int64_t)((((uint64_t)x - (Ev << sh)) << k) | read_bits(bits + b * stride, nbits[b], st.pos, k));
-                st.pos += (uint64_t)k;
-            }
-            st.l = nl;
-            st.h = nh;
-            st.x = nx;
-            st.nsym++;
-            sym_out[b] = (int32_t)s;
         }
+        sym_out[b] = err ? -1 : (int32_t)s;
         states[b] = st;
     }
+}
+
+// Decode `nsteps` steps of every stream in one launch, one wave per stream
+// (large stream counts).  Pass 1 streams the row (8 x 16-B loads in flight
+// per lane) into <= 64 chunk totals, chunk c's total kept by lane c; the
+// search is a wave scan over lanes; only the chunk holding the target is
+// re-read.  Serial per-stream work is hidden behind the other waves' loads.
+template <typename E, int VEC>
+__global__ __launch_bounds__(256) void k_decode_wave(const E *__restrict__ pmf, int64_t step_stride,
+                                                     int64_t stream_stride, int64_t nsteps, int64_t V, int prec,
+                                                     DecState *states, const uint8_t *bits, uint64_t stride,
+                                                     const uint64_t *nbits, int32_t *sym_out, int64_t B,
+                                                     int mapping) {
+    const int lane = (int)lane_id();
+    const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (b >= B) return;
+    DecState st = states[b];
+    const uint8_t *mybits = bits + b * stride;
+    const uint64_t mynbits = nbits[b];
+    const int64_t nvec = V / VEC, nit = (nvec + 63) / 64;
+    constexpr int U = 8;
+    int64_t CI = (nit + 63) / 64;                             // iterations per chunk: <= 64 chunks
+    CI = ((CI + U - 1) / U) * U;
+    const int64_t nch = (nit + CI - 1) / CI;
+    for (int64_t t = 0; t < nsteps; t++) {
+        int32_t *out = sym_out + t * B + b;
+        if (st.err) {
+            if (lane == 0) *out = -1;
+            continue;
+        }
+        const E *row = pmf + t * step_stride + b * stream_stride;
+        uint64_t mine = 0, mn = ~0ull;
+        uint32_t ovf = 0;
+        for (int64_t c = 0; c < nch; c++) {
+            uint64_t acc = 0;
+            for (int64_t g0 = 0; g0 < CI; g0 += U) {
+                typename VecT<E, VEC>::type x[U];
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const int64_t vi = (c * CI + g0 + u) * 64 + lane;
+                    if (vi < nvec) x[u] = load_vec<E, VEC>(row, vi);
+                    else x[u] = (typename VecT<E, VEC>::type)0;
+                }
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+#pragma unroll
+                    for (int j = 0; j < VEC; j++) {
+                        const uint64_t e = (uint64_t)vget<E, VEC>(x[u], j);
+                        const uint64_t n2 = acc + e;
+                        ovf |= n2 < acc;
+                        acc = n2;
+                        const uint64_t m1 = e - 1;
+                        mn = m1 < mn ? m1 : mn;
+                    }
+                }
+            }
+            uint64_t tsum = acc;
+#pragma unroll
+            for (int m = 32; m >= 1; m >>= 1) {
+                const uint64_t o = shfl_xor_u64(tsum, m);
+                const uint64_t n2 = tsum + o;
+                ovf |= n2 < tsum;
+                tsum = n2;
+            }
+            if (lane == c) mine = tsum;
+        }
+        const uint64_t minp = wave_min_u64(mn) + 1;
+        const uint64_t incl = wave_incl_scan_u64(mine);
+        const u128 acc128 = wave_sum_u128((u128)mine);
+        int err = 0;
+        if (__any(ovf) || (acc128 >> 64) || acc128 == 0) err = LAC_E_TABLE;
+        int64_t s = -1;
+        if (!err) {
+            auto find_chunk = [&](uint64_t tgt, int64_t *cv0, int *g, uint64_t *cb) {
+                const uint64_t ex = incl - mine;
+                const bool hit = lane < nch && ex <= tgt && tgt < incl;
+                const uint64_t mask = __ballot(hit);
+                if (!mask) return false;
+                const int src = __ffsll((unsigned long long)mask) - 1;
+                *cv0 = (int64_t)src * CI * 64;
+                *g = (int)CI;
+                *cb = readlane_u64(ex, src);
+                return true;
+            };
+            err = decode_symbol<E, VEC>(st, row, V, (uint64_t)acc128, minp, prec, mapping, mybits, mynbits,
+                                        find_chunk, &s);
+        }
+        if (err) {
+            st.err = err;
+            st.err_step = st.nsym;
+        }
+        if (lane == 0) *out = err ? -1 : (int32_t)s;
+    }
+    if (lane == 0) states[b] = st;
 }
 
 }  // namespace
@@ -733,6 +892,8 @@ struct lac_ctx {
     int mode = 0;                       // 0 encode, 1 decode
     int path = LAC_PATH_AUTO;           // encode kernel path (lac_set_option)
     int64_t fused_min_streams = 2048;   // AUTO: fused kernel from this many streams
+    int dpath = LAC_PATH_AUTO;          // decode kernel path
+    int64_t wave_decode_min_streams = 1024;
     int mapping = LAC_MAP_CEIL;         // symbol_to_range flavour (lac_set_option)
     int term = LAC_TERM_FLUSH;          // stream termination flavour
     // live kernel timing (lac_profile_enable): hipEvent pairs around launches
@@ -742,7 +903,8 @@ struct lac_ctx {
     size_t ev_next = 0;
 };
 
-enum { KID_ROW_STATS = 0, KID_ENCODE = 1, KID_FINISH = 2, KID_DECODE = 3, KID_FUSED = 4, KID_COUNT = 8 };
+enum { KID_ROW_STATS = 0, KID_ENCODE = 1, KID_FINISH = 2, KID_DECODE = 3, KID_FUSED = 4, KID_DECODE_WAVE = 5,
+       KID_COUNT = 8 };
 
 static hipEvent_t ev_get(lac_ctx *c) {
     if (c->ev_next == c->ev_pool.size()) {
@@ -877,17 +1039,43 @@ static int decode_launch(lac_ctx *c, const E *pmf, int64_t step_off, int64_t str
     return LAC_OK;
 }
 
-static int decode_one(lac_ctx *c, const void *pmf, int64_t step_off, int64_t step_stride, int64_t stream_stride,
-                      int32_t *out, hipStream_t st) {
+template <typename E, int VEC>
+static int decode_wave_launch(lac_ctx *c, const E *pmf, int64_t step_stride, int64_t stream_stride, int64_t steps,
+                              int32_t *out, hipStream_t st) {
+    ProfScope ps(c, KID_DECODE_WAVE, st);
+    k_decode_wave<E, VEC><<<(unsigned)((c->B + kWavesPerBlock - 1) / kWavesPerBlock), 64 * kWavesPerBlock, 0, st>>>(
+        pmf, step_stride, stream_stride, steps, c->V, c->prec, c->dec, c->dbits, c->dstride, c->dnbits, out, c->B,
+        c->mapping);
+    CHECK_LAUNCH();
+    return LAC_OK;
+}
+
+static int decode_dispatch(lac_ctx *c, const void *pmf, int64_t step_stride, int64_t stream_stride, int64_t steps,
+                           int32_t *out, hipStream_t st) {
     const uintptr_t p = (uintptr_t)pmf;
-    if (c->pmf_bits == 32) {
-        const bool vec = (p % 16 == 0) && c->V % 4 == 0 && step_stride % 4 == 0 && stream_stride % 4 == 0;
-        if (vec) return decode_launch<uint32_t, 4, 2>(c, (const uint32_t *)pmf, step_off, stream_stride, out, st);
-        return decode_launch<uint32_t, 1, 8>(c, (const uint32_t *)pmf, step_off, stream_stride, out, st);
+    const bool wave = c->dpath == LAC_PATH_FUSED || (c->dpath == LAC_PATH_AUTO && c->B >= c->wave_decode_min_streams);
+    const int vw = c->pmf_bits == 32 ? 4 : 2;
+    const bool vec = (p % 16 == 0) && c->V % vw == 0 && step_stride % vw == 0 && stream_stride % vw == 0;
+    if (wave) {
+        if (c->pmf_bits == 32)
+            return vec ? decode_wave_launch<uint32_t, 4>(c, (const uint32_t *)pmf, step_stride, stream_stride, steps, out, st)
+                       : decode_wave_launch<uint32_t, 1>(c, (const uint32_t *)pmf, step_stride, stream_stride, steps, out, st);
+        return vec ? decode_wave_launch<uint64_t, 2>(c, (const uint64_t *)pmf, step_stride, stream_stride, steps, out, st)
+                   : decode_wave_launch<uint64_t, 1>(c, (const uint64_t *)pmf, step_stride, stream_stride, steps, out, st);
     }
-    const bool vec = (p % 16 == 0) && c->V % 2 == 0 && step_stride % 2 == 0 && stream_stride % 2 == 0;
-    if (vec) return decode_launch<uint64_t, 2, 4>(c, (const uint64_t *)pmf, step_off, stream_stride, out, st);
-    return decode_launch<uint64_t, 1, 8>(c, (const uint64_t *)pmf, step_off, stream_stride, out, st);
+    for (int64_t t = 0; t < steps; t++) {
+        const int64_t off = t * step_stride;
+        int32_t *o = out + t * c->B;
+        int rc;
+        if (c->pmf_bits == 32)
+            rc = vec ? decode_launch<uint32_t, 4, 2>(c, (const uint32_t *)pmf, off, stream_stride, o, st)
+                     : decode_launch<uint32_t, 1, 8>(c, (const uint32_t *)pmf, off, stream_stride, o, st);
+        else
+            rc = vec ? decode_launch<uint64_t, 2, 4>(c, (const uint64_t *)pmf, off, stream_stride, o, st)
+                     : decode_launch<uint64_t, 1, 8>(c, (const uint64_t *)pmf, off, stream_stride, o, st);
+        if (rc) return rc;
+    }
+    return LAC_OK;
 }
 
 extern "C" {
@@ -981,6 +1169,10 @@ int lac_set_option(lac_ctx *c, int option, int64_t value) {
     case LAC_OPT_FUSED_MIN_STREAMS:
         if (value < 1) return fail(LAC_E_ARG, "fused_min_streams must be >= 1");
         c->fused_min_streams = value;
+        return LAC_OK;
+    case LAC_OPT_DECODE_PATH:
+        if (value < LAC_PATH_AUTO || value > LAC_PATH_FUSED) return fail(LAC_E_ARG, "bad decode path");
+        c->dpath = (int)value;
         return LAC_OK;
     case LAC_OPT_MAPPING:
         if (value != LAC_MAP_CEIL && value != LAC_MAP_FLOOR) return fail(LAC_E_ARG, "bad mapping");
@@ -1132,12 +1324,18 @@ int lac_decode_steps(lac_ctx *c, const void *pmf_dev, int64_t step_stride, int64
     if (!c || !pmf_dev || !sym_out_dev) return fail(LAC_E_ARG, "NULL argument");
     if (c->mode != 1) return fail(LAC_E_STATE, "call lac_decode_open first");
     if (steps < 0 || step_stride < 0 || stream_stride < 0) return fail(LAC_E_ARG, "negative size/stride");
+    if (steps == 0) return LAC_OK;
     HIPCHK(hipSetDevice(c->device));
-    for (int64_t t = 0; t < steps; t++) {
-        const int rc = decode_one(c, pmf_dev, t * step_stride, step_stride, stream_stride, sym_out_dev + t * c->B,
-                                  S(stream));
-        if (rc) return rc;
-    }
+    return decode_dispatch(c, pmf_dev, step_stride, stream_stride, steps, sym_out_dev, S(stream));
+}
+
+int lac_decode_determined(lac_ctx *c, int64_t *ndet_host, void *stream) {
+    if (!c || !ndet_host) return fail(LAC_E_ARG, "NULL argument");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(S(stream)));
+    std::vector<DecState> v(c->B);
+    HIPCHK(hipMemcpy(v.data(), c->dec, sizeof(DecState) * c->B, hipMemcpyDeviceToHost));
+    for (int64_t b = 0; b < c->B; b++) ndet_host[b] = v[b].ndet;
     return LAC_OK;
 }
 

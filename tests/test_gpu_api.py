@@ -71,6 +71,8 @@ def test_cdfpredictor_against_golden(kind):
         bits = list(ac.to_bin.bits(c["syms"]))
         assert bytes(group_bits(iter(bits))).hex() == c["bytes"]
         assert list(ac.from_bin.run(bits, stop=0, n=len(c["syms"]))) == c["syms"]
+        # without n: exactly what the reference's bit-serial run(bits, stop=0) emits
+        assert list(ac.from_bin.run(bits, stop=0)) == c["syms"] + c["decoded_extra"]
 
 
 def test_probpredictor_subclass_adaptive():

@@ -52,6 +52,19 @@ def _gpu_encode(pmf_np, sym_np, prec, trace=False, path="auto", job=False):
     return c, pmf, data, n, tr
 
 
+def _decode_both(c, dpmf):
+    """Decode with the per-step workgroup kernel and the one-launch wave kernel;
+    both must agree.  Returns the symbols."""
+    outs = []
+    for path in ("split", "fused"):
+        c.set_decode_path(path)
+        c.decode_open()
+        outs.append(c.decode(dpmf).cpu().numpy())
+    c.set_decode_path("auto")
+    assert (outs[0] == outs[1]).all()
+    return outs[0]
+
+
 def _digits_from_trace(tr, b):
     from lac_amd.batch import digits_of
     t = tr[:, b, :].cpu().numpy()
@@ -70,8 +83,7 @@ def test_golden_gen_case(case, path):
     assert int(n[0]) == case["L"] and data[0].hex() == case["bytes"]
     assert _digits_from_trace(tr, 0) == case["trace"]
     assert c.flush_digits()[0] == case["flush"]
-    c.decode_open()
-    out = c.decode(dpmf).cpu().numpy()[:, 0]
+    out = _decode_both(c, dpmf)[:, 0]
     assert out.tolist() == case["syms"]
     c.raise_on_error()
 
@@ -90,8 +102,7 @@ def test_golden_small_cases(path):
             assert int(n[0]) == c["L"] and data[0].hex() == c["bytes"], c
             assert _digits_from_trace(tr, 0) == c["trace"]
             assert cd.flush_digits()[0] == c["flush"]
-            cd.decode_open()
-            assert cd.decode(dpmf).cpu().numpy()[:, 0].tolist() == c["syms"]
+            assert _decode_both(cd, dpmf)[:, 0].tolist() == c["syms"]
             cd.close()
 
 
@@ -137,8 +148,7 @@ def test_batch_vs_oracle(V, B, steps, prec, kind, path, job):
     for b in range(B):
         assert int(n[b]) == int(nb[b]), b
         assert data[b] == out[b, :(int(nb[b]) + 7) // 8].tobytes(), b
-    c.decode_open()
-    dec = c.decode(dpmf).cpu().numpy()
+    dec = _decode_both(c, dpmf)
     assert (dec == sym).all()
     c.raise_on_error()
 
@@ -155,9 +165,11 @@ def test_decode_external_bits_from_oracle():
     c = _coder(V, B, prec)
     bits = torch.from_numpy(buf).to(DEV)
     nbits = torch.from_numpy(nb.astype(np.int64)).to(DEV)
-    c.decode_open(bits, nbits)
-    dec = c.decode(_dev_pmf(pmf)).cpu().numpy()
-    assert (dec == sym).all()
+    for path in ("split", "fused"):
+        c.set_decode_path(path)
+        c.decode_open(bits, nbits)
+        dec = c.decode(_dev_pmf(pmf)).cpu().numpy()
+        assert (dec == sym).all()
 
 
 def test_incremental_encode_matches_one_shot():
@@ -196,8 +208,10 @@ def test_headline_shape_softmax_tables():
     assert rc == 0
     for i, b in enumerate(sample):
         assert data[b] == out[i, :(int(nb[i]) + 7) // 8].tobytes()
-    c.decode_open()
-    assert torch.equal(c.decode(pmf), sym)
+    for path in ("split", "fused"):
+        c.set_decode_path(path)
+        c.decode_open()
+        assert torch.equal(c.decode(pmf), sym)
     # every stream ends in the group_bits format: padding bits are zero
     for b in range(0, B, 7):
         L = int(n[b])
@@ -252,3 +266,44 @@ def test_open_rejects_bad_prec():
         _coder(300, 1, 8)          # 2^(8-1) < 300: the reference coder hangs
     with pytest.raises(LacError):
         _coder(10, 1, 62)
+
+
+# ---------------------------------------------------------------- run(bits, stop=0) counts
+def _determined_case(rows, syms, extra, count, prec, data, L):
+    """Decode len(syms)+len(extra)+2 steps (rows past the end repeat the last row,
+    as the reference's Replay predictor does) and compare the determined count."""
+    V = len(rows[0])
+    n = len(syms) + len(extra) + 2
+    tab = np.stack([np.asarray(rows[min(i, len(rows) - 1)], dtype=np.uint64) for i in range(n)])
+    stride = ((len(data) + 7) // 8 + 1) * 8
+    buf = np.zeros((1, stride), dtype=np.uint8)
+    buf[0, :len(data)] = np.frombuffer(data, dtype=np.uint8)
+    c = _coder(V, 1, prec, bits=64)
+    out = {}
+    for path in ("split", "fused"):
+        c.set_decode_path(path)
+        c.decode_open(torch.from_numpy(buf).to(DEV), torch.tensor([L], dtype=torch.int64, device=DEV))
+        dec = c.decode(torch.from_numpy(tab.view(np.int64).reshape(n, 1, V)).to(DEV)).cpu().numpy()[:, 0]
+        nd = int(c.determined()[0])
+        assert nd == count, (path, nd, count)
+        assert dec[:count].tolist() == (list(syms) + list(extra))[:count]
+        out[path] = nd
+    c.close()
+    return out
+
+
+def test_determined_count_matches_reference_small():
+    for kind in ("static", "perstep"):
+        for c in load_golden("small_cases.json")[kind]:
+            if not c["syms"] or "decoded_count" not in c:
+                continue
+            _determined_case(c["rows"], c["syms"], c["decoded_extra"], c["decoded_count"], c["prec"],
+                             bytes.fromhex(c["bytes"]), c["L"])
+
+
+@pytest.mark.parametrize("case", [c for c in load_golden("gen_cases.json") if "decoded_count" in c],
+                         ids=lambda c: c["name"])
+def test_determined_count_matches_reference_gen(case):
+    rows = [synth.pmf_row(case["seed"], t, 0, case["V"], case["kind"], case["exp_range"]) for t in range(case["steps"])]
+    _determined_case(rows, case["syms"], case["decoded_extra"], case["decoded_count"], case["prec"],
+                     bytes.fromhex(case["bytes"]), case["L"])

@@ -1,0 +1,32 @@
+#!/bin/bash
+# Build row-scan variants of liblac.so (here) or bench them (on the GPU box):
+#   tools/tune_encode.sh build        -> tools/tune/liblac_<variant>.so
+#   tools/tune_encode.sh run [args]   -> one bench line per variant
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+VARIANTS="u8_nt:-DLAC_UNROLL=8 -DLAC_NT=1 u16_nt:-DLAC_UNROLL=16 -DLAC_NT=1 u8_plain:-DLAC_UNROLL=8 -DLAC_NT=0 u16_plain:-DLAC_UNROLL=16 -DLAC_NT=0 u4_nt:-DLAC_UNROLL=4 -DLAC_NT=1"
+if [ "${1:-}" = build ]; then
+    mkdir -p tools/tune
+    IFS=' '; for v in u8_nt u16_nt u8_plain u16_plain u4_nt; do
+        case $v in
+          u8_nt) f="-DLAC_UNROLL=8 -DLAC_NT=1";; u16_nt) f="-DLAC_UNROLL=16 -DLAC_NT=1";;
+          u8_plain) f="-DLAC_UNROLL=8 -DLAC_NT=0";; u16_plain) f="-DLAC_UNROLL=16 -DLAC_NT=0";;
+          u4_nt) f="-DLAC_UNROLL=4 -DLAC_NT=1";;
+        esac
+        hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Iinclude -Ilac_amd/csrc $f \
+            lac_amd/csrc/lac_kernels.hip -o tools/tune/liblac_$v.so || exit 1
+    done
+    exit 0
+fi
+shift
+mkdir -p gpurun_out/tune
+for rep in 1 2; do
+  for so in tools/tune/liblac_*.so; do
+    v=$(basename "$so" .so)
+    LAC_LIB="$PWD/$so" timeout -k 10 300 python3 bench.py --steps 10 --warmup 3 --cpu-baseline off "$@" \
+        > "gpurun_out/tune/$v.$rep.json" 2> "gpurun_out/tune/$v.$rep.err"
+    rc=$?
+    [ $rc -ne 0 ] && { echo "$v rc=$rc"; tail -5 "gpurun_out/tune/$v.$rep.err"; exit $rc; }
+    python3 -c "import json,sys; d=json.load(open('gpurun_out/tune/$v.$rep.json')); r=d['roofline']; print('$v', round(d['value']/1e6,2), 'Msym/s', r['kernel'], round(r['kernel_ms_per_launch'],4), 'ms', round(r['frac'],4), 'dec', round(d['parity']['decode']['achieved_GBps'] or 0), 'GB/s', d['parity']['bit_exact_vs_oracle'], d['parity']['round_trip_all_streams'])"
+  done
+done
