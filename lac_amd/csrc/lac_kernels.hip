@@ -43,6 +43,25 @@ using namespace lac;
 #ifndef LAC_NT
 #define LAC_NT 1
 #endif
+// Minimum waves per SIMD for the one-wave-per-stream kernels (0 = no bound).
+// With 4096 streams every stream's wave is resident at 4 waves/SIMD; the
+// register cap spills only a few values of the per-step tail, never the row loop.
+#ifndef LAC_ENC_MINW
+#define LAC_ENC_MINW 0
+#endif
+#ifndef LAC_DEC_MINW
+#define LAC_DEC_MINW 4
+#endif
+#if LAC_ENC_MINW > 0
+#define LAC_ENC_BOUNDS __launch_bounds__(256, LAC_ENC_MINW)
+#else
+#define LAC_ENC_BOUNDS __launch_bounds__(256)
+#endif
+#if LAC_DEC_MINW > 0
+#define LAC_DEC_BOUNDS __launch_bounds__(256, LAC_DEC_MINW)
+#else
+#define LAC_DEC_BOUNDS __launch_bounds__(256)
+#endif
 
 namespace {
 
@@ -435,7 +454,7 @@ __global__ __launch_bounds__(256) void k_encode(const RowStats *__restrict__ sta
 enum { kReset = 1, kFinish = 2 };
 
 template <typename E, int VEC>
-__global__ __launch_bounds__(256) void k_encode_fused(const E *__restrict__ pmf, int64_t step_stride,
+__global__ LAC_ENC_BOUNDS void k_encode_fused(const E *__restrict__ pmf, int64_t step_stride,
                                                       int64_t stream_stride, const int32_t *__restrict__ sym,
                                                       int64_t B, int64_t t0, int64_t nsteps, int64_t V, int prec,
                                                       EncState *states, uint64_t *planeA, uint64_t *planeC,
@@ -570,7 +589,7 @@ __device__ inline int decode_fudged(const E *row, int64_t V, uint64_t w, uint64_
     const uint64_t C = w - (uint64_t)V + 1;
     uint64_t base = 0;
     int64_t best = V;
-    constexpr int FV = 4;
+    constexpr int FV = 2;                                   // cold path: keep register pressure low
     for (int64_t r0 = 0; r0 < V; r0 += 64 * FV) {
         E xe[FV];
         uint64_t ls = 0;
@@ -787,7 +806,7 @@ __global__ __launch_bounds__(256) void k_decode_step(const E *__restrict__ pmf, 
 // search is a wave scan over lanes; only the chunk holding the target is
 // re-read.  Serial per-stream work is hidden behind the other waves' loads.
 template <typename E, int VEC>
-__global__ __launch_bounds__(256) void k_decode_wave(const E *__restrict__ pmf, int64_t step_stride,
+__global__ LAC_DEC_BOUNDS void k_decode_wave(const E *__restrict__ pmf, int64_t step_stride,
                                                      int64_t stream_stride, int64_t nsteps, int64_t V, int prec,
                                                      DecState *states, const uint8_t *bits, uint64_t stride,
                                                      const uint64_t *nbits, int32_t *sym_out, int64_t B,
@@ -810,7 +829,8 @@ __global__ __launch_bounds__(256) void k_decode_wave(const E *__restrict__ pmf, 
             continue;
         }
         const E *row = pmf + t * step_stride + b * stream_stride;
-        uint64_t mine = 0, mn = ~0ull;
+        uint64_t mine = 0;
+        E mn = (E)~(E)0;
         uint32_t ovf = 0;
         for (int64_t c = 0; c < nch; c++) {
             uint64_t acc = 0;
@@ -826,26 +846,36 @@ __global__ __launch_bounds__(256) void k_decode_wave(const E *__restrict__ pmf, 
                 for (int u = 0; u < U; u++) {
 #pragma unroll
                     for (int j = 0; j < VEC; j++) {
-                        const uint64_t e = (uint64_t)vget<E, VEC>(x[u], j);
-                        const uint64_t n2 = acc + e;
-                        ovf |= n2 < acc;
-                        acc = n2;
-                        const uint64_t m1 = e - 1;
-                        mn = m1 < mn ? m1 : mn;
+                        const E e = vget<E, VEC>(x[u], j);
+                        if constexpr (sizeof(E) == 8) {       // u64 rows can overflow; u32 chunks cannot
+                            const uint64_t n2 = acc + e;
+                            ovf |= n2 < acc;
+                            acc = n2;
+                        } else {
+                            acc += e;
+                        }
+                        const E m1 = e - 1;
+                        mn = m1 < (E)mn ? m1 : (E)mn;
                     }
                 }
             }
             uint64_t tsum = acc;
+            if constexpr (sizeof(E) == 8) {
 #pragma unroll
-            for (int m = 32; m >= 1; m >>= 1) {
-                const uint64_t o = shfl_xor_u64(tsum, m);
-                const uint64_t n2 = tsum + o;
-                ovf |= n2 < tsum;
-                tsum = n2;
+                for (int m = 32; m >= 1; m >>= 1) {
+                    const uint64_t o = shfl_xor_u64(tsum, m);
+                    const uint64_t n2 = tsum + o;
+                    ovf |= n2 < tsum;
+                    tsum = n2;
+                }
+            } else {
+                tsum = wave_sum_u64(tsum);                    // < 2^32 * 2^31: no overflow
             }
             if (lane == c) mine = tsum;
         }
-        const uint64_t minp = wave_min_u64(mn) + 1;
+        uint64_t minp;
+        if constexpr (sizeof(E) == 8) minp = wave_min_u64(mn) + 1;
+        else minp = (uint64_t)wave_min_u32(mn) + 1;
         const uint64_t incl = wave_incl_scan_u64(mine);
         const u128 acc128 = wave_sum_u128((u128)mine);
         int err = 0;

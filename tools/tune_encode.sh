@@ -4,11 +4,14 @@
 #   tools/tune_encode.sh run [args]   -> one bench line per variant
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-VARIANTS="u8_nt:-DLAC_UNROLL=8 -DLAC_NT=1 u16_nt:-DLAC_UNROLL=16 -DLAC_NT=1 u8_plain:-DLAC_UNROLL=8 -DLAC_NT=0 u16_plain:-DLAC_UNROLL=16 -DLAC_NT=0 u4_nt:-DLAC_UNROLL=4 -DLAC_NT=1"
 if [ "${1:-}" = build ]; then
     mkdir -p tools/tune
-    IFS=' '; for v in u8_nt u16_nt u8_plain u16_plain u4_nt; do
+    rm -f tools/tune/*.so
+    IFS=' '; for v in ${TUNE_VARIANTS:-base enc4 enc3 dec0}; do
         case $v in
+          base) f="";;
+          enc4) f="-DLAC_ENC_MINW=4";; enc3) f="-DLAC_ENC_MINW=3";;
+          dec0) f="-DLAC_DEC_MINW=0";; dec3) f="-DLAC_DEC_MINW=3";;
           u8_nt) f="-DLAC_UNROLL=8 -DLAC_NT=1";; u16_nt) f="-DLAC_UNROLL=16 -DLAC_NT=1";;
           u8_plain) f="-DLAC_UNROLL=8 -DLAC_NT=0";; u16_plain) f="-DLAC_UNROLL=16 -DLAC_NT=0";;
           u4_nt) f="-DLAC_UNROLL=4 -DLAC_NT=1";;
