@@ -158,3 +158,13 @@ def test_kat2_acsampler_gpu():
     bits = encode_acsampler([pmf] * kat["n"], data.tolist(), 48)
     out = bytes(restate.group_bits(bits))
     assert len(out) == kat["out_len"] and hashlib.sha256(out).hexdigest() == kat["out_sha256"]
+
+
+def test_container_compress_decompress_batch():
+    from lac_amd import container, synth
+    from lac_amd.batch import BatchCoder
+    pmf, sym = synth.softmax_tables(6, 300, 2000, seed=7, device="cuda:0")
+    coder = BatchCoder(2000, 300, prec=48, capacity_bits=6 * 50 + 256, device="cuda:0")
+    blob = container.compress_batch(coder, pmf, sym)
+    out, n = container.decompress_batch(blob, pmf)
+    assert n == [6] * 300 and torch.equal(out, sym)
