@@ -142,6 +142,9 @@ ternary = Predictor(3)
 # ------------------------------------------------------------------ tables
 def _row_of(predictor):
     """The predictor's current integer pmf row (numpy uint64) from its CDF."""
+    fast = getattr(predictor, "pmf_row", None)
+    if fast is not None:
+        return np.asarray(fast(), dtype=np.uint64)
     d = getattr(predictor, "dist", None)
     if d is None:
         raise TypeError(f"{type(predictor).__name__} exposes no probability table (.dist); the GPU coder "

@@ -1034,7 +1034,7 @@ static int encode_impl(lac_ctx *c, const E *pmf, int64_t step_stride, int64_t st
 
 static int encode_dispatch(lac_ctx *c, const void *pmf_dev, int64_t step_stride, int64_t stream_stride,
                            const int32_t *sym_dev, int64_t steps, uint64_t *trace_dev, void *stream, int flags) {
-    if (!c || !pmf_dev || !sym_dev) return fail(LAC_E_ARG, "NULL argument");
+    if (!c || (steps > 0 && (!pmf_dev || !sym_dev))) return fail(LAC_E_ARG, "NULL argument");
     if (steps < 0 || step_stride < 0 || stream_stride < 0) return fail(LAC_E_ARG, "negative size/stride");
     if (steps == 0 && !flags) return LAC_OK;
     HIPCHK(hipSetDevice(c->device));

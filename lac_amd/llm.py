@@ -1,0 +1,135 @@
+"""LLM predictors for the GPU coder: the ``Llama_AC`` adapter and a ROCm torch backend.
+
+``Llama_AC`` keeps the surface of /root/reference/llama_compress.py:14-61:
+``reset`` primes the model with BOS (=1), ``accept`` evaluates the accepted token
+and, when the context is full, keeps the last ``n_ctx // overlap`` tokens and
+re-evaluates them; ``calc_dist`` turns the last logits into an integer CDF
+(``max(2, p * 2^60)``, float64, :24-30).  Any object with llama_cpp.Llama's
+duck type works as ``llm``: ``reset()``, ``eval(tokens)``, ``n_ctx()`` and
+``_scores`` (2-D, last row = next-token logits).
+
+``TorchLLM`` provides that duck type for a PyTorch causal LM on the GPU
+(``module(tokens[1, t]) -> logits[1, t, V]``), so a ROCm model drops in where
+llama.cpp was.  It re-runs the window on every ``eval`` -- the same op sequence
+on the encode and the decode side, which is what makes the quantised tables,
+and therefore the bitstream, reproducible.
+
+Coding goes through lac_amd.coder (GPU); this module only produces tables.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .coder import ProbPredictor
+
+
+def quantise_logits(logits) -> np.ndarray:
+    """logits -> inclusive int64 CDF, the reference's quantiser (llama_compress.py:24-30):
+    exp, normalise, scale by 2^60, clip at 2, float64 running sum, truncate."""
+    pdf = np.exp(np.asarray(logits, dtype=np.float64))
+    pdf /= np.sum(pdf)
+    scaled = np.clip((pdf * float(1 << 60)).astype(float), 2, None)
+    return np.cumsum(scaled).astype(np.int64)
+
+
+class Llama_AC(ProbPredictor):
+    """Model-driven predictor (llama_compress.py:14-61) for lac_amd.coder.AC."""
+
+    def __init__(self, llm, maxtoks=2048):
+        super().__init__(0)
+        self.llm = llm
+        self.overlap = 2
+        self.reset()
+
+    def reset(self):
+        self.past = [1]
+        self.llm.reset()
+        self.llm.eval([1])
+
+    def calc_dist(self):
+        self.dcache = quantise_logits(self.llm._scores[-1])
+        return self.dcache
+
+    def pmf_row(self):
+        """The current table as a uint64 pmf row (what the coder uploads)."""
+        cdf = self.dist
+        pmf = np.empty(len(cdf), dtype=np.uint64)
+        pmf[0] = cdf[0]
+        pmf[1:] = np.diff(cdf).astype(np.uint64)
+        return pmf
+
+    def accept(self, symbol):
+        self.past.append(symbol)
+        n_ctx = self.llm.n_ctx()
+        if len(self.past) == n_ctx:
+            self.past = self.past[n_ctx - n_ctx // self.overlap:]
+            self.llm.reset()
+            self.llm.eval(self.past)
+        else:
+            self.llm.eval([symbol])
+        return super().accept(symbol)
+
+    def copy(self):
+        return Llama_AC(self.llm)
+
+    @property
+    def minp(self):
+        return int(min(self.dist[0], np.min(np.diff(self.dist))))
+
+
+class TorchLLM:
+    """llama_cpp.Llama's duck type over a torch causal LM on a HIP device."""
+
+    def __init__(self, module, n_ctx=512, device="cuda"):
+        import torch
+        self.module = module.to(device).eval()
+        self.device = torch.device(device)
+        self._n_ctx = n_ctx
+        self.tokens = []
+        self._scores = None
+
+    def n_ctx(self):
+        return self._n_ctx
+
+    def reset(self):
+        self.tokens = []
+        self._scores = None
+
+    def eval(self, tokens):
+        import torch
+        self.tokens.extend(int(t) for t in tokens)
+        window = self.tokens[-self._n_ctx:]
+        with torch.no_grad():
+            x = torch.tensor([window], dtype=torch.long, device=self.device)
+            logits = self.module(x)[0, -1].float()
+        self._scores = logits.cpu().numpy()[None, :]
+
+
+class TinyCausalLM:
+    """A small random-init causal transformer (torch) for tests and demos -- a
+    stand-in for a real checkpoint, which cannot be fetched offline."""
+
+    def __new__(cls, vocab=32000, d=64, layers=2, heads=4, max_len=512, seed=0):
+        import torch
+        import torch.nn as nn
+
+        class _M(nn.Module):
+            def __init__(self):
+                super().__init__()
+                g = torch.Generator().manual_seed(seed)
+                self.emb = nn.Embedding(vocab, d)
+                self.pos = nn.Embedding(max_len, d)
+                layer = nn.TransformerEncoderLayer(d, heads, 4 * d, dropout=0.0, batch_first=True)
+                self.body = nn.TransformerEncoder(layer, layers)
+                self.head = nn.Linear(d, vocab)
+                with torch.no_grad():
+                    for p in self.parameters():
+                        p.copy_(torch.randn(p.shape, generator=g) * 0.5)
+
+            def forward(self, x):
+                t = x.shape[1]
+                mask = torch.triu(torch.full((t, t), float("-inf"), device=x.device), 1)
+                h = self.emb(x) + self.pos(torch.arange(t, device=x.device))[None]
+                return self.head(self.body(h, mask=mask, is_causal=True))
+
+        return _M()

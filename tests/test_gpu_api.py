@@ -168,3 +168,36 @@ def test_container_compress_decompress_batch():
     blob = container.compress_batch(coder, pmf, sym)
     out, n = container.decompress_batch(blob, pmf)
     assert n == [6] * 300 and torch.equal(out, sym)
+
+
+def test_llama_ac_adapter_with_torch_model_roundtrip():
+    """Llama_AC (llama_compress.py:14-61) driven by a ROCm torch model: encode, decode,
+    and bit-exact against the oracle on the tables the model produced."""
+    from lac_amd.coder import AC, group_bits
+    from lac_amd.llm import Llama_AC, TinyCausalLM, TorchLLM
+    from oracle import restate
+    V = 2000
+    llm = TorchLLM(TinyCausalLM(vocab=V, d=32, layers=1, heads=2, max_len=64), n_ctx=24, device="cuda:0")
+    rng = np.random.default_rng(11)
+    toks = rng.integers(0, V, 40).tolist()           # crosses the n_ctx sliding window
+    ac = AC(Llama_AC(llm), 48)
+    bits = list(ac.to_bin.bits(toks))
+    # replay the same model to get the integer rows, encode them with the oracle
+    p = Llama_AC(llm)
+    rows = []
+    for t in toks:
+        rows.append([int(x) for x in p.pmf_row()])
+        p.accept(t)
+    want, L = restate.encode_bytes(rows, toks, 48)
+    assert len(bits) == L and bytes(group_bits(iter(bits))) == want
+    assert list(ac.from_bin.run(bits, stop=0, n=len(toks))) == toks
+
+
+def test_quantiser_matches_reference_numpy_ops():
+    """quantise_logits is the reference's float64 numpy quantiser (llama_compress.py:24-30)."""
+    from lac_amd.llm import quantise_logits
+    logits = np.random.default_rng(3).standard_normal(1000).astype(np.float32) * 3
+    pdf = np.exp(logits.astype(np.float64))
+    pdf /= np.sum(pdf)
+    want = np.cumsum(np.clip((pdf * (1 << 60)).astype(float), 2, None)).astype(int)
+    assert (quantise_logits(logits) == want).all()

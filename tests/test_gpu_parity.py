@@ -307,3 +307,84 @@ def test_determined_count_matches_reference_gen(case):
     rows = [synth.pmf_row(case["seed"], t, 0, case["V"], case["kind"], case["exp_range"]) for t in range(case["steps"])]
     _determined_case(rows, case["syms"], case["decoded_extra"], case["decoded_count"], case["prec"],
                      bytes.fromhex(case["bytes"]), case["L"])
+
+
+# ---------------------------------------------------------------- edge cases
+@pytest.mark.parametrize("path", ["split", "fused"])
+def test_edge_single_symbol_alphabet(path):
+    """V=1: every symbol is certain, no bits are emitted (as the reference)."""
+    from oracle import restate
+    c = _coder(1, 3, 16)
+    c.set_path(path)
+    pmf = torch.full((5, 3, 1), 7, dtype=torch.int32, device=DEV)
+    sym = torch.zeros((5, 3), dtype=torch.int32, device=DEV)
+    c.encode_job(pmf, sym)
+    data, n = c.to_bytes()
+    want, L = restate.encode_bytes([[7]], [0] * 5, 16)
+    assert all(d == want for d in data) and (n == L).all()
+    c.decode_open()
+    assert torch.equal(c.decode(pmf), sym)
+
+
+@pytest.mark.parametrize("prec,V", [(2, 2), (3, 4), (10, 512), (11, 1024), (17, 65536)])
+def test_edge_vocab_at_precision_boundary(prec, V):
+    """2^(prec-1) == V (the largest vocabulary a precision admits) and tiny precisions."""
+    from oracle import oracle as coracle
+    pmf, sym = synth.make_batch(prec * 7 + V, 12, 5, V, "flat")
+    c, dpmf, data, n, tr = _gpu_encode(pmf, sym, prec)
+    out, nb, status, rc = coracle.encode_batch(pmf, sym, prec, nthreads=4)
+    assert rc == 0
+    for b in range(5):
+        assert data[b] == out[b, :(int(nb[b]) + 7) // 8].tobytes()
+    assert (_decode_both(c, dpmf) == sym).all()
+
+
+@pytest.mark.parametrize("path", ["split", "fused"])
+def test_edge_zero_steps_job(path):
+    """A job with no symbols flushes the initial interval only (A_to_bin().run([]))."""
+    from oracle import restate
+    c = _coder(10, 4, 20)
+    c.set_path(path)
+    pmf = torch.ones((0, 4, 10), dtype=torch.int32, device=DEV)
+    sym = torch.zeros((0, 4), dtype=torch.int32, device=DEV)
+    c.encode_job(pmf, sym)
+    data, n = c.to_bytes()
+    want, L = restate.encode_bytes([[1] * 10], [], 20)
+    assert all(d == want for d in data) and (n == L).all()
+
+
+def test_edge_ragged_streams_and_extreme_tables():
+    """Streams of very different entropy in one batch (one near-deterministic, one
+    uniform, one with a 2^31 spike) end at different lengths; all bit-exact."""
+    from oracle import oracle as coracle
+    V, B, T, prec = 4096, 6, 40, 48
+    rng = np.random.default_rng(5)
+    pmf = np.ones((T, B, V), dtype=np.uint32)
+    pmf[:, 0, 17] = 2 ** 31                      # near-certain symbol 17
+    pmf[:, 2, :] = rng.integers(1, 2 ** 31, (T, V), dtype=np.uint32)
+    pmf[:, 3, ::2] = 0                           # half the alphabet impossible
+    pmf[:, 4, :] = 0
+    pmf[:, 4, 100:102] = 2 ** 31 - 1             # two-symbol row
+    pmf[:, 5, :] = 2 ** 32 - 1                   # maximal entries everywhere
+    sym = rng.integers(0, V, (T, B)).astype(np.int32)
+    sym[:, 0] = 17
+    sym[:, 3] = (sym[:, 3] // 2) * 2 + 1
+    sym[:, 4] = 100 + (sym[:, 4] & 1)
+    c, dpmf, data, n, tr = _gpu_encode(pmf, sym, prec)
+    out, nb, status, rc = coracle.encode_batch(pmf, sym, prec, nthreads=6)
+    assert rc == 0
+    assert len(set(int(x) for x in n)) >= 4
+    for b in range(B):
+        assert data[b] == out[b, :(int(nb[b]) + 7) // 8].tobytes(), b
+    assert (_decode_both(c, dpmf) == sym).all()
+
+
+def test_edge_u64_total_overflow_is_an_error():
+    V, B = 8, 2
+    pmf = np.full((1, B, V), 2 ** 62, dtype=np.uint64)      # total 2^65
+    pmf[0, 1, :] = 1
+    sym = np.zeros((1, B), dtype=np.int32)
+    c = _coder(V, B, 48, bits=64)
+    c.encode(_dev_pmf(pmf), torch.from_numpy(sym).to(DEV))
+    rc, err, step = c.status()
+    assert err.tolist() == [-5, 0]
