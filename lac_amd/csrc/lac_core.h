@@ -33,6 +33,8 @@ struct RowStats {          // per (step, stream) row, written by the row-stats k
     uint64_t hi;           // c_s
     uint64_t tot;          // T = c_{V-1}; 0 marks a bad row (minp: 0 empty, 1 overflow)
     uint64_t minp;         // smallest positive pmf entry
+    double inv_tot;        // 1.0 / T, so the serial coder step multiplies instead of divides
+    uint64_t pad;
 };
 
 struct EncState {          // per stream, persistent across lac_encode calls
@@ -81,6 +83,23 @@ __host__ __device__ inline uint64_t div_ceil(u128 N, uint64_t d) {
     return div_floor(N + (d - 1), d);
 }
 
+// div_floor with a precomputed inv = 1.0 / d (same estimate accuracy, no
+// float64 divide on the latency chain of the sequential coder).
+__host__ __device__ inline uint64_t div_floor_inv(u128 N, uint64_t d, double inv) {
+    const double two64 = 18446744073709551616.0;
+    const double dn = (double)(uint64_t)(N >> 64) * two64 + (double)(uint64_t)N;
+    double qd = dn * inv;
+    uint64_t q = qd >= 9.2e18 ? (uint64_t)9.2e18 : (uint64_t)qd;
+    i128 r = (i128)(N - (u128)q * d);
+    const double rd = (double)(int64_t)(r >> 64) * two64 + (double)(uint64_t)r;
+    const int64_t adj = (int64_t)(rd * inv);
+    q += (uint64_t)adj;
+    r -= (i128)adj * (i128)d;
+    while (r < 0) { q -= 1; r += d; }
+    while (r >= (i128)d) { q += 1; r -= d; }
+    return q;
+}
+
 // CDFPredictor.fudged_dist test (arith_code.py:84): fudged iff T > w*minp.
 __host__ __device__ inline bool is_fudged(uint64_t T, uint64_t w, uint64_t minp) {
     return (u128)T > (u128)w * minp;
@@ -91,6 +110,12 @@ __host__ __device__ inline void unfudged_range(uint64_t lo, uint64_t hi, uint64_
                                                uint64_t *a, uint64_t *b) {
     *a = lo ? div_ceil((u128)lo * w, T) : 0;
     *b = div_ceil((u128)hi * w, T);
+}
+
+__host__ __device__ inline void unfudged_range_inv(uint64_t lo, uint64_t hi, uint64_t T, double inv, uint64_t w,
+                                                   uint64_t *a, uint64_t *b) {
+    *a = lo ? div_floor_inv((u128)lo * w + (T - 1), T, inv) : 0;
+    *b = div_floor_inv((u128)hi * w + (T - 1), T, inv);
 }
 
 // Floor mapping of Predictor.symbol_to_range (arith_code.py:69-70) and of

@@ -283,7 +283,8 @@ __device__ i128 wave_xmax_prefix(const E *row, int64_t n, uint64_t w, uint64_t T
 template <typename E>
 __device__ inline bool coder_step(EncState &st, int64_t &l, int64_t &h, uint64_t lo, uint64_t hi, uint64_t T,
                                   uint64_t minp, int64_t s, const E *row, int64_t V, int prec, uint64_t *pa,
-                                  uint64_t *pc, uint64_t cap_words, uint64_t *trace_slot, int lane, int mapping) {
+                                  uint64_t *pc, uint64_t cap_words, uint64_t *trace_slot, int lane, int mapping,
+                                  double inv_T = 0.0) {
     if (s < 0 || s >= V) { st.err = LAC_E_SYMBOL_RANGE; return false; }   // arith_code.py:100-101
     if (T == 0) { st.err = LAC_E_TABLE; return false; }
     const uint64_t w = (uint64_t)(h - l + 1);
@@ -291,7 +292,8 @@ __device__ inline bool coder_step(EncState &st, int64_t &l, int64_t &h, uint64_t
     if (mapping == LAC_MAP_FLOOR) {
         floor_range(lo, hi, T, w, &a, &bb);
     } else if (!is_fudged(T, w, minp)) {
-        unfudged_range(lo, hi, T, w, &a, &bb);
+        if (inv_T != 0.0) unfudged_range_inv(lo, hi, T, inv_T, w, &a, &bb);
+        else unfudged_range(lo, hi, T, w, &a, &bb);
     } else {                                                  // CDFPredictor.fudged_dist
         const i128 xprev = s > 0 ? wave_xmax_prefix<E>(row, s, w, T) : kI128Min;
         const i128 xs = fudge_x(hi, s, w, T);
@@ -404,15 +406,17 @@ __global__ __launch_bounds__(256) void k_row_stats(const E *__restrict__ pmf, in
             st.tot = (uint64_t)rs.T;
             st.minp = rs.T ? rs.minp : 0;
         }
+        st.inv_tot = st.tot ? 1.0 / (double)st.tot : 0.0;
+        st.pad = 0;
         out[r] = st;
     }
 }
 
-// k_encode: one wave per stream over a chunk of <= 64 steps; lane i prefetches
-// step i's RowStats.
+// k_encode: one wave per stream over a chunk of steps; lane i prefetches the
+// RowStats of step g0 + i, 64 steps at a time.
 template <typename E>
 __global__ __launch_bounds__(256) void k_encode(const RowStats *__restrict__ stats, const int32_t *__restrict__ sym,
-                                                int64_t B, int64_t t0, int nsteps, const E *pmf,
+                                                int64_t B, int64_t t0, int64_t nsteps, const E *pmf,
                                                 int64_t step_stride, int64_t stream_stride, int64_t V, int prec,
                                                 EncState *states, uint64_t *planeA, uint64_t *planeC,
                                                 uint64_t cap_words, uint64_t *trace, int mapping) {
@@ -424,22 +428,31 @@ __global__ __launch_bounds__(256) void k_encode(const RowStats *__restrict__ sta
         if (lane == 0 && !st.err && st.nflush >= 0) { st.err = LAC_E_STATE; st.err_step = st.nsym; states[b] = st; }
         return;
     }
-    RowStats my = {0, 0, 0, 0};
-    int32_t mys = 0;
-    if (lane < nsteps) {
-        my = stats[(int64_t)lane * B + b];
-        mys = sym[(t0 + lane) * B + b];
-    }
     uint64_t *pa = planeA + (uint64_t)b * cap_words, *pc = planeC + (uint64_t)b * cap_words;
     int64_t l = st.l, h = st.h;
-    for (int i = 0; i < nsteps; i++) {
-        const uint64_t lo = readlane_u64(my.lo, i), hi = readlane_u64(my.hi, i);
-        const uint64_t T = readlane_u64(my.tot, i), minp = readlane_u64(my.minp, i);
-        const int64_t s = __builtin_amdgcn_readlane(mys, i);
-        const E *row = pmf + (t0 + i) * step_stride + b * stream_stride;
-        if (!coder_step<E>(st, l, h, lo, hi, T, minp, s, row, V, prec, pa, pc, cap_words,
-                           trace ? trace + 2 * ((t0 + i) * B + b) : nullptr, lane, mapping))
-            break;
+    bool ok = true;
+    for (int64_t g0 = 0; g0 < nsteps && ok; g0 += 64) {
+        const int n = (int)((nsteps - g0) < 64 ? (nsteps - g0) : 64);
+        RowStats my = {0, 0, 0, 0, 0.0, 0};
+        int32_t mys = 0;
+        if (lane < n) {
+            my = stats[(g0 + lane) * B + b];
+            mys = sym[(t0 + g0 + lane) * B + b];
+        }
+        for (int i = 0; i < n; i++) {
+            const uint64_t lo = readlane_u64(my.lo, i), hi = readlane_u64(my.hi, i);
+            const uint64_t T = readlane_u64(my.tot, i), minp = readlane_u64(my.minp, i);
+            const uint64_t invb = readlane_u64(__builtin_bit_cast(uint64_t, my.inv_tot), i);
+            const int64_t s = __builtin_amdgcn_readlane(mys, i);
+            const int64_t t = t0 + g0 + i;
+            const E *row = pmf + t * step_stride + b * stream_stride;
+            if (!coder_step<E>(st, l, h, lo, hi, T, minp, s, row, V, prec, pa, pc, cap_words,
+                               trace ? trace + 2 * (t * B + b) : nullptr, lane, mapping,
+                               __builtin_bit_cast(double, invb))) {
+                ok = false;
+                break;
+            }
+        }
     }
     if (lane == 0) store_state(st, l, h, pa, pc, cap_words, &states[b]);
 }
@@ -697,15 +710,17 @@ __device__ inline int decode_symbol(DecState &st, const E *row, int64_t V, uint6
     return decode_advance(st, a, bb, bits, nbits, prec);
 }
 
-// One decode step for every stream, 4 waves per stream (small stream counts).
-template <typename E, int VEC, int G>
-__global__ __launch_bounds__(256) void k_decode_step(const E *__restrict__ pmf, int64_t step_off,
-                                                     int64_t stream_stride, int64_t V, int prec,
-                                                     DecState *states, const uint8_t *bits, uint64_t stride,
-                                                     const uint64_t *nbits, int32_t *sym_out, int64_t B, int mapping) {
+// One decode step for every stream, NW waves per stream (small stream counts:
+// with few streams the row of one stream must be streamed by many waves).
+template <typename E, int VEC, int G, int NW>
+__global__ __launch_bounds__(64 * NW) void k_decode_step(const E *__restrict__ pmf, int64_t step_off,
+                                                         int64_t stream_stride, int64_t V, int prec,
+                                                         DecState *states, const uint8_t *bits, uint64_t stride,
+                                                         const uint64_t *nbits, int32_t *sym_out, int64_t B,
+                                                         int mapping) {
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
-    __shared__ uint64_t wmin[kWavesPerBlock];
-    __shared__ uint32_t wovf[kWavesPerBlock];
+    __shared__ uint64_t wmin[NW];
+    __shared__ uint32_t wovf[NW];
     const int lane = (int)lane_id(), wave = threadIdx.x >> 6;
     const int64_t b = blockIdx.x;
     DecState st = states[b];
@@ -720,7 +735,7 @@ __global__ __launch_bounds__(256) void k_decode_step(const E *__restrict__ pmf, 
     // ---- pass 1: chunk sums, minp (all waves)
     uint64_t mn = ~0ull;
     uint32_t ovf = 0;
-    for (int64_t c = wave; c < nch; c += kWavesPerBlock) {
+    for (int64_t c = wave; c < nch; c += NW) {
         uint64_t ls = 0;
         typename VecT<E, VEC>::type x[G];
 #pragma unroll
@@ -759,7 +774,7 @@ __global__ __launch_bounds__(256) void k_decode_step(const E *__restrict__ pmf, 
     // ---- wave 0: T, minp, chunk prefix
     uint64_t m0 = wmin[0];
     uint32_t anyovf = wovf[0];
-    for (int i = 1; i < kWavesPerBlock; i++) { m0 = wmin[i] < m0 ? wmin[i] : m0; anyovf |= wovf[i]; }
+    for (int i = 1; i < NW; i++) { m0 = wmin[i] < m0 ? wmin[i] : m0; anyovf |= wovf[i]; }
     const int64_t per = (nch + 63) / 64;
     const int64_t c0 = lane * per, c1 = (c0 + per < nch) ? c0 + per : nch;
     u128 local = 0;
@@ -922,6 +937,7 @@ struct lac_ctx {
     int mode = 0;                       // 0 encode, 1 decode
     int path = LAC_PATH_AUTO;           // encode kernel path (lac_set_option)
     int64_t fused_min_streams = 2048;   // AUTO: fused kernel from this many streams
+    int64_t chunk_steps = 64;           // split path: steps per row-stats launch
     int dpath = LAC_PATH_AUTO;          // decode kernel path
     int64_t wave_decode_min_streams = 1024;
     int mapping = LAC_MAP_CEIL;         // symbol_to_range flavour (lac_set_option)
@@ -1006,9 +1022,9 @@ static int encode_impl(lac_ctx *c, const E *pmf, int64_t step_stride, int64_t st
         k_enc_reset<<<(unsigned)((c->B + 255) / 256), 256, 0, st>>>(c->enc, c->B, c->prec);
         CHECK_LAUNCH();
     }
-    for (int64_t t0 = 0; t0 < steps; t0 += kChunkSteps) {
-        const int n = (int)((steps - t0) < kChunkSteps ? (steps - t0) : kChunkSteps);
-        const int64_t rows = (int64_t)n * c->B;
+    for (int64_t t0 = 0; t0 < steps; t0 += c->chunk_steps) {
+        const int64_t n = (steps - t0) < c->chunk_steps ? (steps - t0) : c->chunk_steps;
+        const int64_t rows = n * c->B;
         {
             ProfScope ps(c, KID_ROW_STATS, st);
             k_row_stats<E, VEC><<<(unsigned)((rows + kWavesPerBlock - 1) / kWavesPerBlock), 64 * kWavesPerBlock, 0,
@@ -1063,8 +1079,14 @@ static int decode_launch(lac_ctx *c, const E *pmf, int64_t step_off, int64_t str
     const size_t lds = sizeof(uint64_t) * (size_t)nch;
     if (lds > 64 * 1024) return fail(LAC_E_ARG, "vocab too large for the decode chunk table");
     ProfScope ps(c, KID_DECODE, st);
-    k_decode_step<E, VEC, G><<<(unsigned)c->B, 64 * kWavesPerBlock, lds, st>>>(
-        pmf, step_off, stream_stride, c->V, c->prec, c->dec, c->dbits, c->dstride, c->dnbits, out, c->B, c->mapping);
+    if (c->B <= 256)        // few streams: 16 waves per stream keep the whole row in flight
+        k_decode_step<E, VEC, G, 16><<<(unsigned)c->B, 64 * 16, lds, st>>>(
+            pmf, step_off, stream_stride, c->V, c->prec, c->dec, c->dbits, c->dstride, c->dnbits, out, c->B,
+            c->mapping);
+    else
+        k_decode_step<E, VEC, G, kWavesPerBlock><<<(unsigned)c->B, 64 * kWavesPerBlock, lds, st>>>(
+            pmf, step_off, stream_stride, c->V, c->prec, c->dec, c->dbits, c->dstride, c->dnbits, out, c->B,
+            c->mapping);
     CHECK_LAUNCH();
     return LAC_OK;
 }
@@ -1097,11 +1119,14 @@ static int decode_dispatch(lac_ctx *c, const void *pmf, int64_t step_stride, int
         const int64_t off = t * step_stride;
         int32_t *o = out + t * c->B;
         int rc;
+        const bool few = c->B <= 256;                         // 16-wave workgroups: 8 loads/lane per chunk
         if (c->pmf_bits == 32)
-            rc = vec ? decode_launch<uint32_t, 4, 2>(c, (const uint32_t *)pmf, off, stream_stride, o, st)
+            rc = vec ? (few ? decode_launch<uint32_t, 4, 8>(c, (const uint32_t *)pmf, off, stream_stride, o, st)
+                            : decode_launch<uint32_t, 4, 2>(c, (const uint32_t *)pmf, off, stream_stride, o, st))
                      : decode_launch<uint32_t, 1, 8>(c, (const uint32_t *)pmf, off, stream_stride, o, st);
         else
-            rc = vec ? decode_launch<uint64_t, 2, 4>(c, (const uint64_t *)pmf, off, stream_stride, o, st)
+            rc = vec ? (few ? decode_launch<uint64_t, 2, 8>(c, (const uint64_t *)pmf, off, stream_stride, o, st)
+                            : decode_launch<uint64_t, 2, 4>(c, (const uint64_t *)pmf, off, stream_stride, o, st))
                      : decode_launch<uint64_t, 1, 8>(c, (const uint64_t *)pmf, off, stream_stride, o, st);
         if (rc) return rc;
     }
@@ -1135,7 +1160,9 @@ int lac_open(int device, int prec, int64_t vocab, int64_t streams, int pmf_bits,
     c->cap_bits = capacity_bits;
     c->cap_words = (capacity_bits + 63) / 64 + 1;
     hipError_t e = hipSuccess;
-    e = e ? e : hipMalloc(&c->stats, sizeof(RowStats) * kChunkSteps * streams);
+    // split path: steps per row-stats launch, enough rows to fill the chip even for 1 stream
+    c->chunk_steps = streams >= 512 ? kChunkSteps : ((32768 / streams + 63) / 64) * 64;
+    e = e ? e : hipMalloc(&c->stats, sizeof(RowStats) * c->chunk_steps * streams);
     e = e ? e : hipMalloc(&c->enc, sizeof(EncState) * streams);
     e = e ? e : hipMalloc(&c->dec, sizeof(DecState) * streams);
     e = e ? e : hipMalloc(&c->planeA, sizeof(uint64_t) * (c->cap_words * streams + 1));

@@ -17,6 +17,9 @@ using namespace lac;
 extern "C" {
 
 uint64_t cc_div_floor(uint64_t nh, uint64_t nl, uint64_t d) { return div_floor(((u128)nh << 64) | nl, d); }
+uint64_t cc_div_floor_inv(uint64_t nh, uint64_t nl, uint64_t d) {
+    return div_floor_inv(((u128)nh << 64) | nl, d, 1.0 / (double)d);
+}
 
 // pmf rows [steps][V] (eb = 4 or 8 bytes), one stream.  Returns status, writes
 // MSB-first bytes and the bit count.

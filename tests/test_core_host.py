@@ -27,6 +27,8 @@ def core():
     lib = C.CDLL(SO)
     lib.cc_div_floor.restype = C.c_uint64
     lib.cc_div_floor.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64]
+    lib.cc_div_floor_inv.restype = C.c_uint64
+    lib.cc_div_floor_inv.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64]
     lib.cc_encode.restype = C.c_int
     lib.cc_encode.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.c_int64, C.c_int64, C.c_void_p, C.c_int,
                               C.c_void_p, C.c_uint64, C.c_void_p]
@@ -56,6 +58,7 @@ def test_div_floor_exact(core):
         if N >> 128:
             continue
         assert core.cc_div_floor(N >> 64, N & ((1 << 64) - 1), d) == q
+        assert core.cc_div_floor_inv(N >> 64, N & ((1 << 64) - 1), d) == q
 
 
 def test_core_matches_golden(core):
