@@ -22,7 +22,6 @@ import numpy as np
 from . import _lib
 from ._lib import LacError, check
 
-_ASSERT_CODES = (_lib.LAC_E_SYMBOL_RANGE, _lib.LAC_E_DECODE_RANGE)
 
 
 def _torch():
@@ -64,7 +63,6 @@ class BatchCoder:
         check(self.lib.lac_open(self.device.index or 0, self.prec, self.vocab, self.streams, self.pmf_bits,
                                 self.capacity_bits, C.byref(ctx)))
         self.ctx = ctx
-        self._finished = False
 
     # ------------------------------------------------------------ lifetime
     def close(self):
@@ -104,7 +102,6 @@ class BatchCoder:
     # ------------------------------------------------------------ encode
     def reset(self):
         check(self.lib.lac_encode_reset(self.ctx, self._stream))
-        self._finished = False
 
     def _encode_args(self, pmf, sym, trace):
         torch = _torch()
@@ -150,7 +147,6 @@ class BatchCoder:
     def encode_job(self, pmf, sym, trace=None):
         """reset + encode + finish in one call (one kernel at >= 2048 streams)."""
         check(self.lib.lac_encode_job(*self._encode_args(pmf, sym, trace)))
-        self._finished = True
 
     def set_mapping(self, mapping):
         """'ceil' (CDFPredictor, default) or 'floor' (Predictor / ACSampler Region.map)."""
@@ -174,7 +170,6 @@ class BatchCoder:
 
     def finish(self):
         check(self.lib.lac_encode_finish(self.ctx, self._stream))
-        self._finished = True
 
     def status(self):
         err = np.zeros(self.streams, dtype=np.int32)

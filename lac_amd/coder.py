@@ -206,7 +206,6 @@ class A_to_bin:
         self.debug_log = None
         self._coder = None
         self._V = None
-        self._pending_flush = False
 
     # -- device plumbing
     def _ensure(self, V, steps_hint=1):

@@ -65,7 +65,7 @@ using namespace lac;
 
 namespace {
 
-constexpr int kChunkSteps = 64;       // steps per encode launch pair (= lanes of a wave)
+constexpr int kChunkSteps = 64;       // split path: steps per row-stats launch at >= 512 streams
 constexpr int kWavesPerBlock = 4;     // 256-thread workgroups
 
 // ------------------------------------------------------------------ wave helpers
