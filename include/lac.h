@@ -170,6 +170,40 @@ int lac_decode_step(lac_ctx *ctx, const void *pmf_dev, int64_t stream_stride,
 int lac_decode_steps(lac_ctx *ctx, const void *pmf_dev, int64_t step_stride, int64_t stream_stride,
                      int64_t steps, int32_t *sym_out_dev, void *stream);
 
+/* ---- logits path --------------------------------
+ * Tables are computed in-kernel from raw logits with the integer-exact "q1"
+ * quantiser instead of being read from a pmf in HBM: for each row
+ *   m = max_i x_i,  q_i = max(1, floor(2^k * 2^(-(m - x_i) * log2 e)))
+ * evaluated with a 16.16 fixed-point exponent and a 1024-entry 2^-j/1024 table
+ * (include/lac_q1_table.h; bit-exact spec in DESIGN.md "logits path"), with
+ * k = lac_q1_k(prec, vocab) = min(31, prec - 1 - ceil(log2 vocab)) so that
+ * T <= 2^(prec-1) and no row is ever fudged.  It replaces the float64 numpy
+ * quantiser of llama_compress.py:29-36 (whose output is platform-dependent)
+ * with a rule both the GPU and the C oracle reproduce bit for bit; the coder
+ * semantics are those of CDFPredictor + A_to_bin / A_from_bin
+ * (arith_code.py:17-92, 199-299).  Logit rows: bf16 (uint16 bit patterns) or
+ * f32, 16-byte aligned, vocab and strides (in elements) multiples of 8 (bf16)
+ * or 4 (f32).  Requires the CEIL mapping and FLUSH termination. */
+#define LAC_LOGITS_BF16 1
+#define LAC_LOGITS_F32 2
+
+int lac_q1_k(int prec, int64_t vocab);
+
+/* reset + encode `steps` symbols per stream from logits + finish, one launch
+ * (logits[t*step_stride + b*stream_stride + i], sym_dev[t*streams + b]). */
+int lac_encode_logits_job(lac_ctx *ctx, const void *logits_dev, int logit_type, int64_t step_stride,
+                          int64_t stream_stride, const int32_t *sym_dev, int64_t steps, uint64_t *trace_dev,
+                          void *stream);
+
+/* Decode `steps` symbols per stream (after lac_decode_open) with the tables
+ * computed from logits; sym_out_dev[t*streams + b] (-1 after an error). */
+int lac_decode_logits_steps(lac_ctx *ctx, const void *logits_dev, int logit_type, int64_t step_stride,
+                            int64_t stream_stride, int64_t steps, int32_t *sym_out_dev, void *stream);
+
+/* Materialise the q1 tables: pmf_out_dev[(t*streams + b)*vocab + i] (uint32). */
+int lac_quantize_logits(lac_ctx *ctx, const void *logits_dev, int logit_type, int64_t step_stride,
+                        int64_t stream_stride, int64_t steps, uint32_t *pmf_out_dev, void *stream);
+
 /* Synchronise; ndet_host[streams] = how many leading decoded symbols the
  * available bits determine, i.e. how many symbols the reference's bit-serial
  * A_from_bin.run(bits, stop=0) emits (arith_code.py:268-299, :322-326). */
@@ -178,7 +212,7 @@ int lac_decode_determined(lac_ctx *ctx, int64_t *ndet_host, void *stream);
 /* Live kernel timing: with profiling on, every kernel launch is bracketed by
  * hipEvents recorded on its own stream.  lac_profile_read synchronises and
  * returns, per kernel id (0 row_stats, 1 encode, 2 finish, 3 decode_step,
- * 4 encode_fused, 5 decode_wave; 8 slots), the summed device milliseconds and the launch
+ * 4 encode_fused, 5 decode_wave, 6 encode_logits, 7 decode_logits; 8 slots), the summed device milliseconds and the launch
  * count; reset != 0 clears. */
 int lac_profile_enable(lac_ctx *ctx, int on);
 int lac_profile_read(lac_ctx *ctx, double *ms_total /*[8]*/, int64_t *launches /*[8]*/, int reset);

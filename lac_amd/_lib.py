@@ -57,9 +57,15 @@ PROTOTYPES = [
     ("lac_decode_determined", _i, [_vp, _vp, _vp]),
     ("lac_profile_enable", _i, [_vp, _i]),
     ("lac_profile_read", _i, [_vp, _vp, _vp, _i]),
+    ("lac_q1_k", _i, [_i, _i64]),
+    ("lac_encode_logits_job", _i, [_vp, _vp, _i, _i64, _i64, _vp, _i64, _vp, _vp]),
+    ("lac_decode_logits_steps", _i, [_vp, _vp, _i, _i64, _i64, _i64, _vp, _vp]),
+    ("lac_quantize_logits", _i, [_vp, _vp, _i, _i64, _i64, _i64, _vp, _vp]),
 ]
 
-KERNEL_IDS = {"row_stats": 0, "encode": 1, "finish": 2, "decode_step": 3, "encode_fused": 4, "decode_wave": 5}
+KERNEL_IDS = {"row_stats": 0, "encode": 1, "finish": 2, "decode_step": 3, "encode_fused": 4, "decode_wave": 5,
+              "encode_logits": 6, "decode_logits": 7}
+LAC_LOGITS_BF16, LAC_LOGITS_F32 = 1, 2
 LAC_OPT_ENCODE_PATH = 1
 LAC_OPT_FUSED_MIN_STREAMS = 2
 LAC_PATH_AUTO, LAC_PATH_SPLIT, LAC_PATH_FUSED = 0, 1, 2

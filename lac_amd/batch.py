@@ -273,6 +273,74 @@ class BatchCoder:
         return out
 
 
+    # ------------------------------------------------------------ logits path
+    def _logits_args(self, logits, steps=None):
+        """-> (type, step_stride, stream_stride, steps) for a [steps, streams, V]
+        bf16/f32 logits tensor (stride-0 broadcasts allowed, rows contiguous)."""
+        torch = _torch()
+        typ = {torch.bfloat16: _lib.LAC_LOGITS_BF16, torch.float32: _lib.LAC_LOGITS_F32}.get(logits.dtype)
+        if typ is None:
+            raise TypeError(f"logits must be bfloat16 or float32, got {logits.dtype}")
+        if logits.device != self.device:
+            raise ValueError(f"logits are on {logits.device}, coder on {self.device}")
+        if logits.dim() == 2:
+            logits = logits.unsqueeze(0)
+        if logits.dim() != 3 or logits.shape[1] not in (1, self.streams) or logits.shape[2] != self.vocab:
+            raise ValueError(f"logits must be [steps, {self.streams}, {self.vocab}]")
+        if logits.stride(2) != 1:
+            raise ValueError("logit rows must be contiguous")
+        n = logits.shape[0] if steps is None else steps
+        if logits.shape[0] not in (1, n):
+            raise ValueError("logits steps do not match the symbols")
+        step_stride = logits.stride(0) if logits.shape[0] > 1 else 0
+        stream_stride = logits.stride(1) if logits.shape[1] > 1 else 0
+        return typ, step_stride, stream_stride, n, logits
+
+    def encode_logits_job(self, logits, sym, trace=None):
+        """reset + encode + finish with tables computed in-kernel from logits by
+        the q1 quantiser (include/lac.h "logits path"): one launch, the pmf never
+        touches HBM.  ``logits`` [steps, streams, V] bf16/f32, ``sym`` [steps, streams]."""
+        torch = _torch()
+        if sym.dtype != torch.int32 or sym.device != self.device:
+            raise TypeError("sym must be an int32 tensor on the coder's device")
+        sym = sym.contiguous()
+        steps = sym.shape[0] if sym.dim() == 2 else 1
+        if sym.numel() != steps * self.streams:
+            raise ValueError(f"sym must be [steps, {self.streams}]")
+        typ, ss, bs, steps, logits = self._logits_args(logits, steps)
+        tp = None
+        if trace is not None:
+            if trace.dtype != torch.int64 or trace.numel() != steps * self.streams * 2 or not trace.is_contiguous():
+                raise ValueError("trace must be a contiguous int64 tensor [steps, streams, 2]")
+            tp = C.c_void_p(trace.data_ptr())
+        self._keep = (logits, sym)
+        check(self.lib.lac_encode_logits_job(self.ctx, C.c_void_p(logits.data_ptr()), typ, ss, bs,
+                                             C.c_void_p(sym.data_ptr()), steps, tp, self._stream))
+
+    def decode_logits(self, logits, out=None):
+        """Decode one symbol per stream per step with q1 tables from ``logits``."""
+        torch = _torch()
+        typ, ss, bs, steps, logits = self._logits_args(logits)
+        if out is None:
+            out = torch.empty((steps, self.streams), dtype=torch.int32, device=self.device)
+        check(self.lib.lac_decode_logits_steps(self.ctx, C.c_void_p(logits.data_ptr()), typ, ss, bs, steps,
+                                               C.c_void_p(out.data_ptr()), self._stream))
+        return out
+
+    def quantize_logits(self, logits):
+        """The q1 tables themselves: int32 tensor (uint32 bit patterns) [steps, streams, V]."""
+        torch = _torch()
+        typ, ss, bs, steps, logits = self._logits_args(logits)
+        out = torch.empty((steps, self.streams, self.vocab), dtype=torch.int32, device=self.device)
+        check(self.lib.lac_quantize_logits(self.ctx, C.c_void_p(logits.data_ptr()), typ, ss, bs, steps,
+                                           C.c_void_p(out.data_ptr()), self._stream))
+        return out
+
+    def q1_k(self):
+        """The q1 table scale: max entry 2^k, k = min(31, prec - 1 - ceil(log2 V))."""
+        return int(self.lib.lac_q1_k(self.prec, self.vocab))
+
+
 def digits_of(E: int, k: int):
     """Raw digits of one symbol from its trace entry (first digit 0..3)."""
     if k <= 0:

@@ -30,6 +30,7 @@
 
 #include "lac.h"
 #include "lac_core.h"
+#include "lac_q1_table.h"
 
 using namespace lac;
 
@@ -284,7 +285,7 @@ template <typename E>
 __device__ inline bool coder_step(EncState &st, int64_t &l, int64_t &h, uint64_t lo, uint64_t hi, uint64_t T,
                                   uint64_t minp, int64_t s, const E *row, int64_t V, int prec, uint64_t *pa,
                                   uint64_t *pc, uint64_t cap_words, uint64_t *trace_slot, int lane, int mapping,
-                                  double inv_T = 0.0) {
+                                  double inv_T = 0.0, bool allow_fudge = true) {
     if (s < 0 || s >= V) { st.err = LAC_E_SYMBOL_RANGE; return false; }   // arith_code.py:100-101
     if (T == 0) { st.err = LAC_E_TABLE; return false; }
     const uint64_t w = (uint64_t)(h - l + 1);
@@ -295,6 +296,7 @@ __device__ inline bool coder_step(EncState &st, int64_t &l, int64_t &h, uint64_t
         if (inv_T != 0.0) unfudged_range_inv(lo, hi, T, inv_T, w, &a, &bb);
         else unfudged_range(lo, hi, T, w, &a, &bb);
     } else {                                                  // CDFPredictor.fudged_dist
+        if (!allow_fudge) { st.err = LAC_E_TABLE; return false; }
         const i128 xprev = s > 0 ? wave_xmax_prefix<E>(row, s, w, T) : kI128Min;
         const i128 xs = fudge_x(hi, s, w, T);
         a = s > 0 ? fudge_f(s - 1, xprev, T, w, V) : 0;
@@ -920,6 +922,315 @@ __global__ LAC_DEC_BOUNDS void k_decode_wave(const E *__restrict__ pmf, int64_t 
     if (lane == 0) states[b] = st;
 }
 
+// ================================================================ q1 logits path
+// Tables computed in-kernel from logits (bf16 or f32) with the integer-exact q1
+// quantiser (include/lac_q1_table.h, DESIGN.md "logits path"), so the pmf never
+// exists in HBM.  Per step: pass 1 = row max, pass 2 = quantise + the usual
+// reductions (the row is re-read while it is still resident in the 256 MB MALL).
+__constant__ uint32_t c_q1_tab[1024] = LAC_Q1_TAB_INIT;
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <typename LT> struct LogitN { static constexpr int N = 16 / sizeof(LT); };
+
+template <typename LT>
+__device__ inline float logit_at(const u32x4 &v, int j) {
+    if constexpr (sizeof(LT) == 2) {
+        const uint32_t w = v[j >> 1];
+        return __uint_as_float((j & 1) ? (w & 0xFFFF0000u) : (w << 16));
+    } else {
+        return __uint_as_float(v[j]);
+    }
+}
+
+__device__ inline u32x4 ld16(const void *row, int64_t vi, bool nt) {
+    const u32x4 *p = reinterpret_cast<const u32x4 *>(row) + vi;
+    return nt ? __builtin_nontemporal_load(p) : *p;
+}
+
+// q1 on the GPU, bit-identical to the spec in include/lac_q1_table.h for every
+// float input (NaN and +-inf included):
+//  * tab[] = LAC_Q1_TAB >> (31 - k) (per launch, in LDS): shifts compose exactly
+//    under floor, so tab[fr] >> ip == LAC_Q1_TAB[fr] >> (ip + 31 - k);
+//  * d is clamped at 255 (NaN -> 255): every d >= 255 has ip >= 367 and q = 1 in
+//    the spec, and so does the clamped value; u = d * 2^16 < 2^24, so the Q32
+//    exponent u * log2(e) is two full-rate 24-bit multiplies;
+//  * ip >= 32 gives 0 in the spec; min(ip, 31) leaves tab[fr] >> 31 <= 1
+//    (tab[] <= 2^31), which the final max(q, 1) turns into the same 1.
+__device__ inline uint32_t q1_val(float x, float m, const uint32_t *tab) {
+    const float d = fminf(m - x, 255.0f);
+    const uint32_t u = (uint32_t)(d * 65536.0f) & 0xFFFFFFu;
+    const uint64_t e = (uint64_t)u * (uint64_t)LAC_Q1_LOG2E_Q16;
+    const uint32_t ip = (uint32_t)(e >> 32), fr = (uint32_t)e >> 22;
+    const uint32_t q = tab[fr] >> (ip < 31u ? ip : 31u);
+    return q ? q : 1u;
+}
+
+// The per-launch LDS table of q1_val (all threads of the block, then a barrier).
+__device__ inline void q1_load_tab(uint32_t *tab, uint32_t xsh) {
+    for (int i = threadIdx.x; i < 1024; i += blockDim.x) tab[i] = c_q1_tab[i] >> xsh;
+    __syncthreads();
+}
+
+__device__ inline float wave_max_f32(float v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m));
+    return v;
+}
+
+// pass 1: the row's max logit (default cache policy so pass 2 finds the row in MALL)
+template <typename LT>
+__device__ inline float q1_row_max(const LT *row, int64_t nvec) {
+    constexpr int N = LogitN<LT>::N, U = LAC_UNROLL;
+    const int lane = (int)lane_id();
+    float mx = -INFINITY;
+    int64_t vi = lane;
+    for (; vi + 64 * (U - 1) < nvec; vi += 64 * U) {
+        u32x4 x[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) x[u] = ld16(row, vi + 64 * u, false);
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int j = 0; j < N; j++) mx = fmaxf(mx, logit_at<LT>(x[u], j));
+    }
+    for (; vi < nvec; vi += 64) {
+        const u32x4 x = ld16(row, vi, false);
+#pragma unroll
+        for (int j = 0; j < N; j++) mx = fmaxf(mx, logit_at<LT>(x, j));
+    }
+    return wave_max_f32(mx);
+}
+
+// pass 2: T, lo = sum_{i<s} q_i, q_s and the positive minimum of the q1 table
+template <typename LT>
+__device__ inline RowSums q1_row_reduce(const LT *row, int64_t nvec, int64_t s, float m, const uint32_t *tab) {
+    constexpr int N = LogitN<LT>::N, U = LAC_UNROLL;
+    const int lane = (int)lane_id();
+    const int64_t V = nvec * N;
+    const int64_t sc = s < 0 ? 0 : (s > V ? V : s);
+    const int64_t sfull = sc / N;
+    const int sr = (int)(sc - sfull * N);
+    uint64_t tot = 0, lo = 0, ps = 0;
+    uint32_t mn = ~0u;
+    auto take = [&](const u32x4 &x, int64_t v) {
+        uint64_t sl = 0;
+        uint32_t qs[N];
+#pragma unroll
+        for (int j = 0; j < N; j++) {
+            qs[j] = q1_val(logit_at<LT>(x, j), m, tab);
+            sl += qs[j];
+            mn = qs[j] < mn ? qs[j] : mn;                     // q >= 1: the positive minimum
+        }
+        tot += sl;
+        if (v < sfull) lo += sl;
+        if (v == sfull) {
+#pragma unroll
+            for (int j = 0; j < N; j++) {
+                if (j < sr) lo += qs[j];
+                if (j == sr) ps = qs[j];
+            }
+        }
+    };
+    int64_t vi = lane;
+    for (; vi + 64 * (U - 1) < nvec; vi += 64 * U) {
+        u32x4 x[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) x[u] = ld16(row, vi + 64 * u, true);
+#pragma unroll
+        for (int u = 0; u < U; u++) take(x[u], vi + 64 * u);
+    }
+    for (; vi < nvec; vi += 64) take(ld16(row, vi, true), vi);
+    RowSums r;
+    r.T = wave_sum_u64(tot);
+    r.lo = wave_sum_u64(lo);
+    r.ps = wave_sum_u64(ps);
+    r.minp = wave_min_u32(mn);
+    return r;
+}
+
+template <typename LT>
+__global__ LAC_ENC_BOUNDS void k_encode_logits(const LT *__restrict__ lg, int64_t step_stride, int64_t stream_stride,
+                                               const int32_t *__restrict__ sym, int64_t B, int64_t nsteps,
+                                               int64_t V, int prec, uint32_t xsh, EncState *states,
+                                               uint64_t *planeA, uint64_t *planeC, uint64_t cap_words,
+                                               uint64_t *trace, uint64_t *nbits, int flags) {
+    __shared__ uint32_t tab[1024];
+    q1_load_tab(tab, xsh);
+    const int lane = (int)lane_id();
+    const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (b >= B) return;
+    EncState st = (flags & kReset) ? fresh_state(prec) : states[b];
+    uint64_t *pa = planeA + (uint64_t)b * cap_words, *pc = planeC + (uint64_t)b * cap_words;
+    if (st.err || st.nflush >= 0) {
+        if (!st.err && st.nflush >= 0 && nsteps > 0) { st.err = LAC_E_STATE; st.err_step = st.nsym; }
+        if (lane == 0) {
+            states[b] = st;
+            if (flags & kFinish) nbits[b] = st.err ? 0 : st.L;
+        }
+        return;
+    }
+    const int64_t nvec = V / LogitN<LT>::N;
+    int64_t l = st.l, h = st.h;
+    for (int64_t t = 0; t < nsteps; t++) {
+        const LT *row = lg + t * step_stride + b * stream_stride;
+        const int64_t s = sym[t * B + b];
+        const float m = q1_row_max<LT>(row, nvec);
+        const RowSums rs = q1_row_reduce<LT>(row, nvec, s, m, tab);
+        const uint64_t lo = (uint64_t)rs.lo;
+        if (!coder_step<uint32_t>(st, l, h, lo, lo + rs.ps, (uint64_t)rs.T, rs.minp, s, nullptr, V, prec, pa, pc,
+                                  cap_words, trace ? trace + 2 * (t * B + b) : nullptr, lane, LAC_MAP_CEIL, 0.0,
+                                  false))
+            break;
+    }
+    if (lane == 0) {
+        store_state(st, l, h, pa, pc, cap_words, &st);
+        if (flags & kFinish) finish_stream(st, pa, pc, cap_words, prec, &nbits[b], LAC_TERM_FLUSH);
+        states[b] = st;
+    }
+}
+
+// Decode from logits: one wave per stream, all steps in one launch (the q1
+// counterpart of k_decode_wave).
+template <typename LT>
+__global__ LAC_DEC_BOUNDS void k_decode_logits(const LT *__restrict__ lg, int64_t step_stride,
+                                               int64_t stream_stride, int64_t nsteps, int64_t V, int prec,
+                                               uint32_t xsh, DecState *states, const uint8_t *bits,
+                                               uint64_t stride, const uint64_t *nbits, int32_t *sym_out,
+                                               int64_t B) {
+    __shared__ uint32_t tab[1024];
+    q1_load_tab(tab, xsh);
+    constexpr int N = LogitN<LT>::N, U = LAC_UNROLL;
+    const int lane = (int)lane_id();
+    const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (b >= B) return;
+    DecState st = states[b];
+    const uint8_t *mybits = bits + b * stride;
+    const uint64_t mynbits = nbits[b];
+    const int64_t nvec = V / N, nit = (nvec + 63) / 64;
+    int64_t CI = (nit + 63) / 64;
+    CI = ((CI + U - 1) / U) * U;
+    const int64_t nch = (nit + CI - 1) / CI;
+    for (int64_t t = 0; t < nsteps; t++) {
+        int32_t *out = sym_out + t * B + b;
+        if (st.err) {
+            if (lane == 0) *out = -1;
+            continue;
+        }
+        const LT *row = lg + t * step_stride + b * stream_stride;
+        const float m = q1_row_max<LT>(row, nvec);
+        uint64_t mine = 0;
+        uint32_t mn = ~0u;
+        for (int64_t c = 0; c < nch; c++) {
+            uint64_t acc = 0;
+            for (int64_t g0 = 0; g0 < CI; g0 += U) {
+                u32x4 x[U];
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const int64_t vi = (c * CI + g0 + u) * 64 + lane;
+                    x[u] = vi < nvec ? ld16(row, vi, true) : u32x4{0, 0, 0, 0};
+                }
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const int64_t vi = (c * CI + g0 + u) * 64 + lane;
+                    if (vi < nvec) {
+#pragma unroll
+                        for (int j = 0; j < N; j++) {
+                            const uint32_t q = q1_val(logit_at<LT>(x[u], j), m, tab);
+                            acc += q;
+                            mn = q < mn ? q : mn;
+                        }
+                    }
+                }
+            }
+            const uint64_t tsum = wave_sum_u64(acc);
+            if (lane == c) mine = tsum;
+        }
+        const uint64_t T = wave_sum_u64(mine);
+        const uint64_t incl = wave_incl_scan_u64(mine);
+        const uint64_t minp = wave_min_u32(mn);
+        int err = 0;
+        int64_t s = -1;
+        const int64_t l = st.l, h = st.h, x = st.x;
+        if (x < l || x > h) err = LAC_E_DECODE_RANGE;
+        const uint64_t w = (uint64_t)(h - l + 1), v = (uint64_t)(x - l);
+        if (!err && is_fudged(T, w, minp)) err = LAC_E_TABLE;       // impossible by the choice of k
+        if (!err) {
+            const uint64_t tgt = div_floor((u128)v * T, w);
+            const uint64_t ex = incl - mine;
+            const uint64_t mask = __ballot(lane < nch && ex <= tgt && tgt < incl);
+            if (!mask) err = LAC_E_DECODE_RANGE;
+            if (!err) {
+                const int src = __ffsll((unsigned long long)mask) - 1;
+                uint64_t cb = readlane_u64(ex, src);
+                const int64_t cv0 = (int64_t)src * CI * 64;
+                uint64_t lo_c = cb, hi_c = ~0ull, cnt = 0;
+                for (int64_t g = 0; g < CI; g++) {
+                    const int64_t vi = cv0 + g * 64 + lane;
+                    const u32x4 xv = vi < nvec ? ld16(row, vi, false) : u32x4{0, 0, 0, 0};
+                    uint64_t loc[N], ls = 0;
+#pragma unroll
+                    for (int j = 0; j < N; j++) {
+                        ls += vi < nvec ? q1_val(logit_at<LT>(xv, j), m, tab) : 0u;
+                        loc[j] = ls;
+                    }
+                    const uint64_t in = wave_incl_scan_u64(ls);
+                    const uint64_t exb = cb + in - ls;
+#pragma unroll
+                    for (int j = 0; j < N; j++) {
+                        const uint64_t ce = exb + loc[j];
+                        if (vi < nvec && ce <= tgt) { cnt++; lo_c = ce > lo_c ? ce : lo_c; }
+                        if (vi < nvec && ce > tgt) hi_c = ce < hi_c ? ce : hi_c;
+                    }
+                    cb += readlane_u64(in, 63);
+                    if (cb > tgt) break;
+                }
+                cnt = wave_sum_u64(cnt);
+                lo_c = wave_max_u64(lo_c);
+                hi_c = wave_min_u64(hi_c);
+                s = cv0 * N + (int64_t)cnt;
+                uint64_t a, bb;
+                unfudged_range(lo_c, hi_c, T, w, &a, &bb);
+                const uint64_t past = st.pos > mynbits ? st.pos - mynbits : 0;
+                const int u = past < (uint64_t)prec ? (int)past : prec;
+                const uint64_t vhi = v + ((1ull << u) - 1);
+                const bool det = vhi < w && div_floor((u128)vhi * T, w) < hi_c;
+                if (st.det && det) st.ndet++;
+                else st.det = 0;
+                err = decode_advance(st, a, bb, mybits, mynbits, prec);
+            }
+        }
+        if (err) {
+            st.err = err;
+            st.err_step = st.nsym;
+        }
+        if (lane == 0) *out = err ? -1 : (int32_t)s;
+    }
+    if (lane == 0) states[b] = st;
+}
+
+// Materialise q1 tables (for parity checks and for callers that want them).
+template <typename LT>
+__global__ __launch_bounds__(256) void k_quantize_logits(const LT *__restrict__ lg, int64_t step_stride,
+                                                         int64_t stream_stride, int64_t B, int64_t rows, int64_t V,
+                                                         uint32_t xsh, uint32_t *__restrict__ out) {
+    __shared__ uint32_t tab[1024];
+    q1_load_tab(tab, xsh);
+    constexpr int N = LogitN<LT>::N;
+    const int lane = (int)lane_id();
+    const int64_t r = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (r >= rows) return;
+    const LT *row = lg + (r / B) * step_stride + (r % B) * stream_stride;
+    const int64_t nvec = V / N;
+    const float m = q1_row_max<LT>(row, nvec);
+    uint32_t *o = out + r * V;
+    for (int64_t vi = lane; vi < nvec; vi += 64) {
+        const u32x4 x = ld16(row, vi, true);
+#pragma unroll
+        for (int j = 0; j < N; j++) o[vi * N + j] = q1_val(logit_at<LT>(x, j), m, tab);
+    }
+}
+
 }  // namespace
 
 // ====================================================================== C-ABI
@@ -950,7 +1261,7 @@ struct lac_ctx {
 };
 
 enum { KID_ROW_STATS = 0, KID_ENCODE = 1, KID_FINISH = 2, KID_DECODE = 3, KID_FUSED = 4, KID_DECODE_WAVE = 5,
-       KID_COUNT = 8 };
+       KID_ENCODE_LOGITS = 6, KID_DECODE_LOGITS = 7, KID_COUNT = 8 };
 
 static hipEvent_t ev_get(lac_ctx *c) {
     if (c->ev_next == c->ev_pool.size()) {
@@ -1130,6 +1441,29 @@ static int decode_dispatch(lac_ctx *c, const void *pmf, int64_t step_stride, int
                      : decode_launch<uint64_t, 1, 8>(c, (const uint64_t *)pmf, off, stream_stride, o, st);
         if (rc) return rc;
     }
+    return LAC_OK;
+}
+
+// ---- logits path host side
+static int q1_shift(lac_ctx *c, uint32_t *xsh) {
+    int cl = 0;
+    while (((int64_t)1 << cl) < c->V) cl++;                      // ceil(log2 V)
+    int k = c->prec - 1 - cl;
+    if (k > 31) k = 31;
+    if (k < 1) return fail(LAC_E_PREC, "prec %d leaves no q1 precision for vocab %lld", c->prec, (long long)c->V);
+    *xsh = (uint32_t)(31 - k);
+    return LAC_OK;
+}
+
+static int logits_check(lac_ctx *c, const void *lg, int type, int64_t step_stride, int64_t stream_stride,
+                        int64_t steps) {
+    if (type != LAC_LOGITS_BF16 && type != LAC_LOGITS_F32) return fail(LAC_E_ARG, "logit type %d", type);
+    if (steps < 0 || step_stride < 0 || stream_stride < 0) return fail(LAC_E_ARG, "negative size/stride");
+    const int n = type == LAC_LOGITS_BF16 ? 8 : 4;
+    if (steps > 0 && ((uintptr_t)lg % 16 || c->V % n || step_stride % n || stream_stride % n))
+        return fail(LAC_E_ARG, "logits rows must be 16-byte aligned with vocab and strides multiples of %d", n);
+    if (c->mapping != LAC_MAP_CEIL || c->term != LAC_TERM_FLUSH)
+        return fail(LAC_E_STATE, "the logits path codes with the CDFPredictor mapping and flush termination");
     return LAC_OK;
 }
 
@@ -1384,6 +1718,87 @@ int lac_decode_steps(lac_ctx *c, const void *pmf_dev, int64_t step_stride, int64
     if (steps == 0) return LAC_OK;
     HIPCHK(hipSetDevice(c->device));
     return decode_dispatch(c, pmf_dev, step_stride, stream_stride, steps, sym_out_dev, S(stream));
+}
+
+int lac_encode_logits_job(lac_ctx *c, const void *logits_dev, int logit_type, int64_t step_stride,
+                          int64_t stream_stride, const int32_t *sym_dev, int64_t steps, uint64_t *trace_dev,
+                          void *stream) {
+    if (!c || (steps > 0 && (!logits_dev || !sym_dev))) return fail(LAC_E_ARG, "NULL argument");
+    int rc = logits_check(c, logits_dev, logit_type, step_stride, stream_stride, steps);
+    uint32_t xsh = 0;
+    if (rc || (rc = q1_shift(c, &xsh))) return rc;
+    HIPCHK(hipSetDevice(c->device));
+    c->mode = 0;
+    hipStream_t st = S(stream);
+    const unsigned blocks = (unsigned)((c->B + kWavesPerBlock - 1) / kWavesPerBlock);
+    ProfScope ps(c, KID_ENCODE_LOGITS, st);
+    if (logit_type == LAC_LOGITS_BF16)
+        k_encode_logits<uint16_t><<<blocks, 64 * kWavesPerBlock, 0, st>>>(
+            (const uint16_t *)logits_dev, step_stride, stream_stride, sym_dev, c->B, steps, c->V, c->prec, xsh,
+            c->enc, c->planeA, c->planeC, c->cap_words, trace_dev, c->nbits, kReset | kFinish);
+    else
+        k_encode_logits<float><<<blocks, 64 * kWavesPerBlock, 0, st>>>(
+            (const float *)logits_dev, step_stride, stream_stride, sym_dev, c->B, steps, c->V, c->prec, xsh,
+            c->enc, c->planeA, c->planeC, c->cap_words, trace_dev, c->nbits, kReset | kFinish);
+    CHECK_LAUNCH();
+    return LAC_OK;
+}
+
+int lac_decode_logits_steps(lac_ctx *c, const void *logits_dev, int logit_type, int64_t step_stride,
+                            int64_t stream_stride, int64_t steps, int32_t *sym_out_dev, void *stream) {
+    if (!c || (steps > 0 && (!logits_dev || !sym_out_dev))) return fail(LAC_E_ARG, "NULL argument");
+    if (c->mode != 1) return fail(LAC_E_STATE, "call lac_decode_open first");
+    int rc = logits_check(c, logits_dev, logit_type, step_stride, stream_stride, steps);
+    uint32_t xsh = 0;
+    if (rc || (rc = q1_shift(c, &xsh))) return rc;
+    if (steps == 0) return LAC_OK;
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = S(stream);
+    const unsigned blocks = (unsigned)((c->B + kWavesPerBlock - 1) / kWavesPerBlock);
+    ProfScope ps(c, KID_DECODE_LOGITS, st);
+    if (logit_type == LAC_LOGITS_BF16)
+        k_decode_logits<uint16_t><<<blocks, 64 * kWavesPerBlock, 0, st>>>(
+            (const uint16_t *)logits_dev, step_stride, stream_stride, steps, c->V, c->prec, xsh, c->dec, c->dbits,
+            c->dstride, c->dnbits, sym_out_dev, c->B);
+    else
+        k_decode_logits<float><<<blocks, 64 * kWavesPerBlock, 0, st>>>(
+            (const float *)logits_dev, step_stride, stream_stride, steps, c->V, c->prec, xsh, c->dec, c->dbits,
+            c->dstride, c->dnbits, sym_out_dev, c->B);
+    CHECK_LAUNCH();
+    return LAC_OK;
+}
+
+int lac_quantize_logits(lac_ctx *c, const void *logits_dev, int logit_type, int64_t step_stride,
+                        int64_t stream_stride, int64_t steps, uint32_t *pmf_out_dev, void *stream) {
+    if (!c || (steps > 0 && (!logits_dev || !pmf_out_dev))) return fail(LAC_E_ARG, "NULL argument");
+    if (logit_type != LAC_LOGITS_BF16 && logit_type != LAC_LOGITS_F32) return fail(LAC_E_ARG, "logit type");
+    const int n = logit_type == LAC_LOGITS_BF16 ? 8 : 4;
+    if (steps < 0 || step_stride < 0 || stream_stride < 0) return fail(LAC_E_ARG, "negative size/stride");
+    if (steps > 0 && ((uintptr_t)logits_dev % 16 || c->V % n || step_stride % n || stream_stride % n))
+        return fail(LAC_E_ARG, "logits rows must be 16-byte aligned with vocab and strides multiples of %d", n);
+    uint32_t xsh = 0;
+    int rc = q1_shift(c, &xsh);
+    if (rc) return rc;
+    if (steps == 0) return LAC_OK;
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = S(stream);
+    const int64_t rows = steps * c->B;
+    const unsigned blocks = (unsigned)((rows + kWavesPerBlock - 1) / kWavesPerBlock);
+    if (logit_type == LAC_LOGITS_BF16)
+        k_quantize_logits<uint16_t><<<blocks, 64 * kWavesPerBlock, 0, st>>>(
+            (const uint16_t *)logits_dev, step_stride, stream_stride, c->B, rows, c->V, xsh, pmf_out_dev);
+    else
+        k_quantize_logits<float><<<blocks, 64 * kWavesPerBlock, 0, st>>>(
+            (const float *)logits_dev, step_stride, stream_stride, c->B, rows, c->V, xsh, pmf_out_dev);
+    CHECK_LAUNCH();
+    return LAC_OK;
+}
+
+int lac_q1_k(int prec, int64_t vocab) {
+    int cl = 0;
+    while (((int64_t)1 << cl) < vocab) cl++;
+    const int k = prec - 1 - cl;
+    return k > 31 ? 31 : k;
 }
 
 int lac_decode_determined(lac_ctx *c, int64_t *ndet_host, void *stream) {

@@ -20,10 +20,16 @@
  * Status codes mirror include/lac.h (the product header is not included so that
  * the oracle stays independent of the thing it checks).
  */
+#include <math.h>
 #include <pthread.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+
+/* The q1 exp2 table is a format constant (the quantiser's definition), shared
+ * with the product; the arithmetic below is an independent restatement. */
+#include "../include/lac_q1_table.h"
+static const uint32_t Q1_TAB[1024] = LAC_Q1_TAB_INIT;
 
 typedef unsigned __int128 u128;
 typedef __int128 i128;
@@ -330,4 +336,43 @@ int lacref_acsampler_encode(const uint64_t *cdf, int64_t V, const int32_t *toks,
     return R_OK;
 #undef ACS_OUT
 #undef ACS_FLUSH
+}
+
+/* ---- q1 logits quantiser (DESIGN.md "logits path"): bf16 (type 1) or f32 (type 2)
+ * logits -> uint32 pmf.  m = max (fmaxf), d = m - x (f32), u = floor(d * 2^16)
+ * saturating at 2^31 - 1 (NaN too), e = u * round(log2 e * 2^16) (Q32),
+ * q = max(1, TAB[frac10(e)] >> (int(e) + 31 - k)), k = min(31, prec-1-ceil(log2 V)). */
+static inline float q1_load(const void *x, int type, int64_t i) {
+    if (type == 1) {
+        uint32_t u = (uint32_t)((const uint16_t *)x)[i] << 16;
+        float f;
+        memcpy(&f, &u, 4);
+        return f;
+    }
+    return ((const float *)x)[i];
+}
+
+int lacref_q1_k(int prec, int64_t V) {
+    int cl = 0;
+    while (((int64_t)1 << cl) < V) cl++;
+    int k = prec - 1 - cl;
+    if (k > 31) k = 31;
+    return k;
+}
+
+int lacref_q1_quantize(const void *x, int type, int64_t V, int prec, uint32_t *q) {
+    const int k = lacref_q1_k(prec, V);
+    if (k < 1 || (type != 1 && type != 2)) return R_E_ARG;
+    float m = -INFINITY;
+    for (int64_t i = 0; i < V; i++) m = fmaxf(m, q1_load(x, type, i));
+    for (int64_t i = 0; i < V; i++) {
+        volatile float d = m - q1_load(x, type, i);
+        uint32_t u = (d < 32767.0f) ? (uint32_t)(d * 65536.0f) : 0x7FFFFFFFu;
+        uint64_t e = (uint64_t)u * LAC_Q1_LOG2E_Q16;
+        uint32_t ip = (uint32_t)(e >> 32), fr = (uint32_t)(e >> 22) & 1023u;
+        uint32_t sh = ip + (uint32_t)(31 - k);
+        uint32_t v = sh >= 32 ? 0u : (Q1_TAB[fr] >> sh);
+        q[i] = v ? v : 1u;
+    }
+    return R_OK;
 }

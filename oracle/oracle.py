@@ -40,6 +40,10 @@ def lib():
         L.lacref_decode.restype = C.c_int
         L.lacref_decode.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.c_int64, C.c_int64, C.c_void_p,
                                     C.c_uint64, C.c_int, C.c_void_p]
+        L.lacref_q1_quantize.restype = C.c_int
+        L.lacref_q1_quantize.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.c_int, C.c_void_p]
+        L.lacref_q1_k.restype = C.c_int
+        L.lacref_q1_k.argtypes = [C.c_int, C.c_int64]
         L.lacref_acsampler_encode.restype = C.c_int
         L.lacref_acsampler_encode.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_int,
                                               C.c_void_p, C.c_uint64, C.c_void_p]
@@ -128,3 +132,20 @@ def acsampler_encode(cdf, tokens, prec=48):
     if rc:
         raise OracleError(rc)
     return out[:int(n[0])].tolist()
+
+
+def q1_quantize(logits, prec):
+    """q1 quantiser (C oracle) over rows of bf16 (numpy uint16 bit patterns) or
+    float32 logits, any leading shape -> uint32 pmf of the same shape."""
+    x = np.ascontiguousarray(logits)
+    typ = 1 if x.dtype == np.uint16 else 2
+    if typ == 2:
+        x = x.astype(np.float32)
+    V = x.shape[-1]
+    flat = x.reshape(-1, V)
+    out = np.zeros(flat.shape, dtype=np.uint32)
+    for r in range(flat.shape[0]):
+        rc = lib().lacref_q1_quantize(_ptr(flat[r]), typ, V, prec, _ptr(out[r]))
+        if rc:
+            raise OracleError(rc)
+    return out.reshape(x.shape)

@@ -1,0 +1,176 @@
+"""Logits path on the GPU vs the C oracle.
+
+The oracle side is ``oracle.q1_quantize`` (C restatement of the q1 quantiser,
+itself checked against an independent numpy restatement in
+tests/test_q1_quantiser.py) followed by ``oracle.encode_batch`` (the literal
+restatement of CDFPredictor + A_to_bin, pinned to the reference's golden
+vectors).  Everything is bit-exact: tables, bytes, lengths, traces, decodes.
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _coder(V, B, prec, cap=None):
+    from lac_amd.batch import BatchCoder
+    return BatchCoder(V, B, prec=prec, pmf_bits=32, capacity_bits=cap, device=DEV)
+
+
+def _logits(seed, steps, B, V, scale=3.0, specials=False):
+    """Normal logits with a few sharp peaks (LLM-like), f32 host array."""
+    rng = np.random.default_rng(seed)
+    x = (rng.standard_normal((steps, B, V)) * scale).astype(np.float32)
+    hot = rng.integers(0, V, size=(steps, B))
+    np.put_along_axis(x, hot[..., None], np.float32(scale * 6), axis=2)
+    if specials and V >= 16:
+        x[0, 0, :3] = [np.nan, -np.inf, 1e30]
+        if B > 1:
+            x[0, 1, :] = -np.inf                                  # all -inf row: uniform table
+        if steps > 1:
+            x[1, 0, 5] = np.inf                                   # +inf max: every other entry 1
+    return x
+
+
+def _device_logits(x, dtype):
+    t = torch.from_numpy(x).to(DEV)
+    return t.to(torch.bfloat16) if dtype == "bf16" else t
+
+
+def _host_bits(t):
+    """The exact logits the GPU sees, for the oracle (bf16 as uint16 patterns)."""
+    if t.dtype == torch.bfloat16:
+        return t.view(torch.int16).cpu().numpy().view(np.uint16)
+    return t.cpu().numpy()
+
+
+def _sample(pmf, seed):
+    """Symbols drawn from the tables themselves (inverse CDF), int32 [steps, B]."""
+    rng = np.random.default_rng(seed)
+    c = np.cumsum(pmf.astype(np.uint64), axis=-1)
+    r = (rng.random(pmf.shape[:-1]) * c[..., -1]).astype(np.uint64)
+    s = np.empty(pmf.shape[:-1], dtype=np.int32)
+    for idx in np.ndindex(*pmf.shape[:-1]):
+        s[idx] = np.searchsorted(c[idx], r[idx], side="right")
+    return np.minimum(s, pmf.shape[-1] - 1).astype(np.int32)
+
+
+CASES = [
+    # V, B, steps, prec, dtype
+    (32000, 64, 8, 48, "bf16"),
+    (32000, 64, 8, 48, "f32"),
+    (1000, 40, 30, 40, "f32"),
+    (1000, 40, 30, 40, "bf16"),
+    (128256, 8, 4, 48, "bf16"),
+    (24, 5, 50, 24, "f32"),
+    (4096, 2048, 3, 48, "bf16"),
+]
+
+
+@pytest.mark.parametrize("V,B,steps,prec,dtype", CASES)
+def test_logits_encode_decode_vs_oracle(V, B, steps, prec, dtype):
+    from oracle import oracle as coracle
+    x = _logits(V + B + prec, steps, B, V, specials=True)
+    dl = _device_logits(x, dtype)
+    c = _coder(V, B, prec, cap=steps * (prec + 2) + 256)
+    # tables
+    want_pmf = coracle.q1_quantize(_host_bits(dl), prec)
+    got_pmf = c.quantize_logits(dl).cpu().numpy().view(np.uint32)
+    assert (got_pmf == want_pmf).all()
+    k = c.q1_k()
+    assert want_pmf.max() <= 1 << k and want_pmf.min() >= 1
+    # encode
+    sym = _sample(want_pmf, V + 1)
+    trace = torch.zeros((steps, B, 2), dtype=torch.int64, device=DEV)
+    c.encode_logits_job(dl, torch.from_numpy(sym).to(DEV), trace=trace)
+    data, n = c.to_bytes()
+    out, nb, status, rc = coracle.encode_batch(want_pmf, sym, prec, nthreads=16)
+    assert rc == 0 and not status.any()
+    for b in range(B):
+        assert int(n[b]) == int(nb[b]), b
+        assert data[b] == out[b, :(int(nb[b]) + 7) // 8].tobytes(), b
+    # the same tables through the pmf path give the same trace and bits
+    c2 = _coder(V, B, prec, cap=steps * (prec + 2) + 256)
+    trace2 = torch.zeros_like(trace)
+    c2.encode_job(torch.from_numpy(want_pmf.view(np.int32)).to(DEV), torch.from_numpy(sym).to(DEV), trace=trace2)
+    assert torch.equal(trace, trace2)
+    # decode from logits (own bits), and from the oracle's bits
+    c.decode_open()
+    dec = c.decode_logits(dl).cpu().numpy()
+    assert (dec == sym).all()
+    stride = (out.shape[1] + 7) // 8 * 8
+    buf = np.zeros((B, stride), dtype=np.uint8)
+    buf[:, :out.shape[1]] = out
+    c.decode_open(torch.from_numpy(buf).to(DEV), torch.from_numpy(nb.astype(np.int64)).to(DEV))
+    assert (c.decode_logits(dl).cpu().numpy() == sym).all()
+    assert (c.determined() <= steps).all()
+    c.raise_on_error()
+
+
+def test_logits_headline_shape_matches_pmf_path():
+    """Full c3 shape (V=32000, B=4096): fused logits kernel == quantise + pmf kernel."""
+    V, B, steps, prec = 32000, 4096, 3, 48
+    g = torch.Generator(device=DEV).manual_seed(3)
+    dl = (torch.randn((steps, B, V), device=DEV, generator=g) * 3).to(torch.bfloat16)
+    c = _coder(V, B, prec)
+    pmf = c.quantize_logits(dl)
+    sym = torch.randint(0, V, (steps, B), device=DEV, generator=g, dtype=torch.int32)
+    c.encode_logits_job(dl, sym)
+    a, na = c.to_bytes()
+    c2 = _coder(V, B, prec)
+    c2.encode_job(pmf, sym)
+    b, nb = c2.to_bytes()
+    assert (na == nb).all() and a == b
+    c.decode_open()
+    assert torch.equal(c.decode_logits(dl), sym)
+
+
+def test_logits_broadcast_and_strides():
+    """A stride-0 step broadcast and a padded stream stride give the same bits."""
+    from oracle import oracle as coracle
+    V, B, steps, prec = 512, 16, 12, 40
+    x = _logits(9, 1, B, V)
+    pad = torch.zeros((B, V + 64), dtype=torch.float32, device=DEV)
+    pad[:, :V] = torch.from_numpy(x[0]).to(DEV)
+    row = pad[:, :V].unsqueeze(0).expand(steps, B, V)              # step stride 0, stream stride V+64
+    want = coracle.q1_quantize(x[0], prec)
+    sym = np.stack([_sample(want, s) for s in range(steps)])
+    c = _coder(V, B, prec)
+    c.encode_logits_job(row, torch.from_numpy(sym).to(DEV))
+    data, n = c.to_bytes()
+    out, nb, _, rc = coracle.encode_batch(np.broadcast_to(want, (steps, B, V)).copy(), sym, prec, nthreads=8)
+    assert rc == 0
+    assert [out[b, :(int(nb[b]) + 7) // 8].tobytes() for b in range(B)] == data
+    c.decode_open()
+    assert (c.decode_logits(row).cpu().numpy() == sym).all()
+
+
+def test_logits_errors():
+    from lac_amd._lib import LacError, LAC_E_ARG, LAC_E_STATE, LAC_E_PREC, LAC_E_SYMBOL_RANGE
+    from lac_amd.batch import StreamError
+    c = _coder(1004, 4, 40)                                        # 1004 % 8 != 0
+    bf = torch.zeros((2, 4, 1004), dtype=torch.bfloat16, device=DEV)
+    with pytest.raises(LacError) as e:
+        c.encode_logits_job(bf, torch.zeros((2, 4), dtype=torch.int32, device=DEV))
+    assert e.value.code == LAC_E_ARG
+    f = torch.zeros((2, 4, 1004), dtype=torch.float32, device=DEV)  # f32 needs V % 4 == 0: fine
+    c.encode_logits_job(f, torch.tensor([[0, 1, 2, 1003], [5, 6, 7, 8]], dtype=torch.int32, device=DEV))
+    c.raise_on_error()
+    c.set_mapping("floor")
+    with pytest.raises(LacError) as e:
+        c.encode_logits_job(f, torch.zeros((2, 4), dtype=torch.int32, device=DEV))
+    assert e.value.code == LAC_E_STATE
+    c.set_mapping("ceil")
+    c.encode_logits_job(f, torch.tensor([[0, 1, 1004, 1], [5, -1, 7, 8]], dtype=torch.int32, device=DEV))
+    with pytest.raises(StreamError) as e:
+        c.raise_on_error()
+    assert e.value.code == LAC_E_SYMBOL_RANGE
+    assert list(e.value.err != 0) == [False, True, True, False]
+    tight = _coder(1 << 20, 1, 22)                                 # prec-1-ceil(log2 V) = 1: ok
+    assert tight.q1_k() == 1
+    with pytest.raises(LacError) as e:
+        _coder(1 << 20, 1, 21).quantize_logits(torch.zeros((1, 1, 1 << 20), device=DEV))
+    assert e.value.code == LAC_E_PREC
