@@ -62,6 +62,9 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-streams", type=int, default=0, help="oracle sample streams (0 = all)")
     ap.add_argument("--path", default="auto", choices=("auto", "split", "fused"), help="encode kernel path")
+    ap.add_argument("--q1-shape", type=int, default=0, help="logits row-stats block shape (tuning)")
+    ap.add_argument("--input", default="pmf", choices=("pmf", "logits-bf16", "logits-f32"),
+                    help="pmf rows (BASELINE c3, default) or raw logits quantised in-kernel (q1, SURVEY §8(f)1)")
     args = ap.parse_args()
 
     import ctypes as C
@@ -84,20 +87,32 @@ def main():
     from lac_amd.dist import gather_bitstreams
 
     V, B, T, P = args.vocab, args.streams, args.tokens, args.prec
-    ebytes = args.pmf_bits // 8
+    logits_in = args.input != "pmf"
+    ebytes = args.pmf_bits // 8 if not logits_in else (2 if args.input == "logits-bf16" else 4)
     t_gen = time.time()
-    pmf, sym = synth.softmax_tables(T, B, V, seed=1234 + 7919 * rank, device=dev,
-                                    scale_bits=31 if args.pmf_bits == 32 else 60)
-    torch.cuda.synchronize()
-    log(f"[rank {rank}] tables {tuple(pmf.shape)} {pmf.dtype} ({pmf.numel() * ebytes / 2**30:.2f} GiB) "
-        f"in {time.time() - t_gen:.1f}s")
     coder = BatchCoder(V, B, prec=P, pmf_bits=args.pmf_bits, capacity_bits=T * (P + 2) + 256, device=dev)
+    if logits_in:
+        logits, sym = synth.logits_batch(T, B, V, seed=1234 + 7919 * rank, device=dev,
+                                         dtype=torch.bfloat16 if ebytes == 2 else torch.float32,
+                                         quantise=coder.quantize_logits)
+        pmf = logits
+    else:
+        pmf, sym = synth.softmax_tables(T, B, V, seed=1234 + 7919 * rank, device=dev,
+                                        scale_bits=31 if args.pmf_bits == 32 else 60)
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] inputs {tuple(pmf.shape)} {pmf.dtype} ({pmf.numel() * ebytes / 2**30:.2f} GiB) "
+        f"in {time.time() - t_gen:.1f}s")
 
     if args.path != "auto":
         coder.set_path(args.path)
+    if args.q1_shape:
+        coder.set_q1_shape(args.q1_shape)
 
     def job():
-        coder.encode_job(pmf, sym)
+        if logits_in:
+            coder.encode_logits_job(pmf, sym)
+        else:
+            coder.encode_job(pmf, sym)
         if world > 1:
             return gather_bitstreams(coder.bits_tensor(), coder.nbits_tensor())
         return None
@@ -130,23 +145,26 @@ def main():
     # ---------------- checks, outside the timed region
     rc, err, err_step = coder.status()
     data, nbits = coder.to_bytes() if rc == 0 else ([], None)
+    decode = coder.decode_logits if logits_in else coder.decode
     coder.decode_open()
-    dec = coder.decode(pmf)                                # warm
+    dec = decode(pmf)                                      # warm
     torch.cuda.synchronize()
     coder.lib.lac_profile_read(coder.ctx, None, None, 1)
     coder.lib.lac_profile_enable(coder.ctx, 1)
     d0 = time.perf_counter()
     coder.decode_open()
-    dec = coder.decode(pmf)
+    dec = decode(pmf)
     torch.cuda.synchronize()
     d1 = time.perf_counter()
     coder.lib.lac_profile_enable(coder.ctx, 0)
     dms = (C.c_double * 8)()
     dcnt = (C.c_int64 * 8)()
     coder.lib.lac_profile_read(coder.ctx, C.cast(dms, C.c_void_p), C.cast(dcnt, C.c_void_p), 1)
-    dkid = 5 if dcnt[5] else 3                            # decode_wave (one launch per call) or decode_step
-    dstep_ms = dms[dkid] / (T if dkid == 5 else max(dcnt[dkid], 1))
-    decode_info = {"symbols_per_s": B * T / (d1 - d0), "kernel": "k_decode_wave" if dkid == 5 else "k_decode_step",
+    dkid = 7 if dcnt[7] else (5 if dcnt[5] else 3)       # q1_decode(+q1_stats) / decode_wave / decode_step
+    dk_ms = dms[dkid] + (dms[6] if dkid == 7 else 0.0)
+    dstep_ms = dk_ms / (T if dkid in (5, 7) else max(dcnt[dkid], 1))
+    decode_info = {"symbols_per_s": B * T / (d1 - d0),
+                   "kernel": {7: "k_q1_stats+k_q1_decode", 5: "k_decode_wave", 3: "k_decode_step"}[dkid],
                    "kernel_ms_per_step": dstep_ms,
                    "achieved_GBps": B * (V * ebytes + 4) / (dstep_ms * 1e-3) / 1e9 if dcnt[dkid] else None}
     round_trip = bool(torch.equal(dec, sym)) and rc == 0
@@ -162,41 +180,52 @@ def main():
         S = B if (args.cpu_streams <= 0 or args.cpu_streams > B) else args.cpu_streams
         if world > 1:
             S = min(S, 256)
-        host = pmf[:, :S, :].cpu().numpy()
-        host = host.view(np.uint32) if args.pmf_bits == 32 else host.view(np.uint64)
+        if logits_in:
+            S = min(S, 512) if args.cpu_streams <= 0 else S          # q1 oracle is per-row, single-threaded
+            host = pmf[:, :S, :].contiguous()
+            host = host.view(torch.int16).cpu().numpy().view(np.uint16) if ebytes == 2 else host.cpu().numpy()
+        else:
+            host = pmf[:, :S, :].cpu().numpy()
+            host = host.view(np.uint32) if args.pmf_bits == 32 else host.view(np.uint64)
         hsym = sym[:, :S].cpu().numpy()
         nthreads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
         c0 = time.perf_counter()
+        if logits_in:
+            host = coracle.q1_quantize(host, P)
         out, onb, ost, orc = coracle.encode_batch(host, hsym, P, nthreads=nthreads)
         c1 = time.perf_counter()
         exact = orc == 0 and rc == 0 and all(
             int(onb[b]) == int(nbits[b]) and out[b, :(int(onb[b]) + 7) // 8].tobytes() == data[b] for b in range(S))
         parity.update({"oracle_streams_checked": S, "bit_exact_vs_oracle": bool(exact)})
         if world == 1 and args.cpu_baseline == "on":
+            what = "q1 quantise (1 thread) + encode" if logits_in else "encode"
             cpu = {"value": S * T / (c1 - c0), "unit": "symbols/s", "cores": nthreads, "kind": "port",
-                   "sample": f"C oracle (oracle/lac_oracle.c) on {S} streams x {T} symbols of the same tables, "
-                             f"{nthreads} threads, {c1 - c0:.2f}s"}
+                   "sample": f"C oracle (oracle/lac_oracle.c) {what} on {S} streams x {T} symbols of the same "
+                             f"inputs, {nthreads} threads, {c1 - c0:.2f}s"}
         avg_bits = float(np.mean(nbits.astype(np.float64))) / T if nbits is not None else None
         parity["bits_per_symbol"] = avg_bits
 
     if rank == 0:
-        kid = 4 if cnt[4] else 0                            # encode_fused, else row_stats
-        kname = "k_encode_fused" if kid == 4 else "k_row_stats"
+        kid = 6 if cnt[6] else (4 if cnt[4] else 0)        # q1_stats, encode_fused, else row_stats
+        kname = {6: "k_q1_stats", 4: "k_encode_fused", 0: "k_row_stats"}[kid]
         units = T * B * args.steps / max(cnt[kid], 1)       # symbols per launch of that kernel
         rs_launch_ms = ms[kid] / max(cnt[kid], 1)
         alg_bytes = units * (V * ebytes + 4)
         achieved = alg_bytes / (rs_launch_ms * 1e-3) / 1e9 if cnt[kid] else None
-        cfg = {"workload": f"c3: vocab={V}, {B} streams/GPU, {T} symbols/stream per job, prec={P}, "
-                           f"uint{args.pmf_bits} pmf rows",
-               "vocab": V, "streams": B, "tokens": T, "prec": P, "pmf_bits": args.pmf_bits,
+        rows = (f"{args.input[7:]} logit rows, q1 tables in-kernel" if logits_in else f"uint{args.pmf_bits} pmf rows")
+        cfg = {"workload": f"c3: vocab={V}, {B} streams/GPU, {T} symbols/stream per job, prec={P}, {rows}",
+               "vocab": V, "streams": B, "tokens": T, "prec": P, "pmf_bits": args.pmf_bits, "input": args.input,
                "parallelism": f"streams sharded over {world} GPU(s)" + (", RCCL bitstream all-gather" if world > 1 else "")}
         value = world * B * T * args.steps / dt
         line = {
             "metric": METRIC, "value": value, "unit": "symbols/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": f"u{args.pmf_bits}",
-            "data": "synthetic: logits 3*N(0,1) per step (torch.Generator seeded 1234+t), "
-                    f"pmf=max(1,floor(softmax*2^{31 if args.pmf_bits == 32 else 60})), symbols by inverse CDF",
+            "scaling": "weak", "vs_baseline": None,
+            "dtype": ("u32" if logits_in else f"u{args.pmf_bits}"),
+            "data": ("synthetic: logits 3*N(0,1) (torch.Generator seeded), symbols by inverse CDF of their q1 tables"
+                     if logits_in else
+                     "synthetic: logits 3*N(0,1) per step (torch.Generator seeded 1234+t), "
+                     f"pmf=max(1,floor(softmax*2^{31 if args.pmf_bits == 32 else 60})), symbols by inverse CDF"),
             "config": cfg,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
@@ -204,7 +233,8 @@ def main():
                          "kernel_ms_per_launch": rs_launch_ms, "launches": int(cnt[kid]),
                          "bytes_per_launch": alg_bytes,
                          "kernel_ms_per_step": {n: ms[i] / args.steps for n, i in
-                                                (("row_stats", 0), ("encode", 1), ("finish", 2), ("encode_fused", 4))
+                                                (("row_stats", 0), ("encode", 1), ("finish", 2), ("encode_fused", 4),
+                                                 ("q1_stats", 6))
                                                 if cnt[i]}},
             "cpu_baseline": cpu,
             "parity": parity,

@@ -67,9 +67,13 @@ enum {                       /* lac_set_option */
     LAC_OPT_FUSED_MIN_STREAMS = 2, /* AUTO picks the fused kernel from this many streams (2048) */
     LAC_OPT_MAPPING = 3,           /* LAC_MAP_*: how a symbol's CDF range maps onto [l, h] */
     LAC_OPT_TERMINATION = 4,       /* LAC_TERM_*: how a stream is closed */
-    LAC_OPT_DECODE_PATH = 5        /* LAC_PATH_*: SPLIT = one 4-wave workgroup per stream and step,
+    LAC_OPT_DECODE_PATH = 5,       /* LAC_PATH_*: SPLIT = one 4-wave workgroup per stream and step,
                                       FUSED = one wave per stream, all steps of a call in one launch;
                                       AUTO = FUSED from 1024 streams */
+    LAC_OPT_Q1_SHAPE = 6           /* logits path row-stats shape: 0 = auto (default), 1..7 = (waves per
+                                      row, vectors/thread, prefetch) (1,4,n) (2,8,n) (4,8,n) (8,8,n)
+                                      (8,8,y) (8,4,y) (4,8,y), 8 = tiles of (8,8,n); identical results,
+                                      only speed differs */
 };
 enum {
     LAC_MAP_CEIL = 0,              /* CDFPredictor.symbol_to_range + fudged_dist (arith_code.py:83-110) */
@@ -173,10 +177,11 @@ int lac_decode_steps(lac_ctx *ctx, const void *pmf_dev, int64_t step_stride, int
 /* ---- logits path --------------------------------
  * Tables are computed in-kernel from raw logits with the integer-exact "q1"
  * quantiser instead of being read from a pmf in HBM: for each row
- *   m = max_i x_i,  q_i = max(1, floor(2^k * 2^(-(m - x_i) * log2 e)))
- * evaluated with a 16.16 fixed-point exponent and a 1024-entry 2^-j/1024 table
- * (include/lac_q1_table.h; bit-exact spec in DESIGN.md "logits path"), with
- * k = lac_q1_k(prec, vocab) = min(31, prec - 1 - ceil(log2 vocab)) so that
+ *   m = max_i x_i (NaN ignored),  d_i = min(m - x_i, 17) in f32 (NaN -> 17),
+ *   q_i = max(1, TAB[floor(32 d_i)] >> (24 - k)),  TAB[i] = round(2^24 e^(-i/32))
+ * i.e. softmax to 1/32-nat resolution (include/lac_q1_table.h; DESIGN.md
+ * "logits path"), with
+ * k = lac_q1_k(prec, vocab) = min(24, prec - 1 - ceil(log2 vocab)) so that
  * T <= 2^(prec-1) and no row is ever fudged.  It replaces the float64 numpy
  * quantiser of llama_compress.py:29-36 (whose output is platform-dependent)
  * with a rule both the GPU and the C oracle reproduce bit for bit; the coder
@@ -189,7 +194,7 @@ int lac_decode_steps(lac_ctx *ctx, const void *pmf_dev, int64_t step_stride, int
 
 int lac_q1_k(int prec, int64_t vocab);
 
-/* reset + encode `steps` symbols per stream from logits + finish, one launch
+/* reset + encode `steps` symbols per stream from logits + finish
  * (logits[t*step_stride + b*stream_stride + i], sym_dev[t*streams + b]). */
 int lac_encode_logits_job(lac_ctx *ctx, const void *logits_dev, int logit_type, int64_t step_stride,
                           int64_t stream_stride, const int32_t *sym_dev, int64_t steps, uint64_t *trace_dev,
@@ -212,7 +217,7 @@ int lac_decode_determined(lac_ctx *ctx, int64_t *ndet_host, void *stream);
 /* Live kernel timing: with profiling on, every kernel launch is bracketed by
  * hipEvents recorded on its own stream.  lac_profile_read synchronises and
  * returns, per kernel id (0 row_stats, 1 encode, 2 finish, 3 decode_step,
- * 4 encode_fused, 5 decode_wave, 6 encode_logits, 7 decode_logits; 8 slots), the summed device milliseconds and the launch
+ * 4 encode_fused, 5 decode_wave, 6 q1_stats, 7 q1_decode; 8 slots), the summed device milliseconds and the launch
  * count; reset != 0 clears. */
 int lac_profile_enable(lac_ctx *ctx, int on);
 int lac_profile_read(lac_ctx *ctx, double *ms_total /*[8]*/, int64_t *launches /*[8]*/, int reset);

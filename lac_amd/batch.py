@@ -336,6 +336,10 @@ class BatchCoder:
                                            C.c_void_p(out.data_ptr()), self._stream))
         return out
 
+    def set_q1_shape(self, shape: int):
+        """Logits row-stats block shape (0 auto, 1..7 forced; identical results)."""
+        check(self.lib.lac_set_option(self.ctx, _lib.LAC_OPT_Q1_SHAPE, int(shape)))
+
     def q1_k(self):
         """The q1 table scale: max entry 2^k, k = min(31, prec - 1 - ceil(log2 V))."""
         return int(self.lib.lac_q1_k(self.prec, self.vocab))

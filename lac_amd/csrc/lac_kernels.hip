@@ -421,7 +421,8 @@ __global__ __launch_bounds__(256) void k_encode(const RowStats *__restrict__ sta
                                                 int64_t B, int64_t t0, int64_t nsteps, const E *pmf,
                                                 int64_t step_stride, int64_t stream_stride, int64_t V, int prec,
                                                 EncState *states, uint64_t *planeA, uint64_t *planeC,
-                                                uint64_t cap_words, uint64_t *trace, int mapping) {
+                                                uint64_t cap_words, uint64_t *trace, int mapping,
+                                                bool allow_fudge) {
     const int lane = (int)lane_id();
     const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
     if (b >= B) return;
@@ -450,7 +451,7 @@ __global__ __launch_bounds__(256) void k_encode(const RowStats *__restrict__ sta
             const E *row = pmf + t * step_stride + b * stream_stride;
             if (!coder_step<E>(st, l, h, lo, hi, T, minp, s, row, V, prec, pa, pc, cap_words,
                                trace ? trace + 2 * (t * B + b) : nullptr, lane, mapping,
-                               __builtin_bit_cast(double, invb))) {
+                               __builtin_bit_cast(double, invb), allow_fudge)) {
                 ok = false;
                 break;
             }
@@ -927,7 +928,11 @@ __global__ LAC_DEC_BOUNDS void k_decode_wave(const E *__restrict__ pmf, int64_t 
 // quantiser (include/lac_q1_table.h, DESIGN.md "logits path"), so the pmf never
 // exists in HBM.  Per step: pass 1 = row max, pass 2 = quantise + the usual
 // reductions (the row is re-read while it is still resident in the 256 MB MALL).
-__constant__ uint32_t c_q1_tab[1024] = LAC_Q1_TAB_INIT;
+__constant__ uint32_t c_q1_tab[LAC_Q1_TAB_SIZE] = LAC_Q1_TAB_INIT;
+
+#ifndef LAC_Q1_NT
+#define LAC_Q1_NT 1              // logits rows are read once: nontemporal loads
+#endif
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -948,29 +953,78 @@ __device__ inline u32x4 ld16(const void *row, int64_t vi, bool nt) {
     return nt ? __builtin_nontemporal_load(p) : *p;
 }
 
-// q1 on the GPU, bit-identical to the spec in include/lac_q1_table.h for every
-// float input (NaN and +-inf included):
-//  * tab[] = LAC_Q1_TAB >> (31 - k) (per launch, in LDS): shifts compose exactly
-//    under floor, so tab[fr] >> ip == LAC_Q1_TAB[fr] >> (ip + 31 - k);
-//  * d is clamped at 255 (NaN -> 255): every d >= 255 has ip >= 367 and q = 1 in
-//    the spec, and so does the clamped value; u = d * 2^16 < 2^24, so the Q32
-//    exponent u * log2(e) is two full-rate 24-bit multiplies;
-//  * ip >= 32 gives 0 in the spec; min(ip, 31) leaves tab[fr] >> 31 <= 1
-//    (tab[] <= 2^31), which the final max(q, 1) turns into the same 1.
+// q1 on the GPU (spec: include/lac_q1_table.h).  tab[] is the per-launch LDS
+// copy of max(1, LAC_Q1_TAB[i] >> (KMAX - k)), so one lookup is the whole map;
+// fminf returns DMAX for a NaN difference, as the spec's clamp does; d * STEPS is
+// exact and d >= 0, so the conversion is the floor.
 __device__ inline uint32_t q1_val(float x, float m, const uint32_t *tab) {
-    const float d = fminf(m - x, 255.0f);
-    const uint32_t u = (uint32_t)(d * 65536.0f) & 0xFFFFFFu;
-    const uint64_t e = (uint64_t)u * (uint64_t)LAC_Q1_LOG2E_Q16;
-    const uint32_t ip = (uint32_t)(e >> 32), fr = (uint32_t)e >> 22;
-    const uint32_t q = tab[fr] >> (ip < 31u ? ip : 31u);
-    return q ? q : 1u;
+    const float d = fminf(m - x, (float)LAC_Q1_DMAX);
+    return tab[(uint32_t)(d * (float)LAC_Q1_STEPS)];
+}
+
+__device__ inline uint32_t q1_entry(int i, uint32_t xsh) {
+    const uint32_t v = c_q1_tab[i] >> xsh;
+    return v ? v : 1u;
 }
 
 // The per-launch LDS table of q1_val (all threads of the block, then a barrier).
 __device__ inline void q1_load_tab(uint32_t *tab, uint32_t xsh) {
-    for (int i = threadIdx.x; i < 1024; i += blockDim.x) tab[i] = c_q1_tab[i] >> xsh;
+    for (int i = threadIdx.x; i < LAC_Q1_TAB_SIZE; i += blockDim.x) tab[i] = q1_entry(i, xsh);
     __syncthreads();
 }
+
+// Lane-private replicated table for the row-stats kernel: entry i, copy c at
+// dword i*32 + c.  A wave64 ds_read_b32 is serviced as two 32-lane groups over 32
+// banks (bank = dword mod 32); lane l reads copy l & 31, so every lookup of a
+// group hits 32 distinct banks whatever the indices -- no bank conflicts for the
+// random gather (a single shared copy measured 68 % conflict cycles).
+constexpr int kQ1Rep = 32;
+__device__ inline void q1_load_tab_rep(uint32_t *tabr, uint32_t xsh) {
+    for (int i = threadIdx.x; i < LAC_Q1_TAB_SIZE * kQ1Rep; i += blockDim.x) tabr[i] = q1_entry(i / kQ1Rep, xsh);
+    __syncthreads();
+}
+
+__device__ inline uint32_t q1_rep_at(const uint32_t *tabr, uint32_t i, uint32_t loff) {
+    return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(tabr) + ((i << 7) | loff));
+}
+
+// Sum of q1 over the N logits of one 16-B vector (replicated table, loff = byte
+// offset of this lane's copy).  For a row max |m| <= 2^100 the scaled difference
+// is y = fma(x, -STEPS, STEPS m) = RNE(STEPS m - STEPS x), which equals
+// STEPS * RNE(m - x) exactly (power-of-two scaling commutes with rounding; STEPS m
+// is exact; a difference too small to be normal gives index 0 either way, one too
+// large to be finite clamps either way), two logits per v_pk_fma_f32; fminf sends
+// NaN to the last entry as the spec's clamp does.  Other rows (max +-inf, NaN or
+// beyond 2^100) take the literal form.  Entries are <= 2^24, so a lane's sum of
+// up to 128 entries fits 32 bits.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+template <typename LT>
+__device__ inline uint32_t q1_vec_sum(const u32x4 &x, float m, float ms, bool fast, const uint32_t *tabr,
+                                      uint32_t loff) {
+    constexpr int N = LogitN<LT>::N;
+    constexpr float kLast = (float)(LAC_Q1_DMAX * LAC_Q1_STEPS);
+    uint32_t s = 0;
+    if (fast) {
+        const f32x2 k = {-(float)LAC_Q1_STEPS, -(float)LAC_Q1_STEPS}, c = {ms, ms};
+#pragma unroll
+        for (int j = 0; j < N; j += 2) {
+            const f32x2 v = {logit_at<LT>(x, j), logit_at<LT>(x, j + 1)};
+            const f32x2 y = __builtin_elementwise_fma(v, k, c);
+            s += q1_rep_at(tabr, (uint32_t)fminf(y.x, kLast), loff);
+            s += q1_rep_at(tabr, (uint32_t)fminf(y.y, kLast), loff);
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < N; j++) {
+            const float d = fminf(m - logit_at<LT>(x, j), (float)LAC_Q1_DMAX);
+            s += q1_rep_at(tabr, (uint32_t)(d * (float)LAC_Q1_STEPS), loff);
+        }
+    }
+    return s;
+}
+
+__device__ inline bool q1_fast_row(float m) { return fabsf(m) <= 0x1p100f; }   // false for inf / NaN
 
 __device__ inline float wave_max_f32(float v) {
 #pragma unroll
@@ -978,194 +1032,246 @@ __device__ inline float wave_max_f32(float v) {
     return v;
 }
 
-// pass 1: the row's max logit (default cache policy so pass 2 finds the row in MALL)
-template <typename LT>
-__device__ inline float q1_row_max(const LT *row, int64_t nvec) {
-    constexpr int N = LogitN<LT>::N, U = LAC_UNROLL;
+// Sum of R per-lane values across the wave, R at once (R a power of two <= 64):
+// a butterfly that halves the live values per step, so lane l ends up holding the
+// total of index l / (64 / R) after R - 1 + log2(64 / R) exchanges (not R * 6).
+template <int R>
+__device__ inline uint64_t wave_multi_sum(uint64_t (&v)[R]) {
     const int lane = (int)lane_id();
-    float mx = -INFINITY;
-    int64_t vi = lane;
-    for (; vi + 64 * (U - 1) < nvec; vi += 64 * U) {
-        u32x4 x[U];
+    int m = 32;
 #pragma unroll
-        for (int u = 0; u < U; u++) x[u] = ld16(row, vi + 64 * u, false);
+    for (int live = R; live > 1; live >>= 1, m >>= 1) {
+        const bool upper = lane & m;
 #pragma unroll
-        for (int u = 0; u < U; u++)
-#pragma unroll
-            for (int j = 0; j < N; j++) mx = fmaxf(mx, logit_at<LT>(x[u], j));
-    }
-    for (; vi < nvec; vi += 64) {
-        const u32x4 x = ld16(row, vi, false);
-#pragma unroll
-        for (int j = 0; j < N; j++) mx = fmaxf(mx, logit_at<LT>(x, j));
-    }
-    return wave_max_f32(mx);
-}
-
-// pass 2: T, lo = sum_{i<s} q_i, q_s and the positive minimum of the q1 table
-template <typename LT>
-__device__ inline RowSums q1_row_reduce(const LT *row, int64_t nvec, int64_t s, float m, const uint32_t *tab) {
-    constexpr int N = LogitN<LT>::N, U = LAC_UNROLL;
-    const int lane = (int)lane_id();
-    const int64_t V = nvec * N;
-    const int64_t sc = s < 0 ? 0 : (s > V ? V : s);
-    const int64_t sfull = sc / N;
-    const int sr = (int)(sc - sfull * N);
-    uint64_t tot = 0, lo = 0, ps = 0;
-    uint32_t mn = ~0u;
-    auto take = [&](const u32x4 &x, int64_t v) {
-        uint64_t sl = 0;
-        uint32_t qs[N];
-#pragma unroll
-        for (int j = 0; j < N; j++) {
-            qs[j] = q1_val(logit_at<LT>(x, j), m, tab);
-            sl += qs[j];
-            mn = qs[j] < mn ? qs[j] : mn;                     // q >= 1: the positive minimum
+        for (int i = 0; i < live / 2; i++) {
+            const uint64_t keep = upper ? v[i + live / 2] : v[i];
+            const uint64_t give = upper ? v[i] : v[i + live / 2];
+            v[i] = keep + shfl_xor_u64(give, m);
         }
-        tot += sl;
-        if (v < sfull) lo += sl;
-        if (v == sfull) {
-#pragma unroll
-            for (int j = 0; j < N; j++) {
-                if (j < sr) lo += qs[j];
-                if (j == sr) ps = qs[j];
-            }
-        }
-    };
-    int64_t vi = lane;
-    for (; vi + 64 * (U - 1) < nvec; vi += 64 * U) {
-        u32x4 x[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) x[u] = ld16(row, vi + 64 * u, true);
-#pragma unroll
-        for (int u = 0; u < U; u++) take(x[u], vi + 64 * u);
     }
-    for (; vi < nvec; vi += 64) take(ld16(row, vi, true), vi);
-    RowSums r;
-    r.T = wave_sum_u64(tot);
-    r.lo = wave_sum_u64(lo);
-    r.ps = wave_sum_u64(ps);
-    r.minp = wave_min_u32(mn);
+    uint64_t r = v[0];
+#pragma unroll
+    for (int k = 32 / R; k >= 1; k >>= 1) r += shfl_xor_u64(r, k);
     return r;
 }
 
-template <typename LT>
-__global__ LAC_ENC_BOUNDS void k_encode_logits(const LT *__restrict__ lg, int64_t step_stride, int64_t stream_stride,
-                                               const int32_t *__restrict__ sym, int64_t B, int64_t nsteps,
-                                               int64_t V, int prec, uint32_t xsh, EncState *states,
-                                               uint64_t *planeA, uint64_t *planeC, uint64_t cap_words,
-                                               uint64_t *trace, uint64_t *nbits, int flags) {
-    __shared__ uint32_t tab[1024];
-    q1_load_tab(tab, xsh);
-    const int lane = (int)lane_id();
-    const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-    if (b >= B) return;
-    EncState st = (flags & kReset) ? fresh_state(prec) : states[b];
-    uint64_t *pa = planeA + (uint64_t)b * cap_words, *pc = planeC + (uint64_t)b * cap_words;
-    if (st.err || st.nflush >= 0) {
-        if (!st.err && st.nflush >= 0 && nsteps > 0) { st.err = LAC_E_STATE; st.err_step = st.nsym; }
-        if (lane == 0) {
-            states[b] = st;
-            if (flags & kFinish) nbits[b] = st.err ? 0 : st.L;
-        }
-        return;
-    }
-    const int64_t nvec = V / LogitN<LT>::N;
-    int64_t l = st.l, h = st.h;
-    for (int64_t t = 0; t < nsteps; t++) {
-        const LT *row = lg + t * step_stride + b * stream_stride;
-        const int64_t s = sym[t * B + b];
-        const float m = q1_row_max<LT>(row, nvec);
-        const RowSums rs = q1_row_reduce<LT>(row, nvec, s, m, tab);
-        const uint64_t lo = (uint64_t)rs.lo;
-        if (!coder_step<uint32_t>(st, l, h, lo, lo + rs.ps, (uint64_t)rs.T, rs.minp, s, nullptr, V, prec, pa, pc,
-                                  cap_words, trace ? trace + 2 * (t * B + b) : nullptr, lane, LAC_MAP_CEIL, 0.0,
-                                  false))
-            break;
-    }
-    if (lane == 0) {
-        store_state(st, l, h, pa, pc, cap_words, &st);
-        if (flags & kFinish) finish_stream(st, pa, pc, cap_words, prec, &nbits[b], LAC_TERM_FLUSH);
-        states[b] = st;
+__device__ inline u32x4 neg_inf16(int type_bytes) {
+    const uint32_t w = type_bytes == 2 ? 0xFF80FF80u : 0xFF800000u;
+    return u32x4{w, w, w, w};
+}
+
+// k_q1_stats: the q1 row statistics.  Persistent blocks of 8 waves (two per CU:
+// the replicated table takes 68 KB of LDS per block) walk the rows r = t*B + b;
+// each row is owned by a group of RW waves (8/RW rows per block iteration).  Each
+// thread holds R 16-B vectors of its row in registers (vector gt + NT*j of each
+// NT*R-vector tile, NT = 64*RW), so a row of <= NT*R vectors is read from HBM
+// exactly once: register max -> group max -> q1 sums from the same registers.
+// With PF the next row's loads are issued before this row's arithmetic.  Longer
+// rows (MULTI) take several tiles and re-read all but the last from the MALL.
+//   encode (DEC = false): RowStats {lo, hi, T} of the row's symbol for k_encode;
+//   decode (DEC = true):  the row max and 64 chunk totals (chunk c = vectors
+//                         [c*64G, (c+1)*64G)) for k_q1_decode.
+// None of this depends on the coder state, so every row of a chunk of steps runs
+// in parallel and the sequential kernels only touch a few bytes per step.
+constexpr int kQ1Waves = 8;
+
+template <typename LT, int R>
+__device__ inline void q1_load_tile(u32x4 (&x)[R], const LT *row, bool valid, int64_t base, int gt, int NT,
+                                    int64_t nvec) {
+#pragma unroll
+    for (int j = 0; j < R; j++) {
+        const int64_t vi = base + gt + (int64_t)NT * j;
+        x[j] = valid && vi < nvec ? ld16(row, vi, LAC_Q1_NT) : neg_inf16(sizeof(LT));
     }
 }
 
-// Decode from logits: one wave per stream, all steps in one launch (the q1
-// counterpart of k_decode_wave).
+template <typename LT, int RW, int R, bool DEC, bool MULTI, bool PF>
+__global__ __launch_bounds__(64 * kQ1Waves, 4) void k_q1_stats(const LT *__restrict__ lg, int64_t step_stride,
+                                                              int64_t stream_stride, const int32_t *__restrict__ sym,
+                                                              int64_t B, int64_t rows, int64_t V, int64_t t0,
+                                                              uint32_t xsh, int64_t G, RowStats *__restrict__ out,
+                                                              uint64_t *__restrict__ chunks,
+                                                              float *__restrict__ mrow) {
+    constexpr int N = LogitN<LT>::N, NT = 64 * RW, NR = kQ1Waves / RW;
+    static_assert(R * N <= 128, "lane sums must fit 32 bits");
+    __shared__ uint32_t tabr[LAC_Q1_TAB_SIZE * kQ1Rep];
+    __shared__ float smax[kQ1Waves];
+    __shared__ uint64_t ssum[kQ1Waves][2];
+    __shared__ uint32_t sps[NR];
+    __shared__ unsigned long long bins[DEC ? NR : 1][64];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = w / RW, wg = w % RW, gt = tid - g * NT;
+    if (DEC && wg == 0) bins[g][lane] = 0;
+    q1_load_tab_rep(tabr, xsh);
+    const uint32_t loff = (uint32_t)(lane & 31) << 2;
+    const int64_t nvec = V / N;
+    const int64_t ntiles = MULTI ? (nvec + (int64_t)NT * R - 1) / ((int64_t)NT * R) : 1;
+    const int64_t stride = (int64_t)gridDim.x * NR;
+    auto row_of = [&](int64_t r) { return lg + (t0 + r / B) * step_stride + (r % B) * stream_stride; };
+    u32x4 x[R], xn[R];
+    if (PF && !MULTI) {
+        const int64_t r0 = (int64_t)blockIdx.x * NR + g;
+        q1_load_tile<LT, R>(x, r0 < rows ? row_of(r0) : lg, r0 < rows, 0, gt, NT, nvec);
+    }
+    for (int64_t rb = (int64_t)blockIdx.x * NR; rb < rows; rb += stride) {
+        const int64_t r = rb + g;
+        const bool valid = r < rows;
+        const LT *row = valid ? row_of(r) : lg;
+        float mx = -INFINITY;
+        if (MULTI) {
+            for (int64_t tile = 0; tile < ntiles; tile++) {
+                q1_load_tile<LT, R>(x, row, valid, tile * NT * R, gt, NT, nvec);
+#pragma unroll
+                for (int j = 0; j < R; j++)
+#pragma unroll
+                    for (int e = 0; e < N; e++) mx = fmaxf(mx, logit_at<LT>(x[j], e));
+            }
+        } else {
+            if (PF) {
+                const int64_t rn = r + stride;
+                q1_load_tile<LT, R>(xn, rn < rows ? row_of(rn) : lg, rn < rows, 0, gt, NT, nvec);
+            } else {
+                q1_load_tile<LT, R>(x, row, valid, 0, gt, NT, nvec);
+            }
+#pragma unroll
+            for (int j = 0; j < R; j++)
+#pragma unroll
+                for (int e = 0; e < N; e++) mx = fmaxf(mx, logit_at<LT>(x[j], e));
+        }
+        mx = wave_max_f32(mx);
+        if (lane == 0) smax[w] = mx;
+        if (!DEC && gt == 0) sps[g] = 0;
+        __syncthreads();
+        float m = smax[g * RW];
+#pragma unroll
+        for (int i = 1; i < RW; i++) m = fmaxf(m, smax[g * RW + i]);
+        const bool fast = q1_fast_row(m);
+        const float ms = m * (float)LAC_Q1_STEPS;
+        int64_t sfull = -1;
+        int sr = 0;
+        if (!DEC && valid) {
+            const int64_t s = sym[(t0 + r / B) * B + r % B];
+            const int64_t sc = s < 0 ? 0 : (s > V ? V : s);
+            sfull = sc / N;
+            sr = (int)(sc - sfull * N);
+        }
+        uint32_t tot = 0, lo = 0;
+        for (int64_t tile = ntiles - 1; tile >= 0; tile--) {
+            if (MULTI && tile != ntiles - 1) q1_load_tile<LT, R>(x, row, valid, tile * NT * R, gt, NT, nvec);
+            uint64_t sv[R];
+#pragma unroll
+            for (int j = 0; j < R; j++) {
+                const int64_t vi = tile * NT * R + gt + (int64_t)NT * j;
+                uint32_t sl = q1_vec_sum<LT>(x[j], m, ms, fast, tabr, loff);
+                sl = vi < nvec ? sl : 0;
+                if (DEC) {
+                    sv[j] = sl;
+                } else {
+                    tot += sl;
+                    lo += vi < sfull ? sl : 0;
+                    if (vi == sfull) {                         // the vector holding s: split it once
+                        uint32_t pl = 0, ps = 0;
+#pragma unroll
+                        for (int e = 0; e < N; e++) {
+                            const float d = fminf(m - logit_at<LT>(x[j], e), (float)LAC_Q1_DMAX);
+                            const uint32_t q = q1_rep_at(tabr, (uint32_t)(d * (float)LAC_Q1_STEPS), loff);
+                            pl += e < sr ? q : 0;
+                            ps += e == sr ? q : 0;
+                        }
+                        lo += pl;
+                        sps[g] = ps;
+                    }
+                }
+            }
+            if (DEC) {
+                const uint64_t gsum = wave_multi_sum<R>(sv);  // group total of index lane / (64/R)
+                if ((lane & (64 / R - 1)) == 0) {
+                    const int64_t grp = tile * RW * R + wg + (int64_t)RW * (lane / (64 / R));
+                    if (grp * 64 < nvec) atomicAdd(&bins[g][grp / G], (unsigned long long)gsum);
+                }
+            }
+        }
+        if (!DEC) {
+            const uint64_t t64 = wave_sum_u64(tot), l64 = wave_sum_u64(lo);
+            if (lane == 0) { ssum[w][0] = t64; ssum[w][1] = l64; }
+        }
+        __syncthreads();
+        if (DEC) {
+            if (wg == 0) {
+                if (valid) chunks[r * 64 + lane] = bins[g][lane];
+                bins[g][lane] = 0;
+                if (valid && lane == 0) mrow[r] = m;
+            }
+        } else if (gt == 0 && valid) {
+            uint64_t T = 0, L = 0;
+#pragma unroll
+            for (int i = 0; i < RW; i++) { T += ssum[g * RW + i][0]; L += ssum[g * RW + i][1]; }
+            RowStats st;
+            st.lo = L;
+            st.hi = L + sps[g];
+            st.tot = T;
+            st.minp = 1;                                       // q1 entries are >= 1
+            st.inv_tot = 1.0 / (double)T;
+            st.pad = 0;
+            out[r] = st;
+        }
+        if (PF && !MULTI) {
+#pragma unroll
+            for (int j = 0; j < R; j++) x[j] = xn[j];
+        }
+    }
+}
+
+// k_q1_decode: one wave per stream, sequential over a chunk of steps, from the
+// chunk totals of k_q1_stats: per step it finds the chunk holding
+// floor((x-l)*T/w), re-quantises only that chunk's logits and scans them to the
+// symbol, then renormalises as A_from_bin does (decode_advance).
 template <typename LT>
-__global__ LAC_DEC_BOUNDS void k_decode_logits(const LT *__restrict__ lg, int64_t step_stride,
-                                               int64_t stream_stride, int64_t nsteps, int64_t V, int prec,
-                                               uint32_t xsh, DecState *states, const uint8_t *bits,
-                                               uint64_t stride, const uint64_t *nbits, int32_t *sym_out,
-                                               int64_t B) {
-    __shared__ uint32_t tab[1024];
+__global__ LAC_DEC_BOUNDS void k_q1_decode(const LT *__restrict__ lg, int64_t step_stride, int64_t stream_stride,
+                                           int64_t t0, int64_t nsteps, int64_t V, int prec, uint32_t xsh,
+                                           int64_t G, const uint64_t *__restrict__ chunks,
+                                           const float *__restrict__ mrow, DecState *states, const uint8_t *bits,
+                                           uint64_t stride, const uint64_t *nbits, int32_t *sym_out, int64_t B) {
+    __shared__ uint32_t tab[LAC_Q1_TAB_SIZE];
     q1_load_tab(tab, xsh);
-    constexpr int N = LogitN<LT>::N, U = LAC_UNROLL;
+    constexpr int N = LogitN<LT>::N;
     const int lane = (int)lane_id();
     const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
     if (b >= B) return;
     DecState st = states[b];
     const uint8_t *mybits = bits + b * stride;
     const uint64_t mynbits = nbits[b];
-    const int64_t nvec = V / N, nit = (nvec + 63) / 64;
-    int64_t CI = (nit + 63) / 64;
-    CI = ((CI + U - 1) / U) * U;
-    const int64_t nch = (nit + CI - 1) / CI;
-    for (int64_t t = 0; t < nsteps; t++) {
+    const int64_t nvec = V / N;
+    uint64_t next = nsteps > 0 ? chunks[b * 64 + lane] : 0;
+    for (int64_t i = 0; i < nsteps; i++) {
+        const int64_t t = t0 + i, r = i * B + b;
+        const uint64_t mine = next;
+        if (i + 1 < nsteps) next = chunks[(r + B) * 64 + lane];     // prefetch: independent of the state
         int32_t *out = sym_out + t * B + b;
         if (st.err) {
             if (lane == 0) *out = -1;
             continue;
         }
         const LT *row = lg + t * step_stride + b * stream_stride;
-        const float m = q1_row_max<LT>(row, nvec);
-        uint64_t mine = 0;
-        uint32_t mn = ~0u;
-        for (int64_t c = 0; c < nch; c++) {
-            uint64_t acc = 0;
-            for (int64_t g0 = 0; g0 < CI; g0 += U) {
-                u32x4 x[U];
-#pragma unroll
-                for (int u = 0; u < U; u++) {
-                    const int64_t vi = (c * CI + g0 + u) * 64 + lane;
-                    x[u] = vi < nvec ? ld16(row, vi, true) : u32x4{0, 0, 0, 0};
-                }
-#pragma unroll
-                for (int u = 0; u < U; u++) {
-                    const int64_t vi = (c * CI + g0 + u) * 64 + lane;
-                    if (vi < nvec) {
-#pragma unroll
-                        for (int j = 0; j < N; j++) {
-                            const uint32_t q = q1_val(logit_at<LT>(x[u], j), m, tab);
-                            acc += q;
-                            mn = q < mn ? q : mn;
-                        }
-                    }
-                }
-            }
-            const uint64_t tsum = wave_sum_u64(acc);
-            if (lane == c) mine = tsum;
-        }
+        const float m = mrow[r];
         const uint64_t T = wave_sum_u64(mine);
         const uint64_t incl = wave_incl_scan_u64(mine);
-        const uint64_t minp = wave_min_u32(mn);
         int err = 0;
         int64_t s = -1;
         const int64_t l = st.l, h = st.h, x = st.x;
         if (x < l || x > h) err = LAC_E_DECODE_RANGE;
         const uint64_t w = (uint64_t)(h - l + 1), v = (uint64_t)(x - l);
-        if (!err && is_fudged(T, w, minp)) err = LAC_E_TABLE;       // impossible by the choice of k
+        if (!err && is_fudged(T, w, 1)) err = LAC_E_TABLE;             // impossible by the choice of k
         if (!err) {
             const uint64_t tgt = div_floor((u128)v * T, w);
             const uint64_t ex = incl - mine;
-            const uint64_t mask = __ballot(lane < nch && ex <= tgt && tgt < incl);
+            const uint64_t mask = __ballot(ex <= tgt && tgt < incl);
             if (!mask) err = LAC_E_DECODE_RANGE;
             if (!err) {
                 const int src = __ffsll((unsigned long long)mask) - 1;
                 uint64_t cb = readlane_u64(ex, src);
-                const int64_t cv0 = (int64_t)src * CI * 64;
+                const int64_t cv0 = (int64_t)src * G * 64;
                 uint64_t lo_c = cb, hi_c = ~0ull, cnt = 0;
-                for (int64_t g = 0; g < CI; g++) {
+                for (int64_t g = 0; g < G; g++) {
                     const int64_t vi = cv0 + g * 64 + lane;
                     const u32x4 xv = vi < nvec ? ld16(row, vi, false) : u32x4{0, 0, 0, 0};
                     uint64_t loc[N], ls = 0;
@@ -1214,7 +1320,7 @@ template <typename LT>
 __global__ __launch_bounds__(256) void k_quantize_logits(const LT *__restrict__ lg, int64_t step_stride,
                                                          int64_t stream_stride, int64_t B, int64_t rows, int64_t V,
                                                          uint32_t xsh, uint32_t *__restrict__ out) {
-    __shared__ uint32_t tab[1024];
+    __shared__ uint32_t tab[LAC_Q1_TAB_SIZE];
     q1_load_tab(tab, xsh);
     constexpr int N = LogitN<LT>::N;
     const int lane = (int)lane_id();
@@ -1222,7 +1328,13 @@ __global__ __launch_bounds__(256) void k_quantize_logits(const LT *__restrict__ 
     if (r >= rows) return;
     const LT *row = lg + (r / B) * step_stride + (r % B) * stream_stride;
     const int64_t nvec = V / N;
-    const float m = q1_row_max<LT>(row, nvec);
+    float mx = -INFINITY;
+    for (int64_t vi = lane; vi < nvec; vi += 64) {
+        const u32x4 x = ld16(row, vi, false);
+#pragma unroll
+        for (int j = 0; j < N; j++) mx = fmaxf(mx, logit_at<LT>(x, j));
+    }
+    const float m = wave_max_f32(mx);
     uint32_t *o = out + r * V;
     for (int64_t vi = lane; vi < nvec; vi += 64) {
         const u32x4 x = ld16(row, vi, true);
@@ -1253,6 +1365,10 @@ struct lac_ctx {
     int64_t wave_decode_min_streams = 1024;
     int mapping = LAC_MAP_CEIL;         // symbol_to_range flavour (lac_set_option)
     int term = LAC_TERM_FLUSH;          // stream termination flavour
+    int cus = 256;                      // compute units (persistent grids)
+    int q1_shape = 0;                   // logits stats block shape (0 auto; lac_set_option tuning)
+    uint64_t *q1chunks = nullptr;       // logits decode: [chunk_steps * B][64] chunk totals
+    float *q1m = nullptr;               //                [chunk_steps * B] row maxima
     // live kernel timing (lac_profile_enable): hipEvent pairs around launches
     bool prof = false;
     std::vector<hipEvent_t> ev_pool;
@@ -1261,7 +1377,7 @@ struct lac_ctx {
 };
 
 enum { KID_ROW_STATS = 0, KID_ENCODE = 1, KID_FINISH = 2, KID_DECODE = 3, KID_FUSED = 4, KID_DECODE_WAVE = 5,
-       KID_ENCODE_LOGITS = 6, KID_DECODE_LOGITS = 7, KID_COUNT = 8 };
+       KID_Q1_STATS = 6, KID_Q1_DECODE = 7, KID_COUNT = 8 };
 
 static hipEvent_t ev_get(lac_ctx *c) {
     if (c->ev_next == c->ev_pool.size()) {
@@ -1346,7 +1462,7 @@ static int encode_impl(lac_ctx *c, const E *pmf, int64_t step_stride, int64_t st
             ProfScope ps(c, KID_ENCODE, st);
             k_encode<E><<<blocks, 64 * kWavesPerBlock, 0, st>>>(c->stats, sym, c->B, t0, n, pmf, step_stride,
                                                                 stream_stride, c->V, c->prec, c->enc, c->planeA,
-                                                                c->planeC, c->cap_words, trace, c->mapping);
+                                                                c->planeC, c->cap_words, trace, c->mapping, true);
         }
         CHECK_LAUNCH();
     }
@@ -1449,9 +1565,9 @@ static int q1_shift(lac_ctx *c, uint32_t *xsh) {
     int cl = 0;
     while (((int64_t)1 << cl) < c->V) cl++;                      // ceil(log2 V)
     int k = c->prec - 1 - cl;
-    if (k > 31) k = 31;
+    if (k > LAC_Q1_KMAX) k = LAC_Q1_KMAX;
     if (k < 1) return fail(LAC_E_PREC, "prec %d leaves no q1 precision for vocab %lld", c->prec, (long long)c->V);
-    *xsh = (uint32_t)(31 - k);
+    *xsh = (uint32_t)(LAC_Q1_KMAX - k);
     return LAC_OK;
 }
 
@@ -1464,6 +1580,123 @@ static int logits_check(lac_ctx *c, const void *lg, int type, int64_t step_strid
         return fail(LAC_E_ARG, "logits rows must be 16-byte aligned with vocab and strides multiples of %d", n);
     if (c->mapping != LAC_MAP_CEIL || c->term != LAC_TERM_FLUSH)
         return fail(LAC_E_STATE, "the logits path codes with the CDFPredictor mapping and flush termination");
+    return LAC_OK;
+}
+
+static int64_t q1_groups_per_chunk(int64_t nvec) {                // 64-vector groups per decode chunk
+    const int64_t groups = (nvec + 63) / 64;
+    return groups <= 64 ? 1 : (groups + 63) / 64;
+}
+
+struct Q1Args {
+    const void *lg;
+    int64_t ss, bs;
+    const int32_t *sym;
+    int64_t rows, t0;
+    uint32_t xsh;
+};
+
+template <typename LT, int RW, int R, bool DEC, bool MULTI, bool PF>
+static int q1_stats_launch(lac_ctx *c, const Q1Args &a, hipStream_t st) {
+    static int per_cu = 0;                                       // resident blocks per CU (occupancy API)
+    if (!per_cu) {
+        int n = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_q1_stats<LT, RW, R, DEC, MULTI, PF>, 64 * kQ1Waves,
+                                                         0) != hipSuccess ||
+            n < 1)
+            n = 1;
+        per_cu = n;
+    }
+    constexpr int NR = kQ1Waves / RW;
+    const int64_t need = (a.rows + NR - 1) / NR, cap = (int64_t)c->cus * per_cu;
+    const unsigned grid = (unsigned)(need < cap ? need : cap);
+    const int64_t nvec = c->V / LogitN<LT>::N;
+    ProfScope ps(c, KID_Q1_STATS, st);
+    k_q1_stats<LT, RW, R, DEC, MULTI, PF><<<grid, 64 * kQ1Waves, 0, st>>>(
+        (const LT *)a.lg, a.ss, a.bs, a.sym, c->B, a.rows, c->V, a.t0, a.xsh, q1_groups_per_chunk(nvec), c->stats,
+        c->q1chunks, c->q1m);
+    CHECK_LAUNCH();
+    return LAC_OK;
+}
+
+// Row-group shapes (waves per row RW, 16-B vectors per thread R, prefetch) of
+// k_q1_stats.  AUTO takes the first prefetch-free shape that holds the row in
+// registers, else tiles of (8, 8) (measured: the prefetching shapes spill at the
+// 128-VGPR cap of 4 waves/SIMD and run 1.7x slower); LAC_OPT_Q1_SHAPE forces
+// one (tuning; identical results).
+static const int kQ1Shapes[][3] = {{1, 4, 0}, {2, 8, 0}, {4, 8, 0}, {8, 8, 0}, {8, 8, 1}, {8, 4, 1}, {4, 8, 1}};
+
+template <typename LT, bool DEC>
+static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
+    const int64_t nvec = c->V / LogitN<LT>::N;
+    int sh = c->q1_shape;
+    auto holds = [&](int i) { return nvec <= 64 * kQ1Shapes[i - 1][0] * kQ1Shapes[i - 1][1]; };
+    if (sh == 0) {
+        for (int i = 1; i <= 4; i++)
+            if (holds(i)) { sh = i; break; }
+        if (sh == 0) sh = 8;
+    }
+    if (sh == 8) return q1_stats_launch<LT, 8, 8, DEC, true, false>(c, a, st);      // tiles of 4096 vectors
+    if (!holds(sh)) return fail(LAC_E_ARG, "q1 shape %d does not hold a row of %lld vectors", sh, (long long)nvec);
+    switch (sh) {
+    case 1: return q1_stats_launch<LT, 1, 4, DEC, false, false>(c, a, st);
+    case 2: return q1_stats_launch<LT, 2, 8, DEC, false, false>(c, a, st);
+    case 3: return q1_stats_launch<LT, 4, 8, DEC, false, false>(c, a, st);
+    case 4: return q1_stats_launch<LT, 8, 8, DEC, false, false>(c, a, st);
+    case 5: return q1_stats_launch<LT, 8, 8, DEC, false, true>(c, a, st);
+    case 6: return q1_stats_launch<LT, 8, 4, DEC, false, true>(c, a, st);
+    default: return q1_stats_launch<LT, 4, 8, DEC, false, true>(c, a, st);
+    }
+}
+
+template <typename LT>
+static int q1_encode_job(lac_ctx *c, const Q1Args &a0, int64_t steps, uint64_t *trace, hipStream_t st) {
+    const unsigned blocks = (unsigned)((c->B + kWavesPerBlock - 1) / kWavesPerBlock);
+    k_enc_reset<<<(unsigned)((c->B + 255) / 256), 256, 0, st>>>(c->enc, c->B, c->prec);
+    CHECK_LAUNCH();
+    for (int64_t t0 = 0; t0 < steps; t0 += c->chunk_steps) {
+        const int64_t n = (steps - t0) < c->chunk_steps ? (steps - t0) : c->chunk_steps;
+        Q1Args a = a0;
+        a.rows = n * c->B;
+        a.t0 = t0;
+        int rc = q1_stats<LT, false>(c, a, st);
+        if (rc) return rc;
+        {
+            ProfScope ps(c, KID_ENCODE, st);
+            k_encode<uint32_t><<<blocks, 64 * kWavesPerBlock, 0, st>>>(
+                c->stats, a.sym, c->B, t0, n, (const uint32_t *)nullptr, 0, 0, c->V, c->prec, c->enc, c->planeA,
+                c->planeC, c->cap_words, trace, LAC_MAP_CEIL, false);
+        }
+        CHECK_LAUNCH();
+    }
+    ProfScope ps(c, KID_FINISH, st);
+    k_finish<<<(unsigned)((c->B + 255) / 256), 256, 0, st>>>(c->enc, c->planeA, c->planeC, c->cap_words, c->B, c->prec,
+                                                             c->nbits, LAC_TERM_FLUSH);
+    CHECK_LAUNCH();
+    return LAC_OK;
+}
+
+template <typename LT>
+static int q1_decode(lac_ctx *c, const Q1Args &a0, int64_t steps, int32_t *out, hipStream_t st) {
+    if (!c->q1chunks) {
+        HIPCHK(hipMalloc(&c->q1chunks, sizeof(uint64_t) * 64 * c->chunk_steps * c->B));
+        HIPCHK(hipMalloc(&c->q1m, sizeof(float) * c->chunk_steps * c->B));
+    }
+    const unsigned blocks = (unsigned)((c->B + kWavesPerBlock - 1) / kWavesPerBlock);
+    const int64_t nvec = c->V / LogitN<LT>::N;
+    for (int64_t t0 = 0; t0 < steps; t0 += c->chunk_steps) {
+        const int64_t n = (steps - t0) < c->chunk_steps ? (steps - t0) : c->chunk_steps;
+        Q1Args a = a0;
+        a.rows = n * c->B;
+        a.t0 = t0;
+        int rc = q1_stats<LT, true>(c, a, st);
+        if (rc) return rc;
+        ProfScope ps(c, KID_Q1_DECODE, st);
+        k_q1_decode<LT><<<blocks, 64 * kWavesPerBlock, 0, st>>>(
+            (const LT *)a.lg, a.ss, a.bs, t0, n, c->V, c->prec, a.xsh, q1_groups_per_chunk(nvec), c->q1chunks,
+            c->q1m, c->dec, c->dbits, c->dstride, c->dnbits, out, c->B);
+        CHECK_LAUNCH();
+    }
     return LAC_OK;
 }
 
@@ -1487,6 +1720,8 @@ int lac_open(int device, int prec, int64_t vocab, int64_t streams, int pmf_bits,
     HIPCHK(hipSetDevice(device));
     lac_ctx *c = new lac_ctx;
     c->device = device;
+    if (hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || c->cus < 1)
+        c->cus = 256;
     c->prec = prec;
     c->pmf_bits = pmf_bits;
     c->V = vocab;
@@ -1524,6 +1759,8 @@ int lac_close(lac_ctx *c) {
     (void)hipFree(c->planeA);
     (void)hipFree(c->planeC);
     (void)hipFree(c->nbits);
+    (void)hipFree(c->q1chunks);
+    (void)hipFree(c->q1m);
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
     delete c;
     return LAC_OK;
@@ -1564,6 +1801,10 @@ int lac_set_option(lac_ctx *c, int option, int64_t value) {
     case LAC_OPT_DECODE_PATH:
         if (value < LAC_PATH_AUTO || value > LAC_PATH_FUSED) return fail(LAC_E_ARG, "bad decode path");
         c->dpath = (int)value;
+        return LAC_OK;
+    case LAC_OPT_Q1_SHAPE:
+        if (value < 0 || value > 8) return fail(LAC_E_ARG, "bad q1 shape");
+        c->q1_shape = (int)value;
         return LAC_OK;
     case LAC_OPT_MAPPING:
         if (value != LAC_MAP_CEIL && value != LAC_MAP_FLOOR) return fail(LAC_E_ARG, "bad mapping");
@@ -1729,19 +1970,9 @@ int lac_encode_logits_job(lac_ctx *c, const void *logits_dev, int logit_type, in
     if (rc || (rc = q1_shift(c, &xsh))) return rc;
     HIPCHK(hipSetDevice(c->device));
     c->mode = 0;
-    hipStream_t st = S(stream);
-    const unsigned blocks = (unsigned)((c->B + kWavesPerBlock - 1) / kWavesPerBlock);
-    ProfScope ps(c, KID_ENCODE_LOGITS, st);
-    if (logit_type == LAC_LOGITS_BF16)
-        k_encode_logits<uint16_t><<<blocks, 64 * kWavesPerBlock, 0, st>>>(
-            (const uint16_t *)logits_dev, step_stride, stream_stride, sym_dev, c->B, steps, c->V, c->prec, xsh,
-            c->enc, c->planeA, c->planeC, c->cap_words, trace_dev, c->nbits, kReset | kFinish);
-    else
-        k_encode_logits<float><<<blocks, 64 * kWavesPerBlock, 0, st>>>(
-            (const float *)logits_dev, step_stride, stream_stride, sym_dev, c->B, steps, c->V, c->prec, xsh,
-            c->enc, c->planeA, c->planeC, c->cap_words, trace_dev, c->nbits, kReset | kFinish);
-    CHECK_LAUNCH();
-    return LAC_OK;
+    const Q1Args a{logits_dev, step_stride, stream_stride, sym_dev, 0, 0, xsh};
+    return logit_type == LAC_LOGITS_BF16 ? q1_encode_job<uint16_t>(c, a, steps, trace_dev, S(stream))
+                                         : q1_encode_job<float>(c, a, steps, trace_dev, S(stream));
 }
 
 int lac_decode_logits_steps(lac_ctx *c, const void *logits_dev, int logit_type, int64_t step_stride,
@@ -1753,19 +1984,9 @@ int lac_decode_logits_steps(lac_ctx *c, const void *logits_dev, int logit_type, 
     if (rc || (rc = q1_shift(c, &xsh))) return rc;
     if (steps == 0) return LAC_OK;
     HIPCHK(hipSetDevice(c->device));
-    hipStream_t st = S(stream);
-    const unsigned blocks = (unsigned)((c->B + kWavesPerBlock - 1) / kWavesPerBlock);
-    ProfScope ps(c, KID_DECODE_LOGITS, st);
-    if (logit_type == LAC_LOGITS_BF16)
-        k_decode_logits<uint16_t><<<blocks, 64 * kWavesPerBlock, 0, st>>>(
-            (const uint16_t *)logits_dev, step_stride, stream_stride, steps, c->V, c->prec, xsh, c->dec, c->dbits,
-            c->dstride, c->dnbits, sym_out_dev, c->B);
-    else
-        k_decode_logits<float><<<blocks, 64 * kWavesPerBlock, 0, st>>>(
-            (const float *)logits_dev, step_stride, stream_stride, steps, c->V, c->prec, xsh, c->dec, c->dbits,
-            c->dstride, c->dnbits, sym_out_dev, c->B);
-    CHECK_LAUNCH();
-    return LAC_OK;
+    const Q1Args a{logits_dev, step_stride, stream_stride, nullptr, 0, 0, xsh};
+    return logit_type == LAC_LOGITS_BF16 ? q1_decode<uint16_t>(c, a, steps, sym_out_dev, S(stream))
+                                         : q1_decode<float>(c, a, steps, sym_out_dev, S(stream));
 }
 
 int lac_quantize_logits(lac_ctx *c, const void *logits_dev, int logit_type, int64_t step_stride,
@@ -1798,7 +2019,7 @@ int lac_q1_k(int prec, int64_t vocab) {
     int cl = 0;
     while (((int64_t)1 << cl) < vocab) cl++;
     const int k = prec - 1 - cl;
-    return k > 31 ? 31 : k;
+    return k > LAC_Q1_KMAX ? LAC_Q1_KMAX : k;
 }
 
 int lac_decode_determined(lac_ctx *c, int64_t *ndet_host, void *stream) {

@@ -148,3 +148,27 @@ def softmax_tables(steps: int, streams: int, V: int, seed: int = 1234, device="c
         out[t] = q.to(dt)
         del q, cdf
     return out, sym
+
+
+def logits_batch(steps: int, streams: int, V: int, seed: int = 1234, device="cuda", dtype=None,
+                 sigma: float = 3.0, quantise=None):
+    """Random logits [steps, streams, V] (bf16 or f32) on the GPU and symbols
+    drawn from their q1 tables (``quantise`` = BatchCoder.quantize_logits) by
+    inverse CDF of a seeded uniform.  Returns (logits, sym int32 [steps, streams])."""
+    import torch
+    dtype = dtype or torch.bfloat16
+    out = torch.empty((steps, streams, V), dtype=dtype, device=device)
+    sym = torch.empty((steps, streams), dtype=torch.int32, device=device)
+    for t in range(steps):
+        g = torch.Generator(device=device)
+        g.manual_seed(seed + t)
+        out[t] = (torch.randn((streams, V), generator=g, device=device, dtype=torch.float32) * sigma).to(dtype)
+        q = quantise(out[t:t + 1])[0].to(torch.int64) & 0xFFFFFFFF
+        cdf = torch.cumsum(q, dim=-1)
+        del q
+        tot = cdf[:, -1]
+        u = torch.rand((streams,), generator=g, device=device, dtype=torch.float64)
+        target = torch.minimum((u * tot.double()).floor().long(), tot - 1)
+        sym[t] = torch.searchsorted(cdf, target.unsqueeze(1), right=True).squeeze(1).to(torch.int32)
+        del cdf
+    return out, sym

@@ -26,10 +26,10 @@
 #include <stdlib.h>
 #include <string.h>
 
-/* The q1 exp2 table is a format constant (the quantiser's definition), shared
+/* The q1 exp table is a format constant (the quantiser's definition), shared
  * with the product; the arithmetic below is an independent restatement. */
 #include "../include/lac_q1_table.h"
-static const uint32_t Q1_TAB[1024] = LAC_Q1_TAB_INIT;
+static const uint32_t Q1_TAB[LAC_Q1_TAB_SIZE] = LAC_Q1_TAB_INIT;
 
 typedef unsigned __int128 u128;
 typedef __int128 i128;
@@ -339,9 +339,9 @@ int lacref_acsampler_encode(const uint64_t *cdf, int64_t V, const int32_t *toks,
 }
 
 /* ---- q1 logits quantiser (DESIGN.md "logits path"): bf16 (type 1) or f32 (type 2)
- * logits -> uint32 pmf.  m = max (fmaxf), d = m - x (f32), u = floor(d * 2^16)
- * saturating at 2^31 - 1 (NaN too), e = u * round(log2 e * 2^16) (Q32),
- * q = max(1, TAB[frac10(e)] >> (int(e) + 31 - k)), k = min(31, prec-1-ceil(log2 V)). */
+ * logits -> uint32 pmf.  m = max (fmaxf: NaN ignored), d = m - x (f32), clamped
+ * to 17 (NaN too), i = floor(d * 32), q = max(1, TAB[i] >> (24 - k)),
+ * TAB[i] = round(2^24 e^(-i/32)), k = min(24, prec-1-ceil(log2 V)). */
 static inline float q1_load(const void *x, int type, int64_t i) {
     if (type == 1) {
         uint32_t u = (uint32_t)((const uint16_t *)x)[i] << 16;
@@ -356,7 +356,7 @@ int lacref_q1_k(int prec, int64_t V) {
     int cl = 0;
     while (((int64_t)1 << cl) < V) cl++;
     int k = prec - 1 - cl;
-    if (k > 31) k = 31;
+    if (k > LAC_Q1_KMAX) k = LAC_Q1_KMAX;
     return k;
 }
 
@@ -367,11 +367,9 @@ int lacref_q1_quantize(const void *x, int type, int64_t V, int prec, uint32_t *q
     for (int64_t i = 0; i < V; i++) m = fmaxf(m, q1_load(x, type, i));
     for (int64_t i = 0; i < V; i++) {
         volatile float d = m - q1_load(x, type, i);
-        uint32_t u = (d < 32767.0f) ? (uint32_t)(d * 65536.0f) : 0x7FFFFFFFu;
-        uint64_t e = (uint64_t)u * LAC_Q1_LOG2E_Q16;
-        uint32_t ip = (uint32_t)(e >> 32), fr = (uint32_t)(e >> 22) & 1023u;
-        uint32_t sh = ip + (uint32_t)(31 - k);
-        uint32_t v = sh >= 32 ? 0u : (Q1_TAB[fr] >> sh);
+        float dc = d < (float)LAC_Q1_DMAX ? d : (float)LAC_Q1_DMAX;      /* NaN compares false */
+        uint32_t idx = (uint32_t)(dc * (float)LAC_Q1_STEPS);
+        uint32_t v = Q1_TAB[idx] >> (LAC_Q1_KMAX - k);
         q[i] = v ? v : 1u;
     }
     return R_OK;

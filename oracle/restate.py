@@ -313,20 +313,16 @@ def acsampler_encode(cdf, tokens, prec=48):
 
 # ------------------------------------------------ q1 logits quantiser (this repo's format)
 def q1_quantize(logits_f32, prec, tab):
-    """Independent numpy restatement of the q1 quantiser for one row
+    """Independent numpy restatement of the q1 quantiser for rows
     of float32 logits (bf16 inputs: widen the bit pattern << 16 first)."""
     import numpy as np
     x = np.asarray(logits_f32, dtype=np.float32)
     V = x.shape[-1]
-    k = min(31, prec - 1 - (V - 1).bit_length())
-    m = np.float32(np.fmax.reduce(x))
-    d = (m - x).astype(np.float32)
-    ok = d < np.float32(32767.0)
-    u = np.where(ok, (np.where(ok, d, 0) * np.float32(65536.0)).astype(np.uint64), 0x7FFFFFFF).astype(np.uint64)
-    e = u * np.uint64(94548)
-    ip = (e >> np.uint64(32)).astype(np.int64)
-    fr = ((e >> np.uint64(22)) & np.uint64(1023)).astype(np.int64)
-    sh = ip + (31 - k)
-    t = np.asarray(tab, dtype=np.uint64)[fr]
-    q = np.where(sh >= 32, 0, t >> np.minimum(sh, 63).astype(np.uint64))
+    k = min(24, prec - 1 - (V - 1).bit_length())
+    m = np.fmax.reduce(x, axis=-1, keepdims=True).astype(np.float32)
+    with np.errstate(invalid="ignore"):
+        d = (m - x).astype(np.float32)
+        d = np.where(d < np.float32(17.0), d, np.float32(17.0))            # NaN -> 17
+    i = (d * np.float32(32.0)).astype(np.int64)
+    q = np.asarray(tab, dtype=np.uint64)[i] >> np.uint64(24 - k)
     return np.maximum(q, 1).astype(np.uint32)

@@ -25,11 +25,12 @@ def _widen(b):
     return (b.astype(np.uint32) << 16).view(np.float32)
 
 
-def test_table_is_exact_exp2():
+def test_table_is_exact_exp():
+    import math
     tab = _tab()
-    assert len(tab) == 1024 and tab[0] == 1 << 31
-    for j in (1, 100, 511, 1023):
-        assert abs(tab[j] - 2 ** (31 - j / 1024)) <= 0.5 + 1e-6 * tab[j]
+    assert len(tab) == 17 * 32 + 1 and tab[0] == 1 << 24 and tab[-1] >= 1
+    for i in (1, 31, 100, 311, 500, 544):
+        assert abs(tab[i] - 2 ** 24 * math.exp(-i / 32)) <= 0.5 + 1e-9 * tab[i]
 
 
 @pytest.mark.parametrize("V,prec", [(32000, 48), (128256, 48), (1000, 40), (17, 24)])
@@ -45,7 +46,7 @@ def test_c_oracle_matches_numpy_restatement(V, prec):
         got_f = coracle.q1_quantize(x, prec)
         want_f = restate.q1_quantize(x, prec, tab)
         assert (got_f == want_f).all()
-        k = min(31, prec - 1 - (V - 1).bit_length())
+        k = min(24, prec - 1 - (V - 1).bit_length())
         assert got_f.max() == 1 << k and got_f.min() >= 1
         assert int(got_f.astype(np.uint64).sum()) <= V << k       # never fudged: T <= 2^(prec-1)
 
@@ -55,7 +56,7 @@ def test_non_finite_logits():
     x = np.array([0.0, -np.inf, np.nan, 5.0, -1e30, 1e-40], dtype=np.float32)
     got = coracle.q1_quantize(x, 48)
     assert (got == restate.q1_quantize(x, 48, tab)).all()
-    assert got[3] == 1 << 31 and got[1] == 1 and got[2] == 1
+    assert got[3] == 1 << 24 and got[1] == 1 and got[2] == 1
     allinf = np.full(8, -np.inf, dtype=np.float32)
     assert (coracle.q1_quantize(allinf, 48) == 1).all()
 
