@@ -72,7 +72,7 @@ enum {                       /* lac_set_option */
                                       AUTO = FUSED from 1024 streams */
     LAC_OPT_Q1_SHAPE = 6           /* logits path row-stats shape: 0 = auto (default), 1..7 = (waves per
                                       row, vectors/thread, prefetch) (1,4,n) (2,8,n) (4,8,n) (8,8,n)
-                                      (8,8,y) (8,4,y) (4,8,y), 8 = tiles of (8,8,n); identical results,
+                                      (8,16,n) (8,8,y) (8,4,y), 8 = tiles of (8,8,n); identical results,
                                       only speed differs */
 };
 enum {

@@ -933,6 +933,9 @@ __constant__ uint32_t c_q1_tab[LAC_Q1_TAB_SIZE] = LAC_Q1_TAB_INIT;
 #ifndef LAC_Q1_NT
 #define LAC_Q1_NT 1              // logits rows are read once: nontemporal loads
 #endif
+#ifndef LAC_Q1_SCHED
+#define LAC_Q1_SCHED 0           // scheduling fence between vectors in k_q1_stats
+#endif
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -1076,11 +1079,10 @@ __device__ inline u32x4 neg_inf16(int type_bytes) {
 constexpr int kQ1Waves = 8;
 
 template <typename LT, int R>
-__device__ inline void q1_load_tile(u32x4 (&x)[R], const LT *row, bool valid, int64_t base, int gt, int NT,
-                                    int64_t nvec) {
+__device__ inline void q1_load_tile(u32x4 (&x)[R], const LT *row, bool valid, int base, int gt, int NT, int nvec) {
 #pragma unroll
     for (int j = 0; j < R; j++) {
-        const int64_t vi = base + gt + (int64_t)NT * j;
+        const int vi = base + gt + NT * j;
         x[j] = valid && vi < nvec ? ld16(row, vi, LAC_Q1_NT) : neg_inf16(sizeof(LT));
     }
 }
@@ -1099,12 +1101,15 @@ __global__ __launch_bounds__(64 * kQ1Waves, 4) void k_q1_stats(const LT *__restr
     __shared__ uint64_t ssum[kQ1Waves][2];
     __shared__ uint32_t sps[NR];
     __shared__ unsigned long long bins[DEC ? NR : 1][64];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = w / RW, wg = w % RW, gt = tid - g * NT;
+    // in-row indices are 32-bit (vocab <= 2^31 entries); with one row per block
+    // (RW = 8) the row pointer is provably wave-uniform (SGPR-based loads)
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int g = NR == 1 ? 0 : w / RW, wg = NR == 1 ? w : w % RW, gt = tid - g * NT;
     if (DEC && wg == 0) bins[g][lane] = 0;
     q1_load_tab_rep(tabr, xsh);
     const uint32_t loff = (uint32_t)(lane & 31) << 2;
-    const int64_t nvec = V / N;
-    const int64_t ntiles = MULTI ? (nvec + (int64_t)NT * R - 1) / ((int64_t)NT * R) : 1;
+    const int nvec = (int)(V / N);
+    const int ntiles = MULTI ? (nvec + NT * R - 1) / (NT * R) : 1;
     const int64_t stride = (int64_t)gridDim.x * NR;
     auto row_of = [&](int64_t r) { return lg + (t0 + r / B) * step_stride + (r % B) * stream_stride; };
     u32x4 x[R], xn[R];
@@ -1118,7 +1123,7 @@ __global__ __launch_bounds__(64 * kQ1Waves, 4) void k_q1_stats(const LT *__restr
         const LT *row = valid ? row_of(r) : lg;
         float mx = -INFINITY;
         if (MULTI) {
-            for (int64_t tile = 0; tile < ntiles; tile++) {
+            for (int tile = 0; tile < ntiles; tile++) {
                 q1_load_tile<LT, R>(x, row, valid, tile * NT * R, gt, NT, nvec);
 #pragma unroll
                 for (int j = 0; j < R; j++)
@@ -1146,23 +1151,25 @@ __global__ __launch_bounds__(64 * kQ1Waves, 4) void k_q1_stats(const LT *__restr
         for (int i = 1; i < RW; i++) m = fmaxf(m, smax[g * RW + i]);
         const bool fast = q1_fast_row(m);
         const float ms = m * (float)LAC_Q1_STEPS;
-        int64_t sfull = -1;
-        int sr = 0;
+        int sfull = -1, sr = 0;
         if (!DEC && valid) {
             const int64_t s = sym[(t0 + r / B) * B + r % B];
-            const int64_t sc = s < 0 ? 0 : (s > V ? V : s);
+            const int sc = (int)(s < 0 ? 0 : (s > V ? V : s));
             sfull = sc / N;
-            sr = (int)(sc - sfull * N);
+            sr = sc - sfull * N;
         }
         uint32_t tot = 0, lo = 0;
-        for (int64_t tile = ntiles - 1; tile >= 0; tile--) {
+        for (int tile = ntiles - 1; tile >= 0; tile--) {
             if (MULTI && tile != ntiles - 1) q1_load_tile<LT, R>(x, row, valid, tile * NT * R, gt, NT, nvec);
             uint64_t sv[R];
 #pragma unroll
             for (int j = 0; j < R; j++) {
-                const int64_t vi = tile * NT * R + gt + (int64_t)NT * j;
+                const int vi = tile * NT * R + gt + NT * j;
                 uint32_t sl = q1_vec_sum<LT>(x[j], m, ms, fast, tabr, loff);
                 sl = vi < nvec ? sl : 0;
+#if LAC_Q1_SCHED
+                __builtin_amdgcn_sched_barrier(0);             // bound the lookups in flight (VGPRs)
+#endif
                 if (DEC) {
                     sv[j] = sl;
                 } else {
@@ -1185,8 +1192,8 @@ __global__ __launch_bounds__(64 * kQ1Waves, 4) void k_q1_stats(const LT *__restr
             if (DEC) {
                 const uint64_t gsum = wave_multi_sum<R>(sv);  // group total of index lane / (64/R)
                 if ((lane & (64 / R - 1)) == 0) {
-                    const int64_t grp = tile * RW * R + wg + (int64_t)RW * (lane / (64 / R));
-                    if (grp * 64 < nvec) atomicAdd(&bins[g][grp / G], (unsigned long long)gsum);
+                    const int grp = tile * RW * R + wg + RW * (lane / (64 / R));
+                    if (grp * 64 < nvec) atomicAdd(&bins[g][grp / (int)G], (unsigned long long)gsum);
                 }
             }
         }
@@ -1624,7 +1631,7 @@ static int q1_stats_launch(lac_ctx *c, const Q1Args &a, hipStream_t st) {
 // registers, else tiles of (8, 8) (measured: the prefetching shapes spill at the
 // 128-VGPR cap of 4 waves/SIMD and run 1.7x slower); LAC_OPT_Q1_SHAPE forces
 // one (tuning; identical results).
-static const int kQ1Shapes[][3] = {{1, 4, 0}, {2, 8, 0}, {4, 8, 0}, {8, 8, 0}, {8, 8, 1}, {8, 4, 1}, {4, 8, 1}};
+static const int kQ1Shapes[][3] = {{1, 4, 0}, {2, 8, 0}, {4, 8, 0}, {8, 8, 0}, {8, 16, 0}, {8, 8, 1}, {8, 4, 1}};
 
 template <typename LT, bool DEC>
 static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
@@ -1632,7 +1639,7 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
     int sh = c->q1_shape;
     auto holds = [&](int i) { return nvec <= 64 * kQ1Shapes[i - 1][0] * kQ1Shapes[i - 1][1]; };
     if (sh == 0) {
-        for (int i = 1; i <= 4; i++)
+        for (int i = 1; i <= (sizeof(LT) == 4 ? 5 : 4); i++)             // bf16 (8,16) spills
             if (holds(i)) { sh = i; break; }
         if (sh == 0) sh = 8;
     }
@@ -1643,9 +1650,9 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
     case 2: return q1_stats_launch<LT, 2, 8, DEC, false, false>(c, a, st);
     case 3: return q1_stats_launch<LT, 4, 8, DEC, false, false>(c, a, st);
     case 4: return q1_stats_launch<LT, 8, 8, DEC, false, false>(c, a, st);
-    case 5: return q1_stats_launch<LT, 8, 8, DEC, false, true>(c, a, st);
-    case 6: return q1_stats_launch<LT, 8, 4, DEC, false, true>(c, a, st);
-    default: return q1_stats_launch<LT, 4, 8, DEC, false, true>(c, a, st);
+    case 5: return q1_stats_launch<LT, 8, 16, DEC, false, false>(c, a, st);
+    case 6: return q1_stats_launch<LT, 8, 8, DEC, false, true>(c, a, st);
+    default: return q1_stats_launch<LT, 8, 4, DEC, false, true>(c, a, st);
     }
 }
 
