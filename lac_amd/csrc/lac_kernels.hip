@@ -1162,14 +1162,9 @@ __global__ __launch_bounds__(64 * kQ1Waves, 4) void k_q1_stats(const LT *__restr
         for (int tile = ntiles - 1; tile >= 0; tile--) {
             if (MULTI && tile != ntiles - 1) q1_load_tile<LT, R>(x, row, valid, tile * NT * R, gt, NT, nvec);
             uint64_t sv[R];
-#pragma unroll
-            for (int j = 0; j < R; j++) {
+            auto take = [&](int j, uint32_t sl) {
                 const int vi = tile * NT * R + gt + NT * j;
-                uint32_t sl = q1_vec_sum<LT>(x[j], m, ms, fast, tabr, loff);
                 sl = vi < nvec ? sl : 0;
-#if LAC_Q1_SCHED
-                __builtin_amdgcn_sched_barrier(0);             // bound the lookups in flight (VGPRs)
-#endif
                 if (DEC) {
                     sv[j] = sl;
                 } else {
@@ -1188,6 +1183,13 @@ __global__ __launch_bounds__(64 * kQ1Waves, 4) void k_q1_stats(const LT *__restr
                         sps[g] = ps;
                     }
                 }
+            };
+            if (fast) {                                        // row-uniform branch, outside the vector loop
+#pragma unroll
+                for (int j = 0; j < R; j++) take(j, q1_vec_sum<LT>(x[j], m, ms, true, tabr, loff));
+            } else {
+#pragma unroll
+                for (int j = 0; j < R; j++) take(j, q1_vec_sum<LT>(x[j], m, ms, false, tabr, loff));
             }
             if (DEC) {
                 const uint64_t gsum = wave_multi_sum<R>(sv);  // group total of index lane / (64/R)
