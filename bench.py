@@ -75,12 +75,20 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU; LAC_DIST_BACKEND=gloo + ranks sharing a GPU only for rehearsing the
+    # multi-rank path on a one-GPU box (the driver's runs use nccl = RCCL, one GPU each)
+    backend = os.environ.get("LAC_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    local = local % ndev if backend != "nccl" and ndev else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from lac_amd import synth
     from lac_amd.batch import BatchCoder
@@ -135,7 +143,7 @@ def main():
     coder.lib.lac_profile_enable(coder.ctx, 0)
     dt = t1 - t0
     if dist:
-        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     ms = (C.c_double * 8)()
@@ -169,7 +177,7 @@ def main():
                    "achieved_GBps": B * (V * ebytes + 4) / (dstep_ms * 1e-3) / 1e9 if dcnt[dkid] else None}
     round_trip = bool(torch.equal(dec, sym)) and rc == 0
     if dist:
-        ok = torch.tensor([1 if round_trip else 0], device=dev)
+        ok = torch.tensor([1 if round_trip else 0], device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         round_trip = bool(ok.item())
 

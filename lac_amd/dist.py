@@ -33,6 +33,8 @@ def gather_bitstreams(bits, nbits, group=None):
     B = bits.shape[0]
     width = ((nbits.max() + 7) // 8 if B else torch.zeros((), dtype=torch.int64, device=nbits.device)).to(torch.int64)
     width = width.reshape(1).clone()
+    if width.is_cuda and dist.get_backend(group) == "gloo":
+        width = width.cpu()
     dist.all_reduce(width, op=dist.ReduceOp.MAX, group=group)
     w = int(width.item())
     w = max(8, (w + 7) // 8 * 8)
@@ -50,6 +52,11 @@ def gather_bitstreams(bits, nbits, group=None):
 
 def _all_gather(out, inp, group, world):
     import torch.distributed as dist
+    if out.is_cuda and dist.get_backend(group) == "gloo":   # rehearsal runs: gloo moves host tensors
+        host = out.cpu()
+        _all_gather(host, inp.cpu(), group, world)
+        out.copy_(host)
+        return
     try:
         dist.all_gather_into_tensor(out, inp, group=group)
     except (RuntimeError, NotImplementedError):       # backends without the fused form
