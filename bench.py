@@ -63,6 +63,7 @@ def main():
     ap.add_argument("--cpu-streams", type=int, default=0, help="oracle sample streams (0 = all)")
     ap.add_argument("--path", default="auto", choices=("auto", "split", "fused"), help="encode kernel path")
     ap.add_argument("--q1-shape", type=int, default=0, help="logits row-stats block shape (tuning)")
+    ap.add_argument("--decode-path", default="auto", choices=("auto", "split", "fused", "stats"))
     ap.add_argument("--input", default="pmf", choices=("pmf", "logits-bf16", "logits-f32"),
                     help="pmf rows (BASELINE c3, default) or raw logits quantised in-kernel (q1, SURVEY §8(f)1)")
     args = ap.parse_args()
@@ -115,6 +116,8 @@ def main():
         coder.set_path(args.path)
     if args.q1_shape:
         coder.set_q1_shape(args.q1_shape)
+    if args.decode_path != "auto":
+        coder.set_decode_path(args.decode_path)
 
     def job():
         if logits_in:
@@ -168,13 +171,12 @@ def main():
     dms = (C.c_double * 8)()
     dcnt = (C.c_int64 * 8)()
     coder.lib.lac_profile_read(coder.ctx, C.cast(dms, C.c_void_p), C.cast(dcnt, C.c_void_p), 1)
-    dkid = 7 if dcnt[7] else (5 if dcnt[5] else 3)       # q1_decode(+q1_stats) / decode_wave / decode_step
-    dk_ms = dms[dkid] + (dms[6] if dkid == 7 else 0.0)
-    dstep_ms = dk_ms / (T if dkid in (5, 7) else max(dcnt[dkid], 1))
-    decode_info = {"symbols_per_s": B * T / (d1 - d0),
-                   "kernel": {7: "k_q1_stats+k_q1_decode", 5: "k_decode_wave", 3: "k_decode_step"}[dkid],
+    dkids = [k for k in (3, 5, 6, 7) if dcnt[k]]              # decode_step|stats path, decode_wave, q1 pair
+    dstep_ms = sum(dms[k] for k in dkids) / max(T, 1)
+    names = {3: "k_decode_step or k_dec_stats+k_decode_seq", 5: "k_decode_wave", 6: "k_q1_stats", 7: "k_q1_decode"}
+    decode_info = {"symbols_per_s": B * T / (d1 - d0), "kernel": "+".join(names[k] for k in dkids),
                    "kernel_ms_per_step": dstep_ms,
-                   "achieved_GBps": B * (V * ebytes + 4) / (dstep_ms * 1e-3) / 1e9 if dcnt[dkid] else None}
+                   "achieved_GBps": B * (V * ebytes + 4) / (dstep_ms * 1e-3) / 1e9 if dkids else None}
     round_trip = bool(torch.equal(dec, sym)) and rc == 0
     if dist:
         ok = torch.tensor([1 if round_trip else 0], device=dev if backend == "nccl" else "cpu")

@@ -69,7 +69,8 @@ enum {                       /* lac_set_option */
     LAC_OPT_TERMINATION = 4,       /* LAC_TERM_*: how a stream is closed */
     LAC_OPT_DECODE_PATH = 5,       /* LAC_PATH_*: SPLIT = one 4-wave workgroup per stream and step,
                                       FUSED = one wave per stream, all steps of a call in one launch;
-                                      AUTO = FUSED from 1024 streams */
+                                      STATS = see LAC_PATH_STATS; AUTO = FUSED from 2048 streams,
+                                      else STATS */
     LAC_OPT_Q1_SHAPE = 6           /* logits path row-stats shape: 0 = auto (default), 1..7 = (waves per
                                       row, vectors/thread, prefetch) (1,4,n) (2,8,n) (4,8,n) (8,8,n)
                                       (8,16,n) (8,8,y) (8,4,y), 8 = tiles of (8,8,n); identical results,
@@ -88,7 +89,10 @@ enum {
 enum {
     LAC_PATH_AUTO = 0,             /* fused if streams >= fused_min_streams, else split */
     LAC_PATH_SPLIT = 1,            /* row-stats kernel over all (step, stream) rows + coder kernel */
-    LAC_PATH_FUSED = 2             /* one wave per stream: row scan + coder in one kernel */
+    LAC_PATH_FUSED = 2,            /* one wave per stream: row scan + coder in one kernel */
+    LAC_PATH_STATS = 3             /* decode only: chunk totals of every (step, stream) row in one
+                                      full-chip kernel, then a per-stream sequential kernel that
+                                      re-reads one chunk per step (AUTO below 2048 streams) */
 };
 
 /* Library identification and the last error message of this thread. */

@@ -68,7 +68,7 @@ KERNEL_IDS = {"row_stats": 0, "encode": 1, "finish": 2, "decode_step": 3, "encod
 LAC_LOGITS_BF16, LAC_LOGITS_F32 = 1, 2
 LAC_OPT_ENCODE_PATH = 1
 LAC_OPT_FUSED_MIN_STREAMS = 2
-LAC_PATH_AUTO, LAC_PATH_SPLIT, LAC_PATH_FUSED = 0, 1, 2
+LAC_PATH_AUTO, LAC_PATH_SPLIT, LAC_PATH_FUSED, LAC_PATH_STATS = 0, 1, 2, 3
 LAC_OPT_MAPPING = 3
 LAC_OPT_TERMINATION = 4
 LAC_OPT_DECODE_PATH = 5

@@ -159,8 +159,11 @@ class BatchCoder:
         check(self.lib.lac_set_option(self.ctx, _lib.LAC_OPT_TERMINATION, v))
 
     def set_decode_path(self, path):
-        """'auto', 'split' (one workgroup per stream per step) or 'fused' (one wave per stream, one launch)."""
-        v = {"auto": _lib.LAC_PATH_AUTO, "split": _lib.LAC_PATH_SPLIT, "fused": _lib.LAC_PATH_FUSED}[path]
+        """'auto', 'split' (one workgroup per stream per step), 'fused' (one wave per
+        stream, one launch) or 'stats' (all rows' chunk totals at once, then a
+        sequential per-stream kernel); identical results."""
+        v = {"auto": _lib.LAC_PATH_AUTO, "split": _lib.LAC_PATH_SPLIT, "fused": _lib.LAC_PATH_FUSED,
+             "stats": _lib.LAC_PATH_STATS}[path]
         check(self.lib.lac_set_option(self.ctx, _lib.LAC_OPT_DECODE_PATH, v))
 
     def set_path(self, path):

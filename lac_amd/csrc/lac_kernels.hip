@@ -97,24 +97,64 @@ __device__ inline uint64_t readlane_u64(uint64_t v, int l) {
     const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
     return ((uint64_t)hi << 32) | lo;
 }
+// Wave-wide reductions and scans on DPP (data-parallel primitives: VALU operand
+// swizzles, a few cycles each) instead of ds_bpermute shuffles, whose LDS-path
+// latency dominated the sequential per-step kernels.  Within each 16-lane row:
+// quad_perm xor-1, xor-2, row_half_mirror, row_mirror leave the row's total in
+// every lane; readlane of lanes 0/16/32/48 combines the four rows (uniform
+// result).  The inclusive scan is Hillis-Steele over row_shr 1/2/4/8 (bound_ctrl:
+// lanes shifted in from outside the row read 0), then row_bcast15 (rows 1, 3)
+// and row_bcast31 (rows 2, 3).  All callers run with the whole wave active.
+template <int CTRL, int ROWS = 0xF>
+__device__ inline uint32_t dpp32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xF, true);
+}
+template <int CTRL, int ROWS = 0xF>
+__device__ inline uint64_t dpp64(uint64_t v) {
+    return ((uint64_t)dpp32<CTRL, ROWS>((uint32_t)(v >> 32)) << 32) | dpp32<CTRL, ROWS>((uint32_t)v);
+}
+enum : int { kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppHalfMirror = 0x141, kDppMirror = 0x140, kDppShr1 = 0x111,
+             kDppShr2 = 0x112, kDppShr4 = 0x114, kDppShr8 = 0x118, kDppBcast15 = 0x142, kDppBcast31 = 0x143 };
+
+template <typename T, typename Op>
+__device__ inline T wave_reduce(T v, Op op) {
+    if constexpr (sizeof(T) == 8) {
+        v = op(v, (T)dpp64<kDppXor1>((uint64_t)v));
+        v = op(v, (T)dpp64<kDppXor2>((uint64_t)v));
+        v = op(v, (T)dpp64<kDppHalfMirror>((uint64_t)v));
+        v = op(v, (T)dpp64<kDppMirror>((uint64_t)v));
+        const T r0 = (T)readlane_u64((uint64_t)v, 0), r1 = (T)readlane_u64((uint64_t)v, 16);
+        const T r2 = (T)readlane_u64((uint64_t)v, 32), r3 = (T)readlane_u64((uint64_t)v, 48);
+        return op(op(r0, r1), op(r2, r3));
+    } else {
+        v = op(v, (T)dpp32<kDppXor1>((uint32_t)v));
+        v = op(v, (T)dpp32<kDppXor2>((uint32_t)v));
+        v = op(v, (T)dpp32<kDppHalfMirror>((uint32_t)v));
+        v = op(v, (T)dpp32<kDppMirror>((uint32_t)v));
+        const T r0 = (T)__builtin_amdgcn_readlane((int)v, 0), r1 = (T)__builtin_amdgcn_readlane((int)v, 16);
+        const T r2 = (T)__builtin_amdgcn_readlane((int)v, 32), r3 = (T)__builtin_amdgcn_readlane((int)v, 48);
+        return op(op(r0, r1), op(r2, r3));
+    }
+}
 __device__ inline uint64_t wave_sum_u64(uint64_t v) {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) v += shfl_xor_u64(v, m);
-    return v;
+    return wave_reduce(v, [](uint64_t a, uint64_t b) { return a + b; });
 }
 __device__ inline uint64_t wave_min_u64(uint64_t v) {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) { const uint64_t o = shfl_xor_u64(v, m); v = o < v ? o : v; }
-    return v;
+    return wave_reduce(v, [](uint64_t a, uint64_t b) { return a < b ? a : b; });
 }
 __device__ inline uint64_t wave_max_u64(uint64_t v) {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) { const uint64_t o = shfl_xor_u64(v, m); v = o > v ? o : v; }
-    return v;
+    return wave_reduce(v, [](uint64_t a, uint64_t b) { return a > b ? a : b; });
 }
 __device__ inline uint32_t wave_min_u32(uint32_t v) {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) { const uint32_t o = (uint32_t)__shfl_xor((int)v, m); v = o < v ? o : v; }
+    return wave_reduce(v, [](uint32_t a, uint32_t b) { return a < b ? a : b; });
+}
+__device__ inline uint64_t wave_incl_scan_u64(uint64_t v) {
+    v += dpp64<kDppShr1>(v);
+    v += dpp64<kDppShr2>(v);
+    v += dpp64<kDppShr4>(v);
+    v += dpp64<kDppShr8>(v);
+    v += dpp64<kDppBcast15, 0xA>(v);
+    v += dpp64<kDppBcast31, 0xC>(v);
     return v;
 }
 __device__ inline i128 wave_max_i128(i128 v) {
@@ -126,12 +166,6 @@ __device__ inline u128 wave_sum_u128(u128 v) {
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1)
         v += ((u128)shfl_xor_u64((uint64_t)(v >> 64), m) << 64) | shfl_xor_u64((uint64_t)v, m);
-    return v;
-}
-__device__ inline uint64_t wave_incl_scan_u64(uint64_t v) {
-    const int lane = (int)lane_id();
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) { const uint64_t t = shfl_up_u64(v, d); if (lane >= d) v += t; }
     return v;
 }
 constexpr i128 kI128Min = (i128)((u128)1 << 127);
@@ -568,25 +602,35 @@ __device__ inline void scan_chunk(const E *row, int64_t nvec, int64_t cv0, int G
                                   uint64_t *cnt_out, uint64_t *lo_out, uint64_t *hi_out) {
     const int lane = (int)lane_id();
     uint64_t lo_c = cb, hi_c = ~0ull, cnt = 0;
-    for (int g = 0; g < G; g++) {
-        const int64_t vi = cv0 + (int64_t)g * 64 + lane;
-        typename VecT<E, VEC>::type xv;
-        if (vi < nvec) xv = load_vec<E, VEC>(row, vi);
-        else xv = (typename VecT<E, VEC>::type)0;
-        uint64_t loc[VEC], ls = 0;
+    constexpr int PF = 4;                                     // loads in flight: the scan is latency-bound
+    bool done = false;
+    for (int g0 = 0; g0 < G && !done; g0 += PF) {
+        typename VecT<E, VEC>::type xs[PF];
 #pragma unroll
-        for (int j = 0; j < VEC; j++) { ls += (uint64_t)vget<E, VEC>(xv, j); loc[j] = ls; }
-        const uint64_t in = wave_incl_scan_u64(ls);
-        const uint64_t ex = cb + in - ls;
-#pragma unroll
-        for (int j = 0; j < VEC; j++) {
-            const uint64_t ce = ex + loc[j];
-            const bool valid = vi < nvec;
-            if (valid && ce <= tgt) { cnt++; lo_c = ce > lo_c ? ce : lo_c; }
-            if (valid && ce > tgt) hi_c = ce < hi_c ? ce : hi_c;
+        for (int u = 0; u < PF; u++) {
+            const int64_t vi = cv0 + (int64_t)(g0 + u) * 64 + lane;
+            if (g0 + u < G && vi < nvec) xs[u] = load_vec<E, VEC>(row, vi);
+            else xs[u] = (typename VecT<E, VEC>::type)0;
         }
-        cb += readlane_u64(in, 63);
-        if (cb > tgt) break;                                  // later entries all exceed tgt
+#pragma unroll
+        for (int u = 0; u < PF; u++) {
+            if (g0 + u >= G) break;
+            const int64_t vi = cv0 + (int64_t)(g0 + u) * 64 + lane;
+            uint64_t loc[VEC], ls = 0;
+#pragma unroll
+            for (int j = 0; j < VEC; j++) { ls += (uint64_t)vget<E, VEC>(xs[u], j); loc[j] = ls; }
+            const uint64_t in = wave_incl_scan_u64(ls);
+            const uint64_t ex = cb + in - ls;
+#pragma unroll
+            for (int j = 0; j < VEC; j++) {
+                const uint64_t ce = ex + loc[j];
+                const bool valid = vi < nvec;
+                if (valid && ce <= tgt) { cnt++; lo_c = ce > lo_c ? ce : lo_c; }
+                if (valid && ce > tgt) hi_c = ce < hi_c ? ce : hi_c;
+            }
+            cb += readlane_u64(in, 63);
+            if (cb > tgt) { done = true; break; }             // later entries all exceed tgt
+        }
     }
     *cnt_out = wave_sum_u64(cnt);
     *lo_out = wave_max_u64(lo_c);
@@ -923,6 +967,153 @@ __global__ LAC_DEC_BOUNDS void k_decode_wave(const E *__restrict__ pmf, int64_t 
     if (lane == 0) states[b] = st;
 }
 
+// ---------------------------------------------------------- decode, stats path
+// Few streams: the per-step kernels above leave the chip idle (one stream's row
+// per step) and pay a launch per step.  The row statistics a decode step needs
+// -- the <= 64 chunk totals of k_decode_wave's layout, T and minp -- do not
+// depend on the decoder state, so k_dec_stats computes them for every (step,
+// stream) row of a chunk of steps at once (one wave per row, the whole chip),
+// and k_decode_seq walks each stream's steps touching only those 528 bytes plus
+// the one chunk holding the target (1/64 of the row; fudged rows take
+// decode_symbol's full-row form).
+struct DecRowMeta {
+    uint64_t T;            // 0 marks a bad row (empty or total >= 2^64)
+    uint64_t minp;
+};
+
+template <typename E, int VEC>
+__device__ inline void dec_chunk_layout(int64_t V, int64_t *CI, int64_t *nch) {
+    constexpr int U = 8;
+    const int64_t nvec = V / VEC, nit = (nvec + 63) / 64;
+    int64_t ci = (nit + 63) / 64;
+    ci = ((ci + U - 1) / U) * U;
+    *CI = ci;
+    *nch = (nit + ci - 1) / ci;
+}
+
+template <typename E, int VEC>
+__global__ __launch_bounds__(256) void k_dec_stats(const E *__restrict__ pmf, int64_t step_stride,
+                                                   int64_t stream_stride, int64_t B, int64_t rows, int64_t V,
+                                                   int64_t t0, uint64_t *__restrict__ chunks,
+                                                   DecRowMeta *__restrict__ meta) {
+    const int lane = (int)lane_id();
+    const int64_t r = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (r >= rows) return;
+    const E *row = pmf + (t0 + r / B) * step_stride + (r % B) * stream_stride;
+    constexpr int U = 8;
+    const int64_t nvec = V / VEC;
+    int64_t CI, nch;
+    dec_chunk_layout<E, VEC>(V, &CI, &nch);
+    uint64_t mine = 0;
+    E mn = (E)~(E)0;
+    uint32_t ovf = 0;
+    for (int64_t c = 0; c < nch; c++) {
+        uint64_t acc = 0;
+        for (int64_t g0 = 0; g0 < CI; g0 += U) {
+            typename VecT<E, VEC>::type x[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const int64_t vi = (c * CI + g0 + u) * 64 + lane;
+                if (vi < nvec) x[u] = load_vec<E, VEC>(row, vi);
+                else x[u] = (typename VecT<E, VEC>::type)0;
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+#pragma unroll
+                for (int j = 0; j < VEC; j++) {
+                    const E e = vget<E, VEC>(x[u], j);
+                    if constexpr (sizeof(E) == 8) {
+                        const uint64_t n2 = acc + e;
+                        ovf |= n2 < acc;
+                        acc = n2;
+                    } else {
+                        acc += e;
+                    }
+                    const E m1 = e - 1;
+                    mn = m1 < (E)mn ? m1 : (E)mn;
+                }
+            }
+        }
+        uint64_t tsum = acc;
+        if constexpr (sizeof(E) == 8) {
+#pragma unroll
+            for (int m = 32; m >= 1; m >>= 1) {
+                const uint64_t o = shfl_xor_u64(tsum, m);
+                const uint64_t n2 = tsum + o;
+                ovf |= n2 < tsum;
+                tsum = n2;
+            }
+        } else {
+            tsum = wave_sum_u64(tsum);
+        }
+        if (lane == c) mine = tsum;
+    }
+    uint64_t minp;
+    if constexpr (sizeof(E) == 8) minp = wave_min_u64(mn) + 1;
+    else minp = (uint64_t)wave_min_u32(mn) + 1;
+    const u128 acc128 = wave_sum_u128((u128)mine);
+    const bool bad = __any(ovf) || (acc128 >> 64) || acc128 == 0;
+    chunks[r * 64 + lane] = mine;
+    if (lane == 0) meta[r] = DecRowMeta{bad ? 0 : (uint64_t)acc128, minp};
+}
+
+template <typename E, int VEC>
+__global__ LAC_DEC_BOUNDS void k_decode_seq(const E *__restrict__ pmf, int64_t step_stride, int64_t stream_stride,
+                                            int64_t t0, int64_t nsteps, int64_t V, int prec,
+                                            const uint64_t *__restrict__ chunks,
+                                            const DecRowMeta *__restrict__ meta, DecState *states,
+                                            const uint8_t *bits, uint64_t stride, const uint64_t *nbits,
+                                            int32_t *sym_out, int64_t B, int mapping) {
+    const int lane = (int)lane_id();
+    const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (b >= B) return;
+    DecState st = states[b];
+    const uint8_t *mybits = bits + b * stride;
+    const uint64_t mynbits = nbits[b];
+    int64_t CI, nch;
+    dec_chunk_layout<E, VEC>(V, &CI, &nch);
+    uint64_t next = nsteps > 0 ? chunks[b * 64 + lane] : 0;
+    DecRowMeta nmeta = nsteps > 0 ? meta[b] : DecRowMeta{0, 0};
+    for (int64_t i = 0; i < nsteps; i++) {
+        const int64_t t = t0 + i;
+        const uint64_t mine = next;
+        const DecRowMeta rm = nmeta;
+        if (i + 1 < nsteps) {                                  // prefetch: independent of the state
+            next = chunks[((i + 1) * B + b) * 64 + lane];
+            nmeta = meta[(i + 1) * B + b];
+        }
+        int32_t *out = sym_out + t * B + b;
+        if (st.err) {
+            if (lane == 0) *out = -1;
+            continue;
+        }
+        const E *row = pmf + t * step_stride + b * stream_stride;
+        int err = rm.T ? 0 : LAC_E_TABLE;
+        int64_t s = -1;
+        if (!err) {
+            const uint64_t incl = wave_incl_scan_u64(mine);
+            auto find_chunk = [&](uint64_t tgt, int64_t *cv0, int *g, uint64_t *cb) {
+                const uint64_t ex = incl - mine;
+                const bool hit = lane < nch && ex <= tgt && tgt < incl;
+                const uint64_t mask = __ballot(hit);
+                if (!mask) return false;
+                const int src = __ffsll((unsigned long long)mask) - 1;
+                *cv0 = (int64_t)src * CI * 64;
+                *g = (int)CI;
+                *cb = readlane_u64(ex, src);
+                return true;
+            };
+            err = decode_symbol<E, VEC>(st, row, V, rm.T, rm.minp, prec, mapping, mybits, mynbits, find_chunk, &s);
+        }
+        if (err) {
+            st.err = err;
+            st.err_step = st.nsym;
+        }
+        if (lane == 0) *out = err ? -1 : (int32_t)s;
+    }
+    if (lane == 0) states[b] = st;
+}
+
 // ================================================================ q1 logits path
 // Tables computed in-kernel from logits (bf16 or f32) with the integer-exact q1
 // quantiser (include/lac_q1_table.h, DESIGN.md "logits path"), so the pmf never
@@ -1030,9 +1221,8 @@ __device__ inline uint32_t q1_vec_sum(const u32x4 &x, float m, float ms, bool fa
 __device__ inline bool q1_fast_row(float m) { return fabsf(m) <= 0x1p100f; }   // false for inf / NaN
 
 __device__ inline float wave_max_f32(float v) {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m));
-    return v;
+    auto mx = [](uint32_t a, uint32_t b) { return __float_as_uint(fmaxf(__uint_as_float(a), __uint_as_float(b))); };
+    return __uint_as_float(wave_reduce(__float_as_uint(v), mx));
 }
 
 // Sum of R per-lane values across the wave, R at once (R a power of two <= 64):
@@ -1371,12 +1561,13 @@ struct lac_ctx {
     int64_t fused_min_streams = 2048;   // AUTO: fused kernel from this many streams
     int64_t chunk_steps = 64;           // split path: steps per row-stats launch
     int dpath = LAC_PATH_AUTO;          // decode kernel path
-    int64_t wave_decode_min_streams = 1024;
+    int64_t wave_decode_min_streams = 2048;   // measured: the stats path wins at 1024 streams
     int mapping = LAC_MAP_CEIL;         // symbol_to_range flavour (lac_set_option)
     int term = LAC_TERM_FLUSH;          // stream termination flavour
     int cus = 256;                      // compute units (persistent grids)
     int q1_shape = 0;                   // logits stats block shape (0 auto; lac_set_option tuning)
-    uint64_t *q1chunks = nullptr;       // logits decode: [chunk_steps * B][64] chunk totals
+    uint64_t *q1chunks = nullptr;       // logits / stats-path decode: [chunk_steps * B][64] chunk totals
+    void *dmeta = nullptr;              // stats-path decode: [chunk_steps * B] DecRowMeta
     float *q1m = nullptr;               //                [chunk_steps * B] row maxima
     // live kernel timing (lac_profile_enable): hipEvent pairs around launches
     bool prof = false;
@@ -1387,6 +1578,7 @@ struct lac_ctx {
 
 enum { KID_ROW_STATS = 0, KID_ENCODE = 1, KID_FINISH = 2, KID_DECODE = 3, KID_FUSED = 4, KID_DECODE_WAVE = 5,
        KID_Q1_STATS = 6, KID_Q1_DECODE = 7, KID_COUNT = 8 };
+// the stats-path decode (k_dec_stats + k_decode_seq) reports under KID_DECODE
 
 static hipEvent_t ev_get(lac_ctx *c) {
     if (c->ev_next == c->ev_pool.size()) {
@@ -1538,12 +1730,47 @@ static int decode_wave_launch(lac_ctx *c, const E *pmf, int64_t step_stride, int
     return LAC_OK;
 }
 
+static int ensure_chunk_buffers(lac_ctx *c) {
+    if (!c->q1chunks) HIPCHK(hipMalloc(&c->q1chunks, sizeof(uint64_t) * 64 * c->chunk_steps * c->B));
+    if (!c->q1m) HIPCHK(hipMalloc(&c->q1m, sizeof(float) * c->chunk_steps * c->B));
+    if (!c->dmeta) HIPCHK(hipMalloc(&c->dmeta, sizeof(DecRowMeta) * c->chunk_steps * c->B));
+    return LAC_OK;
+}
+
+template <typename E, int VEC>
+static int decode_stats_path(lac_ctx *c, const E *pmf, int64_t step_stride, int64_t stream_stride, int64_t steps,
+                             int32_t *out, hipStream_t st) {
+    int rc = ensure_chunk_buffers(c);
+    if (rc) return rc;
+    const unsigned blocks = (unsigned)((c->B + kWavesPerBlock - 1) / kWavesPerBlock);
+    for (int64_t t0 = 0; t0 < steps; t0 += c->chunk_steps) {
+        const int64_t n = (steps - t0) < c->chunk_steps ? (steps - t0) : c->chunk_steps;
+        const int64_t rows = n * c->B;
+        ProfScope ps(c, KID_DECODE, st);
+        k_dec_stats<E, VEC><<<(unsigned)((rows + kWavesPerBlock - 1) / kWavesPerBlock), 64 * kWavesPerBlock, 0, st>>>(
+            pmf, step_stride, stream_stride, c->B, rows, c->V, t0, c->q1chunks, (DecRowMeta *)c->dmeta);
+        CHECK_LAUNCH();
+        k_decode_seq<E, VEC><<<blocks, 64 * kWavesPerBlock, 0, st>>>(
+            pmf, step_stride, stream_stride, t0, n, c->V, c->prec, c->q1chunks, (const DecRowMeta *)c->dmeta, c->dec,
+            c->dbits, c->dstride, c->dnbits, out, c->B, c->mapping);
+        CHECK_LAUNCH();
+    }
+    return LAC_OK;
+}
+
 static int decode_dispatch(lac_ctx *c, const void *pmf, int64_t step_stride, int64_t stream_stride, int64_t steps,
                            int32_t *out, hipStream_t st) {
     const uintptr_t p = (uintptr_t)pmf;
     const bool wave = c->dpath == LAC_PATH_FUSED || (c->dpath == LAC_PATH_AUTO && c->B >= c->wave_decode_min_streams);
     const int vw = c->pmf_bits == 32 ? 4 : 2;
     const bool vec = (p % 16 == 0) && c->V % vw == 0 && step_stride % vw == 0 && stream_stride % vw == 0;
+    if (c->dpath == LAC_PATH_STATS || (c->dpath == LAC_PATH_AUTO && !wave)) {
+        if (c->pmf_bits == 32)
+            return vec ? decode_stats_path<uint32_t, 4>(c, (const uint32_t *)pmf, step_stride, stream_stride, steps, out, st)
+                       : decode_stats_path<uint32_t, 1>(c, (const uint32_t *)pmf, step_stride, stream_stride, steps, out, st);
+        return vec ? decode_stats_path<uint64_t, 2>(c, (const uint64_t *)pmf, step_stride, stream_stride, steps, out, st)
+                   : decode_stats_path<uint64_t, 1>(c, (const uint64_t *)pmf, step_stride, stream_stride, steps, out, st);
+    }
     if (wave) {
         if (c->pmf_bits == 32)
             return vec ? decode_wave_launch<uint32_t, 4>(c, (const uint32_t *)pmf, step_stride, stream_stride, steps, out, st)
@@ -1687,10 +1914,8 @@ static int q1_encode_job(lac_ctx *c, const Q1Args &a0, int64_t steps, uint64_t *
 
 template <typename LT>
 static int q1_decode(lac_ctx *c, const Q1Args &a0, int64_t steps, int32_t *out, hipStream_t st) {
-    if (!c->q1chunks) {
-        HIPCHK(hipMalloc(&c->q1chunks, sizeof(uint64_t) * 64 * c->chunk_steps * c->B));
-        HIPCHK(hipMalloc(&c->q1m, sizeof(float) * c->chunk_steps * c->B));
-    }
+    int rc0 = ensure_chunk_buffers(c);
+    if (rc0) return rc0;
     const unsigned blocks = (unsigned)((c->B + kWavesPerBlock - 1) / kWavesPerBlock);
     const int64_t nvec = c->V / LogitN<LT>::N;
     for (int64_t t0 = 0; t0 < steps; t0 += c->chunk_steps) {
@@ -1769,6 +1994,7 @@ int lac_close(lac_ctx *c) {
     (void)hipFree(c->planeC);
     (void)hipFree(c->nbits);
     (void)hipFree(c->q1chunks);
+    (void)hipFree(c->dmeta);
     (void)hipFree(c->q1m);
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
     delete c;
@@ -1808,7 +2034,7 @@ int lac_set_option(lac_ctx *c, int option, int64_t value) {
         c->fused_min_streams = value;
         return LAC_OK;
     case LAC_OPT_DECODE_PATH:
-        if (value < LAC_PATH_AUTO || value > LAC_PATH_FUSED) return fail(LAC_E_ARG, "bad decode path");
+        if (value < LAC_PATH_AUTO || value > LAC_PATH_STATS) return fail(LAC_E_ARG, "bad decode path");
         c->dpath = (int)value;
         return LAC_OK;
     case LAC_OPT_Q1_SHAPE:

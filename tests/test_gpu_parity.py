@@ -52,16 +52,20 @@ def _gpu_encode(pmf_np, sym_np, prec, trace=False, path="auto", job=False):
     return c, pmf, data, n, tr
 
 
+DECODE_PATHS = ("split", "fused", "stats")
+
+
 def _decode_both(c, dpmf):
-    """Decode with the per-step workgroup kernel and the one-launch wave kernel;
-    both must agree.  Returns the symbols."""
+    """Decode with the per-step workgroup kernel, the one-launch wave kernel and
+    the stats path; all must agree.  Returns the symbols."""
     outs = []
-    for path in ("split", "fused"):
+    for path in DECODE_PATHS:
         c.set_decode_path(path)
         c.decode_open()
         outs.append(c.decode(dpmf).cpu().numpy())
     c.set_decode_path("auto")
-    assert (outs[0] == outs[1]).all()
+    for o in outs[1:]:
+        assert (outs[0] == o).all()
     return outs[0]
 
 
@@ -165,7 +169,7 @@ def test_decode_external_bits_from_oracle():
     c = _coder(V, B, prec)
     bits = torch.from_numpy(buf).to(DEV)
     nbits = torch.from_numpy(nb.astype(np.int64)).to(DEV)
-    for path in ("split", "fused"):
+    for path in DECODE_PATHS:
         c.set_decode_path(path)
         c.decode_open(bits, nbits)
         dec = c.decode(_dev_pmf(pmf)).cpu().numpy()
@@ -208,7 +212,7 @@ def test_headline_shape_softmax_tables():
     assert rc == 0
     for i, b in enumerate(sample):
         assert data[b] == out[i, :(int(nb[i]) + 7) // 8].tobytes()
-    for path in ("split", "fused"):
+    for path in DECODE_PATHS:
         c.set_decode_path(path)
         c.decode_open()
         assert torch.equal(c.decode(pmf), sym)
@@ -280,7 +284,7 @@ def _determined_case(rows, syms, extra, count, prec, data, L):
     buf[0, :len(data)] = np.frombuffer(data, dtype=np.uint8)
     c = _coder(V, 1, prec, bits=64)
     out = {}
-    for path in ("split", "fused"):
+    for path in DECODE_PATHS:
         c.set_decode_path(path)
         c.decode_open(torch.from_numpy(buf).to(DEV), torch.tensor([L], dtype=torch.int64, device=DEV))
         dec = c.decode(torch.from_numpy(tab.view(np.int64).reshape(n, 1, V)).to(DEV)).cpu().numpy()[:, 0]
