@@ -133,3 +133,77 @@ class TinyCausalLM:
                 return self.head(self.body(h, mask=mask, is_causal=True))
 
         return _M()
+
+
+class LogitsCompressor:
+    """Batched LLM compression on the GPU through the logits path (SURVEY §8(f) 1 + 3).
+
+    ``compress(tokens[B, T])`` runs the causal LM once, teacher-forced on
+    ``[BOS] + tokens[:, :-1]`` (llama_compress.py primes with BOS = 1, :20-23),
+    and hands its logits -- cast to ``logits_dtype``, still [B, T, V] in HBM --
+    straight to ``BatchCoder.encode_logits_job`` as a strided [T, B, V] view: the
+    q1 tables are computed in-kernel and no pmf is ever written.
+
+    ``decompress`` must see bit-identical logits.  It re-runs the *same*
+    fixed-shape forward ([B, T], not-yet-decoded positions filled with 0) before
+    each step: under the causal mask position t never depends on later positions,
+    and equal shapes select the same kernels, so row t is computed by the
+    identical op sequence as in ``compress``.  (An incremental KV-cache decode
+    would change shapes and kernels, and with them the low bits of the logits.)
+    O(T) forwards: a demonstration driver, not a serving loop.
+    """
+
+    def __init__(self, module, vocab, prec=48, bos=1, logits_dtype=None, device="cuda"):
+        import torch
+        self.module = module.to(device).eval()
+        self.vocab, self.prec, self.bos = int(vocab), int(prec), int(bos)
+        self.dtype = logits_dtype or torch.bfloat16
+        self.device = torch.device(device)
+
+    def _logits(self, ctx):
+        import torch
+        with torch.no_grad():
+            return self.module(ctx).to(self.dtype).contiguous()
+
+    def _coder(self, B, T):
+        from .batch import BatchCoder
+        return BatchCoder(self.vocab, B, prec=self.prec, pmf_bits=32, capacity_bits=T * (self.prec + 2) + 256,
+                          device=self.device)
+
+    def compress(self, tokens):
+        """tokens: int tensor [B, T] -> (list of B byte strings, nbits uint64[B])."""
+        import torch
+        tokens = tokens.to(self.device, torch.long)
+        B, T = tokens.shape
+        ctx = torch.cat([torch.full((B, 1), self.bos, dtype=torch.long, device=self.device), tokens[:, :-1]], 1)
+        lg = self._logits(ctx)                                   # [B, T, V]
+        coder = self._coder(B, T)
+        coder.encode_logits_job(lg.transpose(0, 1), tokens.t().contiguous().to(torch.int32))
+        out = coder.to_bytes()
+        coder.close()
+        return out
+
+    def decompress(self, data, nbits, T):
+        """Inverse of compress: B byte strings + bit counts -> tokens [B, T] (long)."""
+        import torch
+        B = len(data)
+        stride = max(8, (max((len(d) for d in data), default=0) + 8) // 8 * 8)
+        buf = np.zeros((B, stride), dtype=np.uint8)
+        for b, d in enumerate(data):
+            buf[b, :len(d)] = np.frombuffer(d, dtype=np.uint8)
+        coder = self._coder(B, T)
+        bits = torch.from_numpy(buf).to(self.device)
+        nb = torch.as_tensor(np.asarray(nbits, dtype=np.int64), device=self.device)
+        coder.decode_open(bits, nb)
+        ctx = torch.zeros((B, T), dtype=torch.long, device=self.device)
+        ctx[:, 0] = self.bos
+        out = torch.empty((B, T), dtype=torch.long, device=self.device)
+        for t in range(T):
+            lg = self._logits(ctx)[:, t:t + 1, :]                # [B, 1, V]
+            s = coder.decode_logits(lg.transpose(0, 1))[0].to(torch.long)
+            out[:, t] = s
+            if t + 1 < T:
+                ctx[:, t + 1] = s
+        coder.raise_on_error()
+        coder.close()
+        return out

@@ -193,6 +193,29 @@ def test_llama_ac_adapter_with_torch_model_roundtrip():
     assert list(ac.from_bin.run(bits, stop=0, n=len(toks))) == toks
 
 
+def test_logits_compressor_roundtrip_and_oracle():
+    """LLM compression through the logits path: one teacher-forced forward, bf16
+    logits straight into the coder; bytes == q1 oracle + encode oracle on the same
+    logits; the fixed-shape decode loop reproduces the tokens."""
+    from lac_amd.llm import LogitsCompressor, TinyCausalLM
+    from oracle import oracle as coracle
+    V, B, T, prec = 1024, 4, 24, 48
+    model = TinyCausalLM(vocab=V, d=32, layers=1, heads=2, max_len=64)
+    lc = LogitsCompressor(model, V, prec=prec, device="cuda:0")
+    toks = torch.from_numpy(np.random.default_rng(5).integers(0, V, (B, T))).to("cuda:0")
+    data, nbits = lc.compress(toks)
+    ctx = torch.cat([torch.ones((B, 1), dtype=torch.long, device="cuda:0"), toks[:, :-1]], 1)
+    lg = lc._logits(ctx)                                        # [B, T, V] bf16, as compress saw it
+    host = lg.transpose(0, 1).contiguous().view(torch.int16).cpu().numpy().view(np.uint16)
+    pmf = coracle.q1_quantize(host, prec)
+    out, nb, status, rc = coracle.encode_batch(pmf, toks.t().contiguous().cpu().numpy().astype(np.int32), prec)
+    assert rc == 0
+    for b in range(B):
+        assert int(nbits[b]) == int(nb[b]) and data[b] == out[b, :(int(nb[b]) + 7) // 8].tobytes()
+    back = lc.decompress(data, nbits, T)
+    assert torch.equal(back, toks)
+
+
 def test_quantiser_matches_reference_numpy_ops():
     """quantise_logits is the reference's float64 numpy quantiser (llama_compress.py:24-30)."""
     from lac_amd.llm import quantise_logits
