@@ -181,10 +181,11 @@ int lac_decode_steps(lac_ctx *ctx, const void *pmf_dev, int64_t step_stride, int
 /* ---- logits path --------------------------------
  * Tables are computed in-kernel from raw logits with the integer-exact "q1"
  * quantiser instead of being read from a pmf in HBM: for each row
- *   m = max_i x_i (NaN ignored),  d_i = min(m - x_i, 17) in f32 (NaN -> 17),
- *   q_i = max(1, TAB[floor(32 d_i)] >> (24 - k)),  TAB[i] = round(2^24 e^(-i/32))
- * i.e. softmax to 1/32-nat resolution (include/lac_q1_table.h; DESIGN.md
- * "logits path"), with
+ *   m = max_i x_i (NaN ignored),  c = RNE_f32(544 - 32 m),
+ *   j_i = sat_u32(fmaf(x_i, 32, c)) capped at 544 (NaN, -inf, negatives -> 0),
+ *   q_i = max(1, TAB[544 - j_i] >> (24 - k)),  TAB[i] = round(2^24 e^(-i/32))
+ * i.e. softmax to 1/32-nat resolution, gaps clamped at 17 nats
+ * (include/lac_q1_table.h; DESIGN.md "logits path"), with
  * k = lac_q1_k(prec, vocab) = min(24, prec - 1 - ceil(log2 vocab)) so that
  * T <= 2^(prec-1) and no row is ever fudged.  It replaces the float64 numpy
  * quantiser of llama_compress.py:29-36 (whose output is platform-dependent)

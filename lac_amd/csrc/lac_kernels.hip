@@ -1147,28 +1147,42 @@ __device__ inline u32x4 ld16(const void *row, int64_t vi, bool nt) {
     return nt ? __builtin_nontemporal_load(p) : *p;
 }
 
-// q1 on the GPU (spec: include/lac_q1_table.h).  tab[] is the per-launch LDS
-// copy of max(1, LAC_Q1_TAB[i] >> (KMAX - k)), so one lookup is the whole map;
-// fminf returns DMAX for a NaN difference, as the spec's clamp does; d * STEPS is
-// exact and d >= 0, so the conversion is the floor.
-__device__ inline uint32_t q1_val(float x, float m, const uint32_t *tab) {
-    const float d = fminf(m - x, (float)LAC_Q1_DMAX);
-    return tab[(uint32_t)(d * (float)LAC_Q1_STEPS)];
-}
+// q1 on the GPU (spec: include/lac_q1_table.h, oracle/lac_oracle.c).  With
+// L = DMAX*STEPS (544): c = RNE(L - 32 m) once per row, y = fma(x, 32, c) per
+// logit, j = sat_u32(y) capped at L, q = tabj[j] where the LDS tables hold
+// max(1, TAB[L - j] >> (KMAX - k)) (j-indexed).  sat_u32 is v_cvt_u32_f32's own
+// saturation (NaN, -inf and negatives -> 0, >= 2^32 -> 2^32-1), written as asm
+// because a C++ cast of such values is undefined and the optimiser may use that.
+constexpr int kQ1L = LAC_Q1_DMAX * LAC_Q1_STEPS;
 
-__device__ inline uint32_t q1_entry(int i, uint32_t xsh) {
-    const uint32_t v = c_q1_tab[i] >> xsh;
+__device__ inline uint32_t cvt_sat_u32(float y) {
+    uint32_t r;
+    asm("v_cvt_u32_f32 %0, %1" : "=v"(r) : "v"(y));
+    return r;
+}
+__device__ inline float q1_c(float m) { return (float)kQ1L - (float)LAC_Q1_STEPS * m; }   // 32 m exact
+__device__ inline uint32_t q1_j(float x, float c) {                          // general (capped) form
+    const uint32_t j = cvt_sat_u32(fmaf(x, (float)LAC_Q1_STEPS, c));
+    return j < (uint32_t)kQ1L ? j : (uint32_t)kQ1L;
+}
+// |m| < 2^18: |L - 32m| < 2^24 so c is within 0.5 of L - 32m and every y <= 544.5:
+// the cap is provably idle and the fast path drops it.
+__device__ inline bool q1_fast_row(float m) { return fabsf(m) < 0x1p18f; }   // false for inf / NaN
+
+__device__ inline uint32_t q1_entry(int j, uint32_t xsh) {
+    const uint32_t v = c_q1_tab[kQ1L - j] >> xsh;
     return v ? v : 1u;
 }
 
-// The per-launch LDS table of q1_val (all threads of the block, then a barrier).
+// The per-launch j-indexed LDS table (all threads of the block, then a barrier).
 __device__ inline void q1_load_tab(uint32_t *tab, uint32_t xsh) {
     for (int i = threadIdx.x; i < LAC_Q1_TAB_SIZE; i += blockDim.x) tab[i] = q1_entry(i, xsh);
     __syncthreads();
 }
+__device__ inline uint32_t q1_val(float x, float c, const uint32_t *tab) { return tab[q1_j(x, c)]; }
 
-// Lane-private replicated table for the row-stats kernel: entry i, copy c at
-// dword i*32 + c.  A wave64 ds_read_b32 is serviced as two 32-lane groups over 32
+// Lane-private replicated table for the row-stats kernel: entry j, copy c at
+// dword j*32 + c.  A wave64 ds_read_b32 is serviced as two 32-lane groups over 32
 // banks (bank = dword mod 32); lane l reads copy l & 31, so every lookup of a
 // group hits 32 distinct banks whatever the indices -- no bank conflicts for the
 // random gather (a single shared copy measured 68 % conflict cycles).
@@ -1178,47 +1192,35 @@ __device__ inline void q1_load_tab_rep(uint32_t *tabr, uint32_t xsh) {
     __syncthreads();
 }
 
-__device__ inline uint32_t q1_rep_at(const uint32_t *tabr, uint32_t i, uint32_t loff) {
-    return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(tabr) + ((i << 7) | loff));
+__device__ inline uint32_t q1_rep_at(const uint32_t *tabr, uint32_t j, uint32_t loff) {
+    return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(tabr) + ((j << 7) | loff));
 }
 
 // Sum of q1 over the N logits of one 16-B vector (replicated table, loff = byte
-// offset of this lane's copy).  For a row max |m| <= 2^100 the scaled difference
-// is y = fma(x, -STEPS, STEPS m) = RNE(STEPS m - STEPS x), which equals
-// STEPS * RNE(m - x) exactly (power-of-two scaling commutes with rounding; STEPS m
-// is exact; a difference too small to be normal gives index 0 either way, one too
-// large to be finite clamps either way), two logits per v_pk_fma_f32; fminf sends
-// NaN to the last entry as the spec's clamp does.  Other rows (max +-inf, NaN or
-// beyond 2^100) take the literal form.  Entries are <= 2^24, so a lane's sum of
-// up to 128 entries fits 32 bits.
+// offset of this lane's copy).  Fast rows: two logits per v_pk_fma_f32, then the
+// saturating conversion is the whole index computation.  Entries are <= 2^24, so
+// a lane's sum of up to 128 entries fits 32 bits.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 template <typename LT>
-__device__ inline uint32_t q1_vec_sum(const u32x4 &x, float m, float ms, bool fast, const uint32_t *tabr,
-                                      uint32_t loff) {
+__device__ inline uint32_t q1_vec_sum(const u32x4 &x, float c, bool fast, const uint32_t *tabr, uint32_t loff) {
     constexpr int N = LogitN<LT>::N;
-    constexpr float kLast = (float)(LAC_Q1_DMAX * LAC_Q1_STEPS);
     uint32_t s = 0;
     if (fast) {
-        const f32x2 k = {-(float)LAC_Q1_STEPS, -(float)LAC_Q1_STEPS}, c = {ms, ms};
+        const f32x2 k = {(float)LAC_Q1_STEPS, (float)LAC_Q1_STEPS}, cc = {c, c};
 #pragma unroll
         for (int j = 0; j < N; j += 2) {
             const f32x2 v = {logit_at<LT>(x, j), logit_at<LT>(x, j + 1)};
-            const f32x2 y = __builtin_elementwise_fma(v, k, c);
-            s += q1_rep_at(tabr, (uint32_t)fminf(y.x, kLast), loff);
-            s += q1_rep_at(tabr, (uint32_t)fminf(y.y, kLast), loff);
+            const f32x2 y = __builtin_elementwise_fma(v, k, cc);
+            s += q1_rep_at(tabr, cvt_sat_u32(y.x), loff);
+            s += q1_rep_at(tabr, cvt_sat_u32(y.y), loff);
         }
     } else {
 #pragma unroll
-        for (int j = 0; j < N; j++) {
-            const float d = fminf(m - logit_at<LT>(x, j), (float)LAC_Q1_DMAX);
-            s += q1_rep_at(tabr, (uint32_t)(d * (float)LAC_Q1_STEPS), loff);
-        }
+        for (int j = 0; j < N; j++) s += q1_rep_at(tabr, q1_j(logit_at<LT>(x, j), c), loff);
     }
     return s;
 }
-
-__device__ inline bool q1_fast_row(float m) { return fabsf(m) <= 0x1p100f; }   // false for inf / NaN
 
 __device__ inline float wave_max_f32(float v) {
     auto mx = [](uint32_t a, uint32_t b) { return __float_as_uint(fmaxf(__uint_as_float(a), __uint_as_float(b))); };
@@ -1259,7 +1261,7 @@ __device__ inline u32x4 neg_inf16(int type_bytes) {
 // thread holds R 16-B vectors of its row in registers (vector gt + NT*j of each
 // NT*R-vector tile, NT = 64*RW), so a row of <= NT*R vectors is read from HBM
 // exactly once: register max -> group max -> q1 sums from the same registers.
-// With PF the next row's loads are issued before this row's arithmetic.  Longer
+// With PF (rolling prefetch) the next row streams in while this one computes.  Longer
 // rows (MULTI) take several tiles and re-read all but the last from the MALL.
 //   encode (DEC = false): RowStats {lo, hi, T} of the row's symbol for k_encode;
 //   decode (DEC = true):  the row max and 64 chunk totals (chunk c = vectors
@@ -1302,7 +1304,7 @@ __global__ __launch_bounds__(64 * kQ1Waves, 4) void k_q1_stats(const LT *__restr
     const int ntiles = MULTI ? (nvec + NT * R - 1) / (NT * R) : 1;
     const int64_t stride = (int64_t)gridDim.x * NR;
     auto row_of = [&](int64_t r) { return lg + (t0 + r / B) * step_stride + (r % B) * stream_stride; };
-    u32x4 x[R], xn[R];
+    u32x4 x[R];
     if (PF && !MULTI) {
         const int64_t r0 = (int64_t)blockIdx.x * NR + g;
         q1_load_tile<LT, R>(x, r0 < rows ? row_of(r0) : lg, r0 < rows, 0, gt, NT, nvec);
@@ -1321,12 +1323,7 @@ __global__ __launch_bounds__(64 * kQ1Waves, 4) void k_q1_stats(const LT *__restr
                     for (int e = 0; e < N; e++) mx = fmaxf(mx, logit_at<LT>(x[j], e));
             }
         } else {
-            if (PF) {
-                const int64_t rn = r + stride;
-                q1_load_tile<LT, R>(xn, rn < rows ? row_of(rn) : lg, rn < rows, 0, gt, NT, nvec);
-            } else {
-                q1_load_tile<LT, R>(x, row, valid, 0, gt, NT, nvec);
-            }
+            if (!PF) q1_load_tile<LT, R>(x, row, valid, 0, gt, NT, nvec);   // PF: loaded during the last row
 #pragma unroll
             for (int j = 0; j < R; j++)
 #pragma unroll
@@ -1340,7 +1337,7 @@ __global__ __launch_bounds__(64 * kQ1Waves, 4) void k_q1_stats(const LT *__restr
 #pragma unroll
         for (int i = 1; i < RW; i++) m = fmaxf(m, smax[g * RW + i]);
         const bool fast = q1_fast_row(m);
-        const float ms = m * (float)LAC_Q1_STEPS;
+        const float c = q1_c(m);
         int sfull = -1, sr = 0;
         if (!DEC && valid) {
             const int64_t s = sym[(t0 + r / B) * B + r % B];
@@ -1349,6 +1346,12 @@ __global__ __launch_bounds__(64 * kQ1Waves, 4) void k_q1_stats(const LT *__restr
             sr = sc - sfull * N;
         }
         uint32_t tot = 0, lo = 0;
+        if (sizeof(LT) == 2) {
+            // opaque to the optimiser: pass 2 re-unpacks the bf16 pairs instead of keeping
+            // pass 1's 8*R unpacked floats live across the barrier (that spilled)
+#pragma unroll
+            for (int j = 0; j < R; j++) asm volatile("" : "+v"(x[j]));
+        }
         for (int tile = ntiles - 1; tile >= 0; tile--) {
             if (MULTI && tile != ntiles - 1) q1_load_tile<LT, R>(x, row, valid, tile * NT * R, gt, NT, nvec);
             uint64_t sv[R];
@@ -1364,8 +1367,7 @@ __global__ __launch_bounds__(64 * kQ1Waves, 4) void k_q1_stats(const LT *__restr
                         uint32_t pl = 0, ps = 0;
 #pragma unroll
                         for (int e = 0; e < N; e++) {
-                            const float d = fminf(m - logit_at<LT>(x[j], e), (float)LAC_Q1_DMAX);
-                            const uint32_t q = q1_rep_at(tabr, (uint32_t)(d * (float)LAC_Q1_STEPS), loff);
+                            const uint32_t q = q1_rep_at(tabr, q1_j(logit_at<LT>(x[j], e), c), loff);
                             pl += e < sr ? q : 0;
                             ps += e == sr ? q : 0;
                         }
@@ -1374,12 +1376,24 @@ __global__ __launch_bounds__(64 * kQ1Waves, 4) void k_q1_stats(const LT *__restr
                     }
                 }
             };
+            // rolling prefetch (PF): once vector j is consumed its registers load vector j of
+            // the block's next row, so those loads overlap the rest of this row's work
+            const int64_t rn = r + stride;
+            const bool nvalid = rn < rows;
+            const LT *nrow = nvalid ? row_of(rn) : lg;
+            auto roll = [&](int j) {
+                if (PF && !MULTI) {
+                    const int vi = gt + NT * j;
+                    x[j] = nvalid && vi < nvec ? ld16(nrow, vi, LAC_Q1_NT) : neg_inf16(sizeof(LT));
+                    __builtin_amdgcn_sched_barrier(0);         // keep the load after vector j's use
+                }
+            };
             if (fast) {                                        // row-uniform branch, outside the vector loop
 #pragma unroll
-                for (int j = 0; j < R; j++) take(j, q1_vec_sum<LT>(x[j], m, ms, true, tabr, loff));
+                for (int j = 0; j < R; j++) { take(j, q1_vec_sum<LT>(x[j], c, true, tabr, loff)); roll(j); }
             } else {
 #pragma unroll
-                for (int j = 0; j < R; j++) take(j, q1_vec_sum<LT>(x[j], m, ms, false, tabr, loff));
+                for (int j = 0; j < R; j++) { take(j, q1_vec_sum<LT>(x[j], c, false, tabr, loff)); roll(j); }
             }
             if (DEC) {
                 const uint64_t gsum = wave_multi_sum<R>(sv);  // group total of index lane / (64/R)
@@ -1412,10 +1426,6 @@ __global__ __launch_bounds__(64 * kQ1Waves, 4) void k_q1_stats(const LT *__restr
             st.inv_tot = 1.0 / (double)T;
             st.pad = 0;
             out[r] = st;
-        }
-        if (PF && !MULTI) {
-#pragma unroll
-            for (int j = 0; j < R; j++) x[j] = xn[j];
         }
     }
 }
@@ -1451,7 +1461,7 @@ __global__ LAC_DEC_BOUNDS void k_q1_decode(const LT *__restrict__ lg, int64_t st
             continue;
         }
         const LT *row = lg + t * step_stride + b * stream_stride;
-        const float m = mrow[r];
+        const float c = q1_c(mrow[r]);
         const uint64_t T = wave_sum_u64(mine);
         const uint64_t incl = wave_incl_scan_u64(mine);
         int err = 0;
@@ -1476,7 +1486,7 @@ __global__ LAC_DEC_BOUNDS void k_q1_decode(const LT *__restrict__ lg, int64_t st
                     uint64_t loc[N], ls = 0;
 #pragma unroll
                     for (int j = 0; j < N; j++) {
-                        ls += vi < nvec ? q1_val(logit_at<LT>(xv, j), m, tab) : 0u;
+                        ls += vi < nvec ? q1_val(logit_at<LT>(xv, j), c, tab) : 0u;
                         loc[j] = ls;
                     }
                     const uint64_t in = wave_incl_scan_u64(ls);
@@ -1533,12 +1543,12 @@ __global__ __launch_bounds__(256) void k_quantize_logits(const LT *__restrict__ 
 #pragma unroll
         for (int j = 0; j < N; j++) mx = fmaxf(mx, logit_at<LT>(x, j));
     }
-    const float m = wave_max_f32(mx);
+    const float c = q1_c(wave_max_f32(mx));
     uint32_t *o = out + r * V;
     for (int64_t vi = lane; vi < nvec; vi += 64) {
         const u32x4 x = ld16(row, vi, true);
 #pragma unroll
-        for (int j = 0; j < N; j++) o[vi * N + j] = q1_val(logit_at<LT>(x, j), m, tab);
+        for (int j = 0; j < N; j++) o[vi * N + j] = q1_val(logit_at<LT>(x, j), c, tab);
     }
 }
 

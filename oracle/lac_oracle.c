@@ -339,9 +339,12 @@ int lacref_acsampler_encode(const uint64_t *cdf, int64_t V, const int32_t *toks,
 }
 
 /* ---- q1 logits quantiser (DESIGN.md "logits path"): bf16 (type 1) or f32 (type 2)
- * logits -> uint32 pmf.  m = max (fmaxf: NaN ignored), d = m - x (f32), clamped
- * to 17 (NaN too), i = floor(d * 32), q = max(1, TAB[i] >> (24 - k)),
- * TAB[i] = round(2^24 e^(-i/32)), k = min(24, prec-1-ceil(log2 V)). */
+ * logits -> uint32 pmf.  With L = DMAX*STEPS = 544:
+ *   m = max_i x_i (fmaxf: NaN ignored),  c = RNE_f32(L - 32 m),
+ *   y = fmaf(x, 32, c) (one rounding),  j = 0 if y is NaN or y <= 0, else min(trunc(y), L),
+ *   q = max(1, TAB[L - j] >> (24 - k)),  TAB[i] = round(2^24 e^(-i/32)),
+ *   k = min(24, prec-1-ceil(log2 V)).
+ * i = L - j is the logit gap m - x in 1/32-nat steps (rounded up), clamped at 17 nats. */
 static inline float q1_load(const void *x, int type, int64_t i) {
     if (type == 1) {
         uint32_t u = (uint32_t)((const uint16_t *)x)[i] << 16;
@@ -365,11 +368,16 @@ int lacref_q1_quantize(const void *x, int type, int64_t V, int prec, uint32_t *q
     if (k < 1 || (type != 1 && type != 2)) return R_E_ARG;
     float m = -INFINITY;
     for (int64_t i = 0; i < V; i++) m = fmaxf(m, q1_load(x, type, i));
+    const int L = LAC_Q1_DMAX * LAC_Q1_STEPS;
+    volatile float m32 = (float)LAC_Q1_STEPS * m;                     /* exact (power of two) */
+    volatile float c = (float)L - m32;                                 /* one f32 rounding */
     for (int64_t i = 0; i < V; i++) {
-        volatile float d = m - q1_load(x, type, i);
-        float dc = d < (float)LAC_Q1_DMAX ? d : (float)LAC_Q1_DMAX;      /* NaN compares false */
-        uint32_t idx = (uint32_t)(dc * (float)LAC_Q1_STEPS);
-        uint32_t v = Q1_TAB[idx] >> (LAC_Q1_KMAX - k);
+        const float y = fmaf(q1_load(x, type, i), (float)LAC_Q1_STEPS, c);
+        uint32_t j;
+        if (!(y > 0.0f)) j = 0;                                         /* NaN, -inf, negative, zero */
+        else if (y >= (float)L) j = (uint32_t)L;
+        else j = (uint32_t)y;                                           /* truncation */
+        uint32_t v = Q1_TAB[L - j] >> (LAC_Q1_KMAX - k);
         q[i] = v ? v : 1u;
     }
     return R_OK;

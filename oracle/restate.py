@@ -312,6 +312,32 @@ def acsampler_encode(cdf, tokens, prec=48):
 
 
 # ------------------------------------------------ q1 logits quantiser (this repo's format)
+def _fmaf(x, k, c):
+    """Correctly rounded float32 fma(x, k, c) for float32 arrays (k a power of
+    two): the float64 sum is used when it is exact (TwoSum check), otherwise the
+    exact rational value is rounded with Fraction."""
+    import numpy as np
+    from fractions import Fraction
+    x = np.asarray(x, dtype=np.float32)
+    kx = x.astype(np.float64) * float(k)                               # exact
+    cc = np.broadcast_to(np.asarray(c, dtype=np.float32).astype(np.float64), kx.shape)
+    with np.errstate(invalid="ignore", over="ignore"):
+        s = kx + cc
+        exact = ((s - kx) == cc) & ((s - cc) == kx)
+        out = s.astype(np.float32)
+    for idx in zip(*np.nonzero(~exact & np.isfinite(kx) & np.isfinite(cc))):
+        v = Fraction(float(kx[idx])) + Fraction(float(cc[idx]))
+        f = np.float32(float(v))                                       # nearest double, then nearest float
+        if not np.isfinite(f):                                         # overflow: IEEE rounds to inf
+            out[idx] = f
+            continue
+        lo, hi = np.nextafter(f, np.float32(-np.inf)), np.nextafter(f, np.float32(np.inf))
+        cands = [t for t in (lo, f, hi) if np.isfinite(t)]
+        best = min((abs(Fraction(float(t)) - v), int(np.float32(t).view(np.uint32)) & 1, t) for t in cands)
+        out[idx] = best[2]
+    return out
+
+
 def q1_quantize(logits_f32, prec, tab):
     """Independent numpy restatement of the q1 quantiser for rows
     of float32 logits (bf16 inputs: widen the bit pattern << 16 first)."""
@@ -319,10 +345,12 @@ def q1_quantize(logits_f32, prec, tab):
     x = np.asarray(logits_f32, dtype=np.float32)
     V = x.shape[-1]
     k = min(24, prec - 1 - (V - 1).bit_length())
+    L = 17 * 32
     m = np.fmax.reduce(x, axis=-1, keepdims=True).astype(np.float32)
-    with np.errstate(invalid="ignore"):
-        d = (m - x).astype(np.float32)
-        d = np.where(d < np.float32(17.0), d, np.float32(17.0))            # NaN -> 17
-    i = (d * np.float32(32.0)).astype(np.int64)
-    q = np.asarray(tab, dtype=np.uint64)[i] >> np.uint64(24 - k)
+    with np.errstate(invalid="ignore", over="ignore"):
+        c = (np.float32(L) - np.float32(32.0) * m).astype(np.float32)
+        y = _fmaf(x, 32.0, c)
+        pos = y > 0                                                    # False for NaN
+        j = np.where(pos, np.minimum(np.where(pos, y, 0), np.float32(L)), 0).astype(np.int64)
+    q = np.asarray(tab, dtype=np.uint64)[L - j] >> np.uint64(24 - k)
     return np.maximum(q, 1).astype(np.uint32)

@@ -32,6 +32,11 @@ def _logits(seed, steps, B, V, scale=3.0, specials=False):
             x[0, 1, :] = -np.inf                                  # all -inf row: uniform table
         if steps > 1:
             x[1, 0, 5] = np.inf                                   # +inf max: every other entry 1
+        if steps > 2:
+            x[2, 0, 7] = 262143.5                                 # largest max of the GPU fast path
+            x[2, 0, 9] = 262143.5 - 3.0
+            x[2, B - 1, 3] = 3.0e5                                # just past it: capped (slow) path
+            x[2, B - 1, 4] = 3.0e5 - 0.25
     return x
 
 

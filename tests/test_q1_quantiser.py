@@ -69,3 +69,24 @@ def test_library_q1_k_matches_oracle():
         for V in (1, 2, 3, 24, 1000, 1024, 1025, 32000, 128256, 1 << 20):
             if (1 << (prec - 1)) >= V:
                 assert L.lac_q1_k(prec, V) == coracle.lib().lacref_q1_k(prec, V), (prec, V)
+
+
+def test_extreme_rows_exact_fma():
+    """Rows whose fma sum is not exact in float64 (tiny logits next to a large max,
+    maxima around the GPU fast-path bound 2^18): C fmaf == exact rounding."""
+    tab = _tab()
+    rng = np.random.default_rng(9)
+    for m in (3.0e5, 2.0 ** 18, 2.0 ** 18 - 0.5, -2.0 ** 18, 1.5e30, 17.0):
+        x = (np.float32(m) - np.abs(rng.standard_normal(64)).astype(np.float32) * np.float32(5)).astype(np.float32)
+        if m > 0:
+            x[:8] = np.float32(1e-30) * np.arange(1, 9, dtype=np.float32)
+        x[8] = m
+        x[9] = np.float32(m) - np.float32(17.0)
+        x[10] = np.float32(m) - np.float32(1 / 64)
+        x[11] = -np.float32(1e38)
+        got = coracle.q1_quantize(x, 48)
+        assert (got == restate.q1_quantize(x, 48, tab)).all(), m
+        if abs(m) < 2 ** 20:                  # beyond ~2^24, c = RNE(544 - 32m) drops the 544: all-ones table
+            assert got.max() == got[8] == 1 << 24
+        else:
+            assert (got >= 1).all()
