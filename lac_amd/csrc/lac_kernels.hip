@@ -1865,11 +1865,11 @@ static int q1_stats_launch(lac_ctx *c, const Q1Args &a, hipStream_t st) {
     return LAC_OK;
 }
 
-// Row-group shapes (waves per row RW, 16-B vectors per thread R, prefetch) of
-// k_q1_stats.  AUTO takes the first prefetch-free shape that holds the row in
-// registers, else tiles of (8, 8) (measured: the prefetching shapes spill at the
-// 128-VGPR cap of 4 waves/SIMD and run 1.7x slower); LAC_OPT_Q1_SHAPE forces
-// one (tuning; identical results).
+// Row-group shapes (waves per row RW, 16-B vectors per thread R, rolling
+// prefetch) of k_q1_stats.  AUTO takes the first listed shape that holds the row
+// in registers (measured on MI355X, c3 shape: bf16 (8,8,y) 0.76 ms vs (8,8,n)
+// 0.78-0.80 ms), else tiles of (8, 8); LAC_OPT_Q1_SHAPE forces one (tuning;
+// identical results).
 static const int kQ1Shapes[][3] = {{1, 4, 0}, {2, 8, 0}, {4, 8, 0}, {8, 8, 0}, {8, 16, 0}, {8, 8, 1}, {8, 4, 1}};
 
 template <typename LT, bool DEC>
@@ -1878,7 +1878,8 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
     int sh = c->q1_shape;
     auto holds = [&](int i) { return nvec <= 64 * kQ1Shapes[i - 1][0] * kQ1Shapes[i - 1][1]; };
     if (sh == 0) {
-        for (int i = 1; i <= (sizeof(LT) == 4 ? 5 : 4); i++)             // bf16 (8,16) spills
+        static const int order[] = {1, 2, 3, 6, 5};
+        for (int i : order)
             if (holds(i)) { sh = i; break; }
         if (sh == 0) sh = 8;
     }
