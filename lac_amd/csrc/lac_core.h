@@ -60,10 +60,27 @@ struct DecState {
 
 __host__ __device__ inline int bitlen64(uint64_t x) { return x ? 64 - __builtin_clzll(x) : 0; }
 
+__host__ __device__ inline uint64_t div_floor_inv(u128 N, uint64_t d, double inv);
+
+// 1/d for the quotient estimates of div_floor_inv.  On the device one v_rcp_f64
+// (no IEEE divide sequence on the coder's latency chain); its small relative
+// error only moves the first estimate, which the two exact remainder corrections
+// of div_floor_inv absorb, so results stay exact.
+__host__ __device__ inline double recip(uint64_t d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_rcp((double)d);
+#else
+    return 1.0 / (double)d;
+#endif
+}
+
 // floor(N / d) for d > 0 when the quotient is known to be < 2^63.  Two rounds of
 // float64 quotient estimates plus an exact 128-bit remainder correction: no
 // shift-subtract loop (the generic __int128 division is ~5k cycles on gfx950).
 __host__ __device__ inline uint64_t div_floor(u128 N, uint64_t d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return div_floor_inv(N, d, recip(d));
+#endif
     const double two64 = 18446744073709551616.0;
     const double dd = (double)d;
     const double dn = (double)(uint64_t)(N >> 64) * two64 + (double)(uint64_t)N;

@@ -315,6 +315,18 @@ __device__ i128 wave_xmax_prefix(const E *row, int64_t n, uint64_t w, uint64_t T
 // receive_symbol + decide_bit/emit_bit loop of A_to_bin (arith_code.py:169-192)
 // for one stream, executed uniformly by its wave.  Returns false (st.err set)
 // on a coder error.
+// Two quotients floor((n*m + add) / d) with one instruction stream: lane 0 divides
+// n0, the other lanes n1 (the pairs of the coder step -- a and b of
+// symbol_to_range, the decoder's target and its 1-padded twin -- are
+// independent, and the serial per-step chain is what bounds few-stream coding).
+__device__ inline void div_pair(uint64_t n0, uint64_t n1, uint64_t m, uint64_t add, uint64_t d, double inv,
+                                uint64_t *q0, uint64_t *q1) {
+    const uint64_t n = lane_id() == 0 ? n0 : n1;
+    const uint64_t q = div_floor_inv((u128)n * m + add, d, inv);
+    *q0 = readlane_u64(q, 0);
+    *q1 = readlane_u64(q, 1);
+}
+
 template <typename E>
 __device__ inline bool coder_step(EncState &st, int64_t &l, int64_t &h, uint64_t lo, uint64_t hi, uint64_t T,
                                   uint64_t minp, int64_t s, const E *row, int64_t V, int prec, uint64_t *pa,
@@ -324,11 +336,8 @@ __device__ inline bool coder_step(EncState &st, int64_t &l, int64_t &h, uint64_t
     if (T == 0) { st.err = LAC_E_TABLE; return false; }
     const uint64_t w = (uint64_t)(h - l + 1);
     uint64_t a, bb;
-    if (mapping == LAC_MAP_FLOOR) {
-        floor_range(lo, hi, T, w, &a, &bb);
-    } else if (!is_fudged(T, w, minp)) {
-        if (inv_T != 0.0) unfudged_range_inv(lo, hi, T, inv_T, w, &a, &bb);
-        else unfudged_range(lo, hi, T, w, &a, &bb);
+    if (mapping == LAC_MAP_FLOOR || !is_fudged(T, w, minp)) {  // floor: Predictor/ACSampler; else ceil
+        div_pair(lo, hi, w, mapping == LAC_MAP_FLOOR ? 0 : T - 1, T, inv_T != 0.0 ? inv_T : recip(T), &a, &bb);
     } else {                                                  // CDFPredictor.fudged_dist
         if (!allow_fudge) { st.err = LAC_E_TABLE; return false; }
         const i128 xprev = s > 0 ? wave_xmax_prefix<E>(row, s, w, T) : kI128Min;
@@ -735,7 +744,8 @@ __device__ inline int decode_symbol(DecState &st, const E *row, int64_t V, uint6
     const uint64_t vhi = v + ((1ull << u) - 1);
     bool det;
     if (mapping == LAC_MAP_FLOOR || !is_fudged(T, w, minp)) {
-        const uint64_t tgt = div_floor((u128)v * T, w);       // < T
+        uint64_t tgt, thi;                                    // targets of the 0- and 1-padded ends
+        div_pair(v, vhi < w ? vhi : 0, T, 0, w, recip(w), &tgt, &thi);   // tgt < T
         int64_t cv0;
         int G;
         uint64_t cb;
@@ -743,9 +753,8 @@ __device__ inline int decode_symbol(DecState &st, const E *row, int64_t V, uint6
         uint64_t cnt, lo_c, hi_c;
         scan_chunk<E, VEC>(row, V / VEC, cv0, G, cb, tgt, &cnt, &lo_c, &hi_c);
         s = cv0 * VEC + (int64_t)cnt;
-        if (mapping == LAC_MAP_FLOOR) floor_range(lo_c, hi_c, T, w, &a, &bb);
-        else unfudged_range(lo_c, hi_c, T, w, &a, &bb);
-        det = vhi < w && div_floor((u128)vhi * T, w) < hi_c;  // bisect_right(cdf, t_hi) == s
+        div_pair(lo_c, hi_c, w, mapping == LAC_MAP_FLOOR ? 0 : T - 1, T, recip(T), &a, &bb);
+        det = vhi < w && thi < hi_c;                          // bisect_right(cdf, t_hi) == s
     } else {
         const int e = decode_fudged<E>(row, V, w, v, T, &s, &a, &bb);
         if (e) return e;
@@ -1471,7 +1480,13 @@ __global__ LAC_DEC_BOUNDS void k_q1_decode(const LT *__restrict__ lg, int64_t st
         const uint64_t w = (uint64_t)(h - l + 1), v = (uint64_t)(x - l);
         if (!err && is_fudged(T, w, 1)) err = LAC_E_TABLE;             // impossible by the choice of k
         if (!err) {
-            const uint64_t tgt = div_floor((u128)v * T, w);
+            uint64_t tgt, thi;
+            {
+                const uint64_t past = st.pos > mynbits ? st.pos - mynbits : 0;
+                const int u = past < (uint64_t)prec ? (int)past : prec;
+                const uint64_t vh = v + ((1ull << u) - 1);
+                div_pair(v, vh < w ? vh : 0, T, 0, w, recip(w), &tgt, &thi);
+            }
             const uint64_t ex = incl - mine;
             const uint64_t mask = __ballot(ex <= tgt && tgt < incl);
             if (!mask) err = LAC_E_DECODE_RANGE;
@@ -1505,11 +1520,11 @@ __global__ LAC_DEC_BOUNDS void k_q1_decode(const LT *__restrict__ lg, int64_t st
                 hi_c = wave_min_u64(hi_c);
                 s = cv0 * N + (int64_t)cnt;
                 uint64_t a, bb;
-                unfudged_range(lo_c, hi_c, T, w, &a, &bb);
+                div_pair(lo_c, hi_c, w, T - 1, T, recip(T), &a, &bb);
                 const uint64_t past = st.pos > mynbits ? st.pos - mynbits : 0;
                 const int u = past < (uint64_t)prec ? (int)past : prec;
                 const uint64_t vhi = v + ((1ull << u) - 1);
-                const bool det = vhi < w && div_floor((u128)vhi * T, w) < hi_c;
+                const bool det = vhi < w && thi < hi_c;
                 if (st.det && det) st.ndet++;
                 else st.det = 0;
                 err = decode_advance(st, a, bb, mybits, mynbits, prec);
