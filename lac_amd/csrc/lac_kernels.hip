@@ -1259,6 +1259,60 @@ __device__ inline uint64_t wave_multi_sum(uint64_t (&v)[R]) {
     return r;
 }
 
+// Partner exchange across lane bit BIT inside a 16-lane row, on DPP:
+// bits 0/1 by quad_perm, bits 2/3 by row_shl/row_shr (each lane reads l ^ (1 << BIT)).
+template <int BIT>
+__device__ inline uint32_t xor_dpp(uint32_t x) {
+    if constexpr (BIT == 0) return dpp32<kDppXor1>(x);
+    else if constexpr (BIT == 1) return dpp32<kDppXor2>(x);
+    else {
+        const uint32_t up = dpp32<0x100 + (1 << BIT)>(x);    // row_shl: lane l reads l + 2^BIT
+        const uint32_t dn = dpp32<0x110 + (1 << BIT)>(x);    // row_shr: lane l reads l - 2^BIT
+        return ((lane_id() >> BIT) & 1) ? dn : up;
+    }
+}
+
+template <int R, int BIT>
+__device__ inline void multi_halve(uint32_t (&v)[R]) {
+    if constexpr ((R >> BIT) > 1) {
+        constexpr int live = R >> BIT;
+        const bool upper = (lane_id() >> BIT) & 1;
+#pragma unroll
+        for (int i = 0; i < live / 2; i++) {
+            const uint32_t keep = upper ? v[i + live / 2] : v[i];
+            const uint32_t give = upper ? v[i] : v[i + live / 2];
+            v[i] = keep + xor_dpp<BIT>(give);
+        }
+        multi_halve<R, BIT + 1>(v);
+    }
+}
+
+// Sums of R per-lane u32 values (each < 2^27) across the wave, all R at once:
+// halving steps over lane bits 0..log2(R)-1 and the rest of the 16-lane row in
+// 32 bits on DPP (a row sums 16 values < 2^31), then the two cross-row steps in
+// 64 bits.  Lane l ends with the total of index q_index<R>(l) (l < R distinct).
+template <int R>
+__device__ inline uint64_t wave_multi_sum32(uint32_t (&v)[R]) {
+    static_assert(R >= 1 && R <= 16 && (R & (R - 1)) == 0, "R: power of two <= 16");
+    multi_halve<R, 0>(v);
+    uint32_t r = v[0];
+    if constexpr (R < 2) r += xor_dpp<0>(r);
+    if constexpr (R < 4) r += xor_dpp<1>(r);
+    if constexpr (R < 8) r += xor_dpp<2>(r);
+    if constexpr (R < 16) r += xor_dpp<3>(r);
+    uint64_t r64 = r;
+    r64 += shfl_xor_u64(r64, 16);
+    r64 += shfl_xor_u64(r64, 32);
+    return r64;
+}
+template <int R>
+__device__ inline int q_index(int lane) {                   // lane bit b -> index bit log2(R)-1-b
+    int idx = 0;
+#pragma unroll
+    for (int b = 0; (1 << b) < R; b++) idx |= ((lane >> b) & 1) << (__builtin_ctz(R) - 1 - b);
+    return idx;
+}
+
 __device__ inline u32x4 neg_inf16(int type_bytes) {
     const uint32_t w = type_bytes == 2 ? 0xFF80FF80u : 0xFF800000u;
     return u32x4{w, w, w, w};
@@ -1363,7 +1417,7 @@ __global__ __launch_bounds__(64 * kQ1Waves, 4) void k_q1_stats(const LT *__restr
         }
         for (int tile = ntiles - 1; tile >= 0; tile--) {
             if (MULTI && tile != ntiles - 1) q1_load_tile<LT, R>(x, row, valid, tile * NT * R, gt, NT, nvec);
-            uint64_t sv[R];
+            uint32_t sv[R];
             auto take = [&](int j, uint32_t sl) {
                 const int vi = tile * NT * R + gt + NT * j;
                 sl = vi < nvec ? sl : 0;
@@ -1405,9 +1459,9 @@ __global__ __launch_bounds__(64 * kQ1Waves, 4) void k_q1_stats(const LT *__restr
                 for (int j = 0; j < R; j++) { take(j, q1_vec_sum<LT>(x[j], c, false, tabr, loff)); roll(j); }
             }
             if (DEC) {
-                const uint64_t gsum = wave_multi_sum<R>(sv);  // group total of index lane / (64/R)
-                if ((lane & (64 / R - 1)) == 0) {
-                    const int grp = tile * RW * R + wg + RW * (lane / (64 / R));
+                const uint64_t gsum = wave_multi_sum32<R>(sv);    // group total of index q_index(lane)
+                if (lane < R) {
+                    const int grp = tile * RW * R + wg + RW * q_index<R>(lane);
                     if (grp * 64 < nvec) atomicAdd(&bins[g][grp / (int)G], (unsigned long long)gsum);
                 }
             }
@@ -1882,8 +1936,9 @@ static int q1_stats_launch(lac_ctx *c, const Q1Args &a, hipStream_t st) {
 
 // Row-group shapes (waves per row RW, 16-B vectors per thread R, rolling
 // prefetch) of k_q1_stats.  AUTO takes the first listed shape that holds the row
-// in registers (measured on MI355X, c3 shape: bf16 (8,8,y) 0.76 ms vs (8,8,n)
-// 0.78-0.80 ms), else tiles of (8, 8); LAC_OPT_Q1_SHAPE forces one (tuning;
+// in registers (measured on MI355X, c3 shape: encode bf16 (8,8,y) 0.75 ms vs
+// (8,8,n) 0.79 ms; decode (8,8,n) 70 M sym/s vs 46 M for the spilling (8,8,y)),
+// else tiles of (8, 8); LAC_OPT_Q1_SHAPE forces one for both directions (tuning;
 // identical results).
 static const int kQ1Shapes[][3] = {{1, 4, 0}, {2, 8, 0}, {4, 8, 0}, {8, 8, 0}, {8, 16, 0}, {8, 8, 1}, {8, 4, 1}};
 
@@ -1892,9 +1947,9 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
     const int64_t nvec = c->V / LogitN<LT>::N;
     int sh = c->q1_shape;
     auto holds = [&](int i) { return nvec <= 64 * kQ1Shapes[i - 1][0] * kQ1Shapes[i - 1][1]; };
-    if (sh == 0) {
-        static const int order[] = {1, 2, 3, 6, 5};
-        for (int i : order)
+    if (sh == 0) {                     // decode: the prefetching (8,8) spills around the multi-sum
+        static const int enc_order[] = {1, 2, 3, 6, 5}, dec_order[] = {1, 2, 3, 4, 5};
+        for (int i : DEC ? dec_order : enc_order)
             if (holds(i)) { sh = i; break; }
         if (sh == 0) sh = 8;
     }

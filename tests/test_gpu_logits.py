@@ -179,3 +179,19 @@ def test_logits_errors():
     with pytest.raises(LacError) as e:
         _coder(1 << 20, 1, 21).quantize_logits(torch.zeros((1, 1, 1 << 20), device=DEV))
     assert e.value.code == LAC_E_PREC
+
+
+def test_logits_decode_spans_step_chunks():
+    """600 streams x 70 steps of logits: both q1 kernels run in 64-step chunks."""
+    V, B, steps, prec = 1024, 600, 70, 40
+    g = torch.Generator(device=DEV).manual_seed(4)
+    dl = (torch.randn((steps, B, V), device=DEV, generator=g) * 4).to(torch.bfloat16)
+    c = _coder(V, B, prec, cap=steps * (prec + 2) + 256)
+    sym = torch.randint(0, V, (steps, B), device=DEV, generator=g, dtype=torch.int32)
+    c.encode_logits_job(dl, sym)
+    a, na = c.to_bytes()
+    c2 = _coder(V, B, prec, cap=steps * (prec + 2) + 256)
+    c2.encode_job(c.quantize_logits(dl), sym)
+    assert c2.to_bytes()[0] == a
+    c.decode_open()
+    assert torch.equal(c.decode_logits(dl), sym)

@@ -392,3 +392,19 @@ def test_edge_u64_total_overflow_is_an_error():
     c.encode(_dev_pmf(pmf), torch.from_numpy(sym).to(DEV))
     rc, err, step = c.status()
     assert err.tolist() == [-5, 0]
+
+
+def test_stats_decode_spans_step_chunks():
+    """600 streams x 150 steps: the stats-path decode (AUTO below 2048 streams)
+    runs in 64-step chunks; symbols and determined counts match the other paths."""
+    V, B, steps, prec = 512, 600, 150, 40
+    pmf, sym = synth.make_batch(21, steps, B, V, "loguniform")
+    c, dpmf, data, n, tr = _gpu_encode(pmf, sym, prec)
+    dets = []
+    for path in DECODE_PATHS:
+        c.set_decode_path(path)
+        c.decode_open()
+        assert (c.decode(dpmf).cpu().numpy() == sym).all(), path
+        dets.append(c.determined())
+    assert all((d == dets[0]).all() for d in dets[1:])
+    c.raise_on_error()
