@@ -73,8 +73,9 @@ enum {                       /* lac_set_option */
                                       else STATS */
     LAC_OPT_Q1_SHAPE = 6           /* logits path row-stats shape: 0 = auto (default), 1..7 = (waves per
                                       row, vectors/thread, rolling prefetch) (1,4,n) (2,8,n) (4,8,n)
-                                      (8,8,n) (8,16,n) (8,8,y) (8,4,y), 8 = tiles of (8,8,n);
-                                      identical results, only speed differs */
+                                      (8,8,n) (8,16,n) (8,8,y) (8,4,y), 8 = tiles of (8,8,n),
+                                      9 = 16-wave (16,16,n), 10 = tiles of 9; identical results,
+                                      only speed differs */
 };
 enum {
     LAC_MAP_CEIL = 0,              /* CDFPredictor.symbol_to_range + fudged_dist (arith_code.py:83-110) */

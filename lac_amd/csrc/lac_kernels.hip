@@ -1342,18 +1342,18 @@ __device__ inline void q1_load_tile(u32x4 (&x)[R], const LT *row, bool valid, in
     }
 }
 
-template <typename LT, int RW, int R, bool DEC, bool MULTI, bool PF>
-__global__ __launch_bounds__(64 * kQ1Waves, 4) void k_q1_stats(const LT *__restrict__ lg, int64_t step_stride,
+template <typename LT, int RW, int R, bool DEC, bool MULTI, bool PF, int NWB>
+__global__ __launch_bounds__(64 * NWB, 4) void k_q1_stats(const LT *__restrict__ lg, int64_t step_stride,
                                                               int64_t stream_stride, const int32_t *__restrict__ sym,
                                                               int64_t B, int64_t rows, int64_t V, int64_t t0,
                                                               uint32_t xsh, int64_t G, RowStats *__restrict__ out,
                                                               uint64_t *__restrict__ chunks,
                                                               float *__restrict__ mrow) {
-    constexpr int N = LogitN<LT>::N, NT = 64 * RW, NR = kQ1Waves / RW;
+    constexpr int N = LogitN<LT>::N, NT = 64 * RW, NR = NWB / RW;
     static_assert(R * N <= 128, "lane sums must fit 32 bits");
     __shared__ uint32_t tabr[LAC_Q1_TAB_SIZE * kQ1Rep];
-    __shared__ float smax[kQ1Waves];
-    __shared__ uint64_t ssum[kQ1Waves][2];
+    __shared__ float smax[NWB];
+    __shared__ uint64_t ssum[NWB][2];
     __shared__ uint32_t sps[NR];
     __shared__ unsigned long long bins[DEC ? NR : 1][64];
     // in-row indices are 32-bit (vocab <= 2^31 entries); with one row per block
@@ -1911,23 +1911,23 @@ struct Q1Args {
     uint32_t xsh;
 };
 
-template <typename LT, int RW, int R, bool DEC, bool MULTI, bool PF>
+template <typename LT, int RW, int R, bool DEC, bool MULTI, bool PF, int NWB = kQ1Waves>
 static int q1_stats_launch(lac_ctx *c, const Q1Args &a, hipStream_t st) {
     static int per_cu = 0;                                       // resident blocks per CU (occupancy API)
     if (!per_cu) {
         int n = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_q1_stats<LT, RW, R, DEC, MULTI, PF>, 64 * kQ1Waves,
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_q1_stats<LT, RW, R, DEC, MULTI, PF, NWB>, 64 * NWB,
                                                          0) != hipSuccess ||
             n < 1)
             n = 1;
         per_cu = n;
     }
-    constexpr int NR = kQ1Waves / RW;
+    constexpr int NR = NWB / RW;
     const int64_t need = (a.rows + NR - 1) / NR, cap = (int64_t)c->cus * per_cu;
     const unsigned grid = (unsigned)(need < cap ? need : cap);
     const int64_t nvec = c->V / LogitN<LT>::N;
     ProfScope ps(c, KID_Q1_STATS, st);
-    k_q1_stats<LT, RW, R, DEC, MULTI, PF><<<grid, 64 * kQ1Waves, 0, st>>>(
+    k_q1_stats<LT, RW, R, DEC, MULTI, PF, NWB><<<grid, 64 * NWB, 0, st>>>(
         (const LT *)a.lg, a.ss, a.bs, a.sym, c->B, a.rows, c->V, a.t0, a.xsh, q1_groups_per_chunk(nvec), c->stats,
         c->q1chunks, c->q1m);
     CHECK_LAUNCH();
@@ -1951,8 +1951,12 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
         static const int enc_order[] = {1, 2, 3, 6, 5}, dec_order[] = {1, 2, 3, 4, 5};
         for (int i : DEC ? dec_order : enc_order)
             if (holds(i)) { sh = i; break; }
-        if (sh == 0) sh = 8;
+        if (sh == 0) sh = nvec <= 64 * 16 * 16 ? 9 : (DEC ? 10 : 8);   // measured at V = 128256 f32
     }
+    // one 16-wave block per CU (LDS: one table copy), 16 vectors per thread: a bf16 row
+    // of up to 131072 entries in registers (c4's V = 128256) -- one pass, no re-read
+    if (sh == 9 && nvec <= 64 * 16 * 16) return q1_stats_launch<LT, 16, 16, DEC, false, false, 16>(c, a, st);
+    if (sh == 10) return q1_stats_launch<LT, 16, 16, DEC, true, false, 16>(c, a, st);   // tiles of 16384
     if (sh == 8) return q1_stats_launch<LT, 8, 8, DEC, true, false>(c, a, st);      // tiles of 4096 vectors
     if (!holds(sh)) return fail(LAC_E_ARG, "q1 shape %d does not hold a row of %lld vectors", sh, (long long)nvec);
     switch (sh) {
@@ -2119,7 +2123,7 @@ int lac_set_option(lac_ctx *c, int option, int64_t value) {
         c->dpath = (int)value;
         return LAC_OK;
     case LAC_OPT_Q1_SHAPE:
-        if (value < 0 || value > 8) return fail(LAC_E_ARG, "bad q1 shape");
+        if (value < 0 || value > 10) return fail(LAC_E_ARG, "bad q1 shape");
         c->q1_shape = (int)value;
         return LAC_OK;
     case LAC_OPT_MAPPING:
