@@ -69,7 +69,9 @@ CASES = [
     (32000, 64, 8, 48, "f32"),
     (1000, 40, 30, 40, "f32"),
     (1000, 40, 30, 40, "bf16"),
-    (128256, 8, 4, 48, "bf16"),
+    (128256, 8, 4, 48, "bf16"),            # 16-wave single-pass row stats
+    (128256, 4, 3, 48, "f32"),             # tiled row stats (encode 8-wave, decode 16-wave tiles)
+    (65536, 6, 3, 48, "bf16"),             # (8,16) shape
     (24, 5, 50, 24, "f32"),
     (4096, 2048, 3, 48, "bf16"),
 ]
