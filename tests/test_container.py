@@ -21,3 +21,10 @@ def test_rejects_bad_input():
         container.unpack(b"XXXX" + blob[4:])
     with pytest.raises(ValueError):
         container.unpack(blob + b"\x00")
+
+
+def test_q1_flag():
+    blob = container.pack([b"\x80"], [1], [1], 40, 1024, q1_logits=True)
+    h = container.unpack(blob)
+    assert h["q1_logits"] and h["pmf_bits"] == 32 and h["mapping"] == "ceil"
+    assert not container.unpack(container.pack([b"\x80"], [1], [1], 40, 1024))["q1_logits"]

@@ -170,6 +170,20 @@ def test_container_compress_decompress_batch():
     assert n == [6] * 300 and torch.equal(out, sym)
 
 
+def test_container_logits_roundtrip():
+    """A q1 container: bf16 logits in, flag set, decode with the same logits."""
+    from lac_amd import container, synth
+    from lac_amd.batch import BatchCoder
+    coder = BatchCoder(2048, 300, prec=48, capacity_bits=6 * 50 + 256, device="cuda:0")
+    logits, sym = synth.logits_batch(6, 300, 2048, seed=8, device="cuda:0", quantise=coder.quantize_logits)
+    blob = container.compress_batch(coder, logits, sym)
+    assert container.unpack(blob)["q1_logits"]
+    out, n = container.decompress_batch(blob, logits)
+    assert n == [6] * 300 and torch.equal(out, sym)
+    with pytest.raises(ValueError):
+        container.decompress_batch(blob, coder.quantize_logits(logits))
+
+
 def test_llama_ac_adapter_with_torch_model_roundtrip():
     """Llama_AC (llama_compress.py:14-61) driven by a ROCm torch model: encode, decode,
     and bit-exact against the oracle on the tables the model produced."""
