@@ -206,6 +206,14 @@ int lac_encode_logits_job(lac_ctx *ctx, const void *logits_dev, int logit_type, 
                           int64_t stream_stride, const int32_t *sym_dev, int64_t steps, uint64_t *trace_dev,
                           void *stream);
 
+/* Incremental form: encode `steps` more symbols per stream from logits,
+ * continuing each stream where the last call (lac_encode_reset, lac_encode or
+ * lac_encode_logits) left it; close with lac_encode_finish.  Streams may mix
+ * pmf and logits steps (each step's table is exact either way). */
+int lac_encode_logits(lac_ctx *ctx, const void *logits_dev, int logit_type, int64_t step_stride,
+                      int64_t stream_stride, const int32_t *sym_dev, int64_t steps, uint64_t *trace_dev,
+                      void *stream);
+
 /* Decode `steps` symbols per stream (after lac_decode_open) with the tables
  * computed from logits; sym_out_dev[t*streams + b] (-1 after an error). */
 int lac_decode_logits_steps(lac_ctx *ctx, const void *logits_dev, int logit_type, int64_t step_stride,

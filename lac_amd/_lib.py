@@ -59,6 +59,7 @@ PROTOTYPES = [
     ("lac_profile_read", _i, [_vp, _vp, _vp, _i]),
     ("lac_q1_k", _i, [_i, _i64]),
     ("lac_encode_logits_job", _i, [_vp, _vp, _i, _i64, _i64, _vp, _i64, _vp, _vp]),
+    ("lac_encode_logits", _i, [_vp, _vp, _i, _i64, _i64, _vp, _i64, _vp, _vp]),
     ("lac_decode_logits_steps", _i, [_vp, _vp, _i, _i64, _i64, _i64, _vp, _vp]),
     ("lac_quantize_logits", _i, [_vp, _vp, _i, _i64, _i64, _i64, _vp, _vp]),
 ]

@@ -299,10 +299,7 @@ class BatchCoder:
         stream_stride = logits.stride(1) if logits.shape[1] > 1 else 0
         return typ, step_stride, stream_stride, n, logits
 
-    def encode_logits_job(self, logits, sym, trace=None):
-        """reset + encode + finish with tables computed in-kernel from logits by
-        the q1 quantiser (include/lac.h "logits path"): one launch, the pmf never
-        touches HBM.  ``logits`` [steps, streams, V] bf16/f32, ``sym`` [steps, streams]."""
+    def _logits_encode_args(self, logits, sym, trace):
         torch = _torch()
         if sym.dtype != torch.int32 or sym.device != self.device:
             raise TypeError("sym must be an int32 tensor on the coder's device")
@@ -317,8 +314,20 @@ class BatchCoder:
                 raise ValueError("trace must be a contiguous int64 tensor [steps, streams, 2]")
             tp = C.c_void_p(trace.data_ptr())
         self._keep = (logits, sym)
-        check(self.lib.lac_encode_logits_job(self.ctx, C.c_void_p(logits.data_ptr()), typ, ss, bs,
-                                             C.c_void_p(sym.data_ptr()), steps, tp, self._stream))
+        return (self.ctx, C.c_void_p(logits.data_ptr()), typ, ss, bs, C.c_void_p(sym.data_ptr()), steps, tp,
+                self._stream)
+
+    def encode_logits(self, logits, sym, trace=None):
+        """Incremental logits encode: continue every stream by ``steps`` symbols
+        (no reset, no finish -- call :meth:`finish` at the end).  Steps may be
+        interleaved with :meth:`encode` on integer pmfs."""
+        check(self.lib.lac_encode_logits(*self._logits_encode_args(logits, sym, trace)))
+
+    def encode_logits_job(self, logits, sym, trace=None):
+        """reset + encode + finish with tables computed in-kernel from logits by
+        the q1 quantiser (include/lac.h "logits path"): the pmf never touches
+        HBM.  ``logits`` [steps, streams, V] bf16/f32, ``sym`` [steps, streams]."""
+        check(self.lib.lac_encode_logits_job(*self._logits_encode_args(logits, sym, trace)))
 
     def decode_logits(self, logits, out=None):
         """Decode one symbol per stream per step with q1 tables from ``logits``."""

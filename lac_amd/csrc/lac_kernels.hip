@@ -1971,10 +1971,12 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
 }
 
 template <typename LT>
-static int q1_encode_job(lac_ctx *c, const Q1Args &a0, int64_t steps, uint64_t *trace, hipStream_t st) {
+static int q1_encode(lac_ctx *c, const Q1Args &a0, int64_t steps, uint64_t *trace, hipStream_t st, int flags) {
     const unsigned blocks = (unsigned)((c->B + kWavesPerBlock - 1) / kWavesPerBlock);
-    k_enc_reset<<<(unsigned)((c->B + 255) / 256), 256, 0, st>>>(c->enc, c->B, c->prec);
-    CHECK_LAUNCH();
+    if (flags & kReset) {
+        k_enc_reset<<<(unsigned)((c->B + 255) / 256), 256, 0, st>>>(c->enc, c->B, c->prec);
+        CHECK_LAUNCH();
+    }
     for (int64_t t0 = 0; t0 < steps; t0 += c->chunk_steps) {
         const int64_t n = (steps - t0) < c->chunk_steps ? (steps - t0) : c->chunk_steps;
         Q1Args a = a0;
@@ -1990,10 +1992,12 @@ static int q1_encode_job(lac_ctx *c, const Q1Args &a0, int64_t steps, uint64_t *
         }
         CHECK_LAUNCH();
     }
-    ProfScope ps(c, KID_FINISH, st);
-    k_finish<<<(unsigned)((c->B + 255) / 256), 256, 0, st>>>(c->enc, c->planeA, c->planeC, c->cap_words, c->B, c->prec,
-                                                             c->nbits, LAC_TERM_FLUSH);
-    CHECK_LAUNCH();
+    if (flags & kFinish) {
+        ProfScope ps(c, KID_FINISH, st);
+        k_finish<<<(unsigned)((c->B + 255) / 256), 256, 0, st>>>(c->enc, c->planeA, c->planeC, c->cap_words, c->B,
+                                                                 c->prec, c->nbits, LAC_TERM_FLUSH);
+        CHECK_LAUNCH();
+    }
     return LAC_OK;
 }
 
@@ -2281,18 +2285,32 @@ int lac_decode_steps(lac_ctx *c, const void *pmf_dev, int64_t step_stride, int64
     return decode_dispatch(c, pmf_dev, step_stride, stream_stride, steps, sym_out_dev, S(stream));
 }
 
-int lac_encode_logits_job(lac_ctx *c, const void *logits_dev, int logit_type, int64_t step_stride,
-                          int64_t stream_stride, const int32_t *sym_dev, int64_t steps, uint64_t *trace_dev,
-                          void *stream) {
+static int logits_encode(lac_ctx *c, const void *logits_dev, int logit_type, int64_t step_stride,
+                         int64_t stream_stride, const int32_t *sym_dev, int64_t steps, uint64_t *trace_dev,
+                         void *stream, int flags) {
     if (!c || (steps > 0 && (!logits_dev || !sym_dev))) return fail(LAC_E_ARG, "NULL argument");
     int rc = logits_check(c, logits_dev, logit_type, step_stride, stream_stride, steps);
     uint32_t xsh = 0;
     if (rc || (rc = q1_shift(c, &xsh))) return rc;
+    if (steps == 0 && !flags) return LAC_OK;
     HIPCHK(hipSetDevice(c->device));
     c->mode = 0;
     const Q1Args a{logits_dev, step_stride, stream_stride, sym_dev, 0, 0, xsh};
-    return logit_type == LAC_LOGITS_BF16 ? q1_encode_job<uint16_t>(c, a, steps, trace_dev, S(stream))
-                                         : q1_encode_job<float>(c, a, steps, trace_dev, S(stream));
+    return logit_type == LAC_LOGITS_BF16 ? q1_encode<uint16_t>(c, a, steps, trace_dev, S(stream), flags)
+                                         : q1_encode<float>(c, a, steps, trace_dev, S(stream), flags);
+}
+
+int lac_encode_logits_job(lac_ctx *c, const void *logits_dev, int logit_type, int64_t step_stride,
+                          int64_t stream_stride, const int32_t *sym_dev, int64_t steps, uint64_t *trace_dev,
+                          void *stream) {
+    return logits_encode(c, logits_dev, logit_type, step_stride, stream_stride, sym_dev, steps, trace_dev, stream,
+                         kReset | kFinish);
+}
+
+int lac_encode_logits(lac_ctx *c, const void *logits_dev, int logit_type, int64_t step_stride,
+                      int64_t stream_stride, const int32_t *sym_dev, int64_t steps, uint64_t *trace_dev,
+                      void *stream) {
+    return logits_encode(c, logits_dev, logit_type, step_stride, stream_stride, sym_dev, steps, trace_dev, stream, 0);
 }
 
 int lac_decode_logits_steps(lac_ctx *c, const void *logits_dev, int logit_type, int64_t step_stride,

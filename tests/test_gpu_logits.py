@@ -197,3 +197,26 @@ def test_logits_decode_spans_step_chunks():
     assert c2.to_bytes()[0] == a
     c.decode_open()
     assert torch.equal(c.decode_logits(dl), sym)
+
+
+def test_incremental_logits_encode_mixes_with_pmf_steps():
+    """encode_logits (no reset/finish) in pieces, interleaved with pmf steps of the
+    same q1 tables, equals one encode_logits_job."""
+    V, B, steps, prec = 1024, 48, 40, 40
+    g = torch.Generator(device=DEV).manual_seed(6)
+    dl = (torch.randn((steps, B, V), device=DEV, generator=g) * 3).to(torch.bfloat16)
+    sym = torch.randint(0, V, (steps, B), device=DEV, generator=g, dtype=torch.int32)
+    c = _coder(V, B, prec, cap=steps * (prec + 2) + 256)
+    c.encode_logits_job(dl, sym)
+    one, n1 = c.to_bytes()
+    pmf = c.quantize_logits(dl)
+    c2 = _coder(V, B, prec, cap=steps * (prec + 2) + 256)
+    c2.reset()
+    for a, b, kind in ((0, 7, "logits"), (7, 8, "pmf"), (8, 30, "logits"), (30, 40, "pmf")):
+        if kind == "logits":
+            c2.encode_logits(dl[a:b], sym[a:b].contiguous())
+        else:
+            c2.encode(pmf[a:b], sym[a:b].contiguous())
+    c2.finish()
+    two, n2 = c2.to_bytes()
+    assert (n1 == n2).all() and one == two
