@@ -24,7 +24,7 @@ ok_or_stop() {                # 0 ok; 1 = test failures (continue); anything els
 for s in $STEPS; do
   case $s in
     smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"; rc=$?; [ $rc -ne 0 ] && exit $rc ;;
-    tests) run tests 1200 python3 -m pytest tests -m gpu -q -rf; ok_or_stop $? ;;
+    tests) run tests 900 python3 -u -m pytest tests -m gpu -q -rf --timeout 180 --timeout-method thread; ok_or_stop $? ;;
     bench) run bench 600 python3 bench.py $BENCH_ARGS; ok_or_stop $? ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
                python3 bench.py --steps 10 --warmup 2 --cpu-baseline off $BENCH_ARGS; ok_or_stop $? ;;
