@@ -94,7 +94,7 @@ def main():
 
     from lac_amd import synth
     from lac_amd.batch import BatchCoder
-    from lac_amd.dist import gather_bitstreams
+    from lac_amd.dist import BitstreamGatherer
 
     V, B, T, P = args.vocab, args.streams, args.tokens, args.prec
     logits_in = args.input != "pmf"
@@ -120,14 +120,17 @@ def main():
     if args.decode_path != "auto":
         coder.set_decode_path(args.decode_path)
 
+    # N > 1: each job's bitstreams are all-gathered over RCCL into fixed-width slots,
+    # asynchronously (overlapping the next job's encode), double-buffered
+    gatherer = BitstreamGatherer(coder) if world > 1 else None
+
     def job():
         if logits_in:
             coder.encode_logits_job(pmf, sym)
         else:
             coder.encode_job(pmf, sym)
-        if world > 1:
-            return gather_bitstreams(coder.bits_tensor(), coder.nbits_tensor())
-        return None
+        if gatherer:
+            gatherer.submit()
 
     for _ in range(args.warmup):
         job()
@@ -140,6 +143,8 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         job()
+    if gatherer:
+        gatherer.drain()                                   # every gather is inside the timed region
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if dist:
@@ -155,6 +160,16 @@ def main():
     coder.lib.lac_profile_read(coder.ctx, C.cast(ms, C.c_void_p), C.cast(cnt, C.c_void_p), 1)
 
     # ---------------- checks, outside the timed region
+    gather_ok = None
+    if gatherer:                                           # this rank's slice of the last gather == its bits
+        gb, gn = gatherer.last
+        lo = rank * B
+        mine_b = coder.copy_bits_into(torch.empty_like(gb[lo:lo + B]))
+        mine_n = coder.copy_nbits_into(torch.empty_like(gn[lo:lo + B]))
+        okg = bool(torch.equal(gb[lo:lo + B], mine_b)) and bool(torch.equal(gn[lo:lo + B], mine_n))
+        flag = torch.tensor([1 if okg else 0], device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        gather_ok = bool(flag.item())
     rc, err, err_step = coder.status()
     data, nbits = coder.to_bytes() if rc == 0 else ([], None)
     decode = coder.decode_logits if logits_in else coder.decode
@@ -186,6 +201,8 @@ def main():
 
     cpu = None
     parity = {"round_trip_all_streams": round_trip, "stream_status_ok": rc == 0, "decode": decode_info}
+    if gatherer:
+        parity["gather_ok"] = gather_ok
     if rank == 0:
         from oracle import oracle as coracle
         S = B if (args.cpu_streams <= 0 or args.cpu_streams > B) else args.cpu_streams

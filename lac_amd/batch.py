@@ -213,6 +213,25 @@ class BatchCoder:
         check(self.lib.lac_copy_bits_dev(self.ctx, C.c_void_p(out.data_ptr()), stride, self._stream))
         return out
 
+    def bits_stride(self):
+        """Bytes per stream of the packed output buffer (capacity rounded to 8-byte words)."""
+        return int(self.device_bits()[1])
+
+    def copy_bits_into(self, out):
+        """Copy the packed output into a uint8 device tensor [streams, W] with
+        contiguous rows (W <= bits_stride() keeps the first W bytes), asynchronously."""
+        if out.dim() != 2 or out.shape[0] != self.streams or out.stride(1) != 1 or out.dtype != _torch().uint8:
+            raise ValueError("out must be a uint8 [streams, W] tensor with contiguous rows")
+        check(self.lib.lac_copy_bits_dev(self.ctx, C.c_void_p(out.data_ptr()), out.stride(0), self._stream))
+        return out
+
+    def copy_nbits_into(self, out):
+        """Copy the per-stream bit counts into a contiguous 8-byte integer device tensor [streams]."""
+        if out.shape != (self.streams,) or not out.is_contiguous() or out.element_size() != 8:
+            raise ValueError("out must be a contiguous 8-byte integer tensor [streams]")
+        check(self.lib.lac_copy_nbits_dev(self.ctx, C.c_void_p(out.data_ptr()), self._stream))
+        return out
+
     def nbits_tensor(self):
         """Per-stream bit counts as a fresh int64 device tensor (asynchronous copy)."""
         torch = _torch()

@@ -61,3 +61,71 @@ def _all_gather(out, inp, group, world):
         dist.all_gather_into_tensor(out, inp, group=group)
     except (RuntimeError, NotImplementedError):       # backends without the fused form
         dist.all_gather(list(out.chunk(world)), inp, group=group)
+
+
+class BitstreamGatherer:
+    """Fixed-width, asynchronous, double-buffered bitstream all-gather for
+    back-to-back compression jobs.
+
+    ``gather_bitstreams`` agrees on the widest stream first (an all-reduce and a
+    host read), which serialises every job behind two collective latencies.  A
+    job's slot width is known up front: no stream can exceed the coder's
+    capacity (``cap_words`` 8-byte words).  So each ``submit()`` copies the
+    packed bits and bit counts into one of ``depth`` slot buffers on the
+    caller's stream and enqueues the all-gathers with ``async_op=True``: RCCL
+    runs them on its own stream while the next job's encode kernel streams its
+    tables, and the caller's stream only waits for a collective when its slot is
+    about to be reused ``depth`` jobs later.  ``drain()`` makes the caller's
+    stream wait for everything still in flight.
+
+    Under ``gloo`` (CPU tests, one-GPU rehearsals) the gather goes through host
+    tensors synchronously, like ``gather_bitstreams``.
+    """
+
+    def __init__(self, coder, group=None, depth: int = 2):
+        import torch
+        import torch.distributed as dist
+        self.coder, self.group, self.depth = coder, group, max(1, int(depth))
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.gloo = dist.get_backend(group) == "gloo"
+        self.width = coder.bits_stride()                      # cap_words * 8 bytes per stream
+        B, dev = coder.streams, coder.device
+        self.slots = [(torch.empty((B, self.width), dtype=torch.uint8, device=dev),
+                       torch.empty((B,), dtype=torch.int64, device=dev)) for _ in range(self.depth)]
+        self.outs = [(torch.empty((self.world * B, self.width), dtype=torch.uint8, device=dev),
+                      torch.empty((self.world * B,), dtype=torch.int64, device=dev)) for _ in range(self.depth)]
+        self.pending = [None] * self.depth
+        self.k = 0
+        self.last = None
+
+    def submit(self):
+        """Gather the coder's current output; returns the (bits, nbits) output
+        buffers, valid on the caller's stream after ``drain()``."""
+        import torch.distributed as dist
+        i = self.k % self.depth
+        self.k += 1
+        self._wait(i)                                           # slot i's previous gather is done
+        bits, nbits = self.slots[i]
+        self.coder.copy_bits_into(bits)                          # on the caller's stream
+        self.coder.copy_nbits_into(nbits)
+        ob, on = self.outs[i]
+        if self.gloo:
+            _all_gather(ob, bits, self.group, self.world)
+            _all_gather(on, nbits, self.group, self.world)
+        else:
+            self.pending[i] = [dist.all_gather_into_tensor(ob, bits, group=self.group, async_op=True),
+                               dist.all_gather_into_tensor(on, nbits, group=self.group, async_op=True)]
+        self.last = (ob, on)
+        return self.last
+
+    def _wait(self, i):
+        if self.pending[i]:
+            for w in self.pending[i]:
+                w.wait()                                        # caller's stream waits; the host does not
+            self.pending[i] = None
+
+    def drain(self):
+        for i in range(self.depth):
+            self._wait(i)
+        return self.last

@@ -7,7 +7,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from lac_amd.dist import gather_bitstreams, shard_range
+from lac_amd.dist import BitstreamGatherer, gather_bitstreams, shard_range
 
 
 def _free_port():
@@ -61,3 +61,60 @@ def test_gather_bitstreams_gloo_world2():
     for i, (row, n) in enumerate(zip(b0 + b1, n0 + n1)):
         nb = (n + 7) // 8
         assert A0[i][:nb] == row[:nb]
+
+
+class _FakeCoder:
+    """CPU stand-in for BatchCoder's output accessors (the gatherer's only dependency)."""
+
+    def __init__(self, streams, stride, seed):
+        self.streams, self.stride, self.device = streams, stride, "cpu"
+        self.g = torch.Generator().manual_seed(seed)
+        self.new_job()
+
+    def new_job(self):
+        self.nbits = torch.randint(0, self.stride * 8 + 1, (self.streams,), generator=self.g, dtype=torch.int64)
+        self.bits = torch.randint(0, 256, (self.streams, self.stride), generator=self.g, dtype=torch.uint8)
+
+    def bits_stride(self):
+        return self.stride
+
+    def copy_bits_into(self, out):
+        out.copy_(self.bits[:, :out.shape[1]])
+
+    def copy_nbits_into(self, out):
+        out.copy_(self.nbits)
+
+
+def _gatherer_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    coder = _FakeCoder(3, 24, seed=100 + rank)
+    g = BitstreamGatherer(coder, depth=2)
+    jobs = []
+    for _ in range(5):                                  # more jobs than slots: slots are reused
+        coder.new_job()
+        ob, on = g.submit()
+        jobs.append((coder.bits.clone(), coder.nbits.clone(), ob.clone(), on.clone()))
+    g.drain()
+    q.put((rank, [(b.tolist(), n.tolist(), ob.tolist(), on.tolist()) for b, n, ob, on in jobs]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bitstream_gatherer_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_gatherer_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(2))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for j in range(5):
+        b0, n0, ob0, on0 = res[0][j]
+        b1, n1, ob1, on1 = res[1][j]
+        assert ob0 == ob1 == b0 + b1                    # fixed-width slots: every byte travels
+        assert on0 == on1 == n0 + n1
