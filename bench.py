@@ -64,7 +64,7 @@ def main():
     ap.add_argument("--cpu-streams", type=int, default=0, help="oracle sample streams (0 = all)")
     ap.add_argument("--path", default="auto", choices=("auto", "split", "fused"), help="encode kernel path")
     ap.add_argument("--q1-shape", type=int, default=0, help="logits row-stats block shape (tuning)")
-    ap.add_argument("--decode-path", default="auto", choices=("auto", "split", "fused", "stats"))
+    ap.add_argument("--decode-path", default="auto", choices=("auto", "split", "fused", "fused_chunk", "stats"))
     ap.add_argument("--input", default="pmf", choices=("pmf", "logits-bf16", "logits-f32"),
                     help="pmf rows (BASELINE c3, default) or raw logits quantised in-kernel (q1, SURVEY §8(f)1)")
     args = ap.parse_args()

@@ -74,6 +74,7 @@ LAC_OPT_MAPPING = 3
 LAC_OPT_TERMINATION = 4
 LAC_OPT_DECODE_PATH = 5
 LAC_OPT_Q1_SHAPE = 6
+LAC_OPT_DECODE_FINE = 7
 LAC_MAP_CEIL, LAC_MAP_FLOOR = 0, 1
 LAC_TERM_FLUSH, LAC_TERM_ACSAMPLER = 0, 1
 

@@ -71,6 +71,10 @@ constexpr int kWavesPerBlock = 4;     // 256-thread workgroups
 
 // ------------------------------------------------------------------ wave helpers
 __device__ inline uint32_t lane_id() { return __lane_id(); }
+// The wave's index in its workgroup as a wave-uniform (SGPR) value: the
+// compiler cannot tell threadIdx.x >> 6 is uniform, so everything derived from
+// it (stream index, row pointers, coder state) would otherwise occupy VGPRs.
+__device__ inline int wave_in_block() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
 
 __device__ inline uint64_t shfl_u64(uint64_t v, int src) {
     const uint32_t lo = __shfl((int)(uint32_t)v, src), hi = __shfl((int)(uint32_t)(v >> 32), src);
@@ -115,6 +119,19 @@ __device__ inline uint64_t dpp64(uint64_t v) {
 }
 enum : int { kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppHalfMirror = 0x141, kDppMirror = 0x140, kDppShr1 = 0x111,
              kDppShr2 = 0x112, kDppShr4 = 0x114, kDppShr8 = 0x118, kDppBcast15 = 0x142, kDppBcast31 = 0x143 };
+
+// Partner exchange across lane bit BIT inside a 16-lane row, on DPP:
+// bits 0/1 by quad_perm, bits 2/3 by row_shl/row_shr (each lane reads l ^ (1 << BIT)).
+template <int BIT>
+__device__ inline uint32_t xor_dpp(uint32_t x) {
+    if constexpr (BIT == 0) return dpp32<kDppXor1>(x);
+    else if constexpr (BIT == 1) return dpp32<kDppXor2>(x);
+    else {
+        const uint32_t up = dpp32<0x100 + (1 << BIT)>(x);    // row_shl: lane l reads l + 2^BIT
+        const uint32_t dn = dpp32<0x110 + (1 << BIT)>(x);    // row_shr: lane l reads l - 2^BIT
+        return ((lane_id() >> BIT) & 1) ? dn : up;
+    }
+}
 
 template <typename T, typename Op>
 __device__ inline T wave_reduce(T v, Op op) {
@@ -191,6 +208,17 @@ __device__ inline E vget(const typename VecT<E, VEC>::type &v, int j) {
     if constexpr (VEC == 1) { (void)j; return v; } else { return v[j]; }
 }
 
+// Vector vi of a row when vi < nvec, else zeros -- branch-free (a clamped load and
+// a select), so a predicated tail keeps all its loads in flight.  A guarded
+// `vi < nvec ? load : 0` compiles to an exec-masked branch with an
+// s_waitcnt vmcnt(0) inside it: one load in flight at a time.
+template <typename E, int VEC>
+__device__ inline typename VecT<E, VEC>::type load_vec_or0(const E *row, int64_t vi, int64_t nvec) {
+    const bool ok = vi < nvec;
+    const typename VecT<E, VEC>::type x = load_vec<E, VEC>(row, ok ? vi : nvec - 1);
+    return ok ? x : (typename VecT<E, VEC>::type)0;
+}
+
 // ------------------------------------------------------------------ row reduction
 // One wave scans a pmf row: T = sum pmf, lo = sum_{i<s} pmf, ps = pmf[s],
 // minp = smallest positive entry (CDFPredictor.minp, arith_code.py:79-82) -- the
@@ -247,7 +275,7 @@ __device__ inline RowSums row_reduce(const E *row, int64_t V, int64_t s) {
         typename VecT<E, VEC>::type x[U];
 #pragma unroll
         for (int u = 0; u < U; u++)
-            x[u] = (vi + 64 * u < nvec) ? load_vec<E, VEC>(row, vi + 64 * u) : (typename VecT<E, VEC>::type)0;
+            x[u] = load_vec_or0<E, VEC>(row, vi + 64 * u, nvec);
 #pragma unroll
         for (int u = 0; u < U; u++) take(x[u], vi + 64 * u);
     }
@@ -618,8 +646,7 @@ __device__ inline void scan_chunk(const E *row, int64_t nvec, int64_t cv0, int G
 #pragma unroll
         for (int u = 0; u < PF; u++) {
             const int64_t vi = cv0 + (int64_t)(g0 + u) * 64 + lane;
-            if (g0 + u < G && vi < nvec) xs[u] = load_vec<E, VEC>(row, vi);
-            else xs[u] = (typename VecT<E, VEC>::type)0;
+            xs[u] = load_vec_or0<E, VEC>(row, g0 + u < G ? vi : nvec, nvec);
         }
 #pragma unroll
         for (int u = 0; u < PF; u++) {
@@ -797,8 +824,7 @@ __global__ __launch_bounds__(64 * NW) void k_decode_step(const E *__restrict__ p
 #pragma unroll
         for (int g = 0; g < G; g++) {
             const int64_t vi = c * 64 * G + g * 64 + lane;
-            if (vi < nvec) x[g] = load_vec<E, VEC>(row, vi);
-            else x[g] = (typename VecT<E, VEC>::type)0;
+            x[g] = load_vec_or0<E, VEC>(row, vi, nvec);
         }
 #pragma unroll
         for (int g = 0; g < G; g++) {
@@ -883,7 +909,7 @@ __global__ LAC_DEC_BOUNDS void k_decode_wave(const E *__restrict__ pmf, int64_t 
                                                      const uint64_t *nbits, int32_t *sym_out, int64_t B,
                                                      int mapping) {
     const int lane = (int)lane_id();
-    const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + wave_in_block();
     if (b >= B) return;
     DecState st = states[b];
     const uint8_t *mybits = bits + b * stride;
@@ -907,11 +933,13 @@ __global__ LAC_DEC_BOUNDS void k_decode_wave(const E *__restrict__ pmf, int64_t 
             uint64_t acc = 0;
             for (int64_t g0 = 0; g0 < CI; g0 += U) {
                 typename VecT<E, VEC>::type x[U];
+                const bool full = (c * CI + g0 + U) * 64 <= nvec;
+                if (full) {
 #pragma unroll
-                for (int u = 0; u < U; u++) {
-                    const int64_t vi = (c * CI + g0 + u) * 64 + lane;
-                    if (vi < nvec) x[u] = load_vec<E, VEC>(row, vi);
-                    else x[u] = (typename VecT<E, VEC>::type)0;
+                    for (int u = 0; u < U; u++) x[u] = load_vec<E, VEC>(row, (c * CI + g0 + u) * 64 + lane);
+                } else {
+#pragma unroll
+                    for (int u = 0; u < U; u++) x[u] = load_vec_or0<E, VEC>(row, (c * CI + g0 + u) * 64 + lane, nvec);
                 }
 #pragma unroll
                 for (int u = 0; u < U; u++) {
@@ -976,6 +1004,163 @@ __global__ LAC_DEC_BOUNDS void k_decode_wave(const E *__restrict__ pmf, int64_t 
     if (lane == 0) states[b] = st;
 }
 
+// 64-bit partner exchange across lane bit BIT (DPP inside a 16-lane row, a
+// ds_bpermute swizzle across rows).
+template <int BIT>
+__device__ inline uint64_t xor_lane_u64(uint64_t x) {
+    if constexpr (BIT < 4) return ((uint64_t)xor_dpp<BIT>((uint32_t)(x >> 32)) << 32) | xor_dpp<BIT>((uint32_t)x);
+    else return shfl_xor_u64(x, 1 << BIT);
+}
+template <bool CHK>
+__device__ inline uint64_t add_ovf(uint64_t a, uint64_t b, uint32_t &ovf) {
+    const uint64_t s = a + b;
+    if constexpr (CHK) ovf |= s < a;
+    return s;
+}
+
+// Totals of 8 per-lane values s[0..7] over the wave, all 8 at once: halving
+// exchanges over lane bits 0..2 (DPP), then full sums over bits 3..5.  Lane l
+// ends with the total of s[l & 7] (the inputs are fed bit-reversed, so the
+// halving's reversed index order comes out straight).  CHK tracks u64 wrap.
+template <bool CHK>
+__device__ inline uint64_t wave_sum8_u64(const uint64_t (&s)[8], uint32_t &ovf) {
+    const int lane = (int)lane_id();
+    uint64_t v[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) v[i] = s[((i & 1) << 2) | (i & 2) | ((i >> 2) & 1)];
+    {
+        const bool up = lane & 1;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint64_t keep = up ? v[i + 4] : v[i], give = up ? v[i] : v[i + 4];
+            v[i] = add_ovf<CHK>(keep, xor_lane_u64<0>(give), ovf);
+        }
+    }
+    {
+        const bool up = lane & 2;
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            const uint64_t keep = up ? v[i + 2] : v[i], give = up ? v[i] : v[i + 2];
+            v[i] = add_ovf<CHK>(keep, xor_lane_u64<1>(give), ovf);
+        }
+    }
+    {
+        const bool up = lane & 4;
+        const uint64_t keep = up ? v[1] : v[0], give = up ? v[0] : v[1];
+        v[0] = add_ovf<CHK>(keep, xor_lane_u64<2>(give), ovf);
+    }
+    uint64_t r = v[0];
+    r = add_ovf<CHK>(r, xor_lane_u64<3>(r), ovf);
+    r = add_ovf<CHK>(r, xor_lane_u64<4>(r), ovf);
+    r = add_ovf<CHK>(r, xor_lane_u64<5>(r), ovf);
+    return r;
+}
+
+// k_decode_wave with one total per 64-vector iteration of the row instead of per
+// <= 64-iteration chunk (rows of <= 512 iterations: V <= 131072 u32 / 65536 u64
+// entries).  Iteration p's total lives in lane p % 64 of register p / 64, the
+// search scans those NR registers, and the re-read after the search is ONE 16-B
+// load per lane (1 KB, 0.8 % of a 32000-entry u32 row) instead of a chunk of
+// eight (6.3 %), which also shortens the dependent tail of every step.
+template <typename E, int VEC, int NR>
+__global__ LAC_DEC_BOUNDS void k_decode_wave_fine(const E *__restrict__ pmf, int64_t step_stride,
+                                                  int64_t stream_stride, int64_t nsteps, int64_t V, int prec,
+                                                  DecState *states, const uint8_t *bits, uint64_t stride,
+                                                  const uint64_t *nbits, int32_t *sym_out, int64_t B, int mapping) {
+    constexpr bool W = sizeof(E) == 8;
+    const int lane = (int)lane_id();
+    const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + wave_in_block();
+    if (b >= B) return;
+    DecState st = states[b];
+    const uint8_t *mybits = bits + b * stride;
+    const uint64_t mynbits = nbits[b];
+    const int nvec = (int)(V / VEC), nit = (nvec + 63) / 64, ngrp = (nit + 7) / 8;
+    for (int64_t t = 0; t < nsteps; t++) {
+        int32_t *out = sym_out + t * B + b;
+        if (st.err) {
+            if (lane == 0) *out = -1;
+            continue;
+        }
+        const E *row = pmf + t * step_stride + b * stream_stride;
+        uint64_t mine[NR];
+#pragma unroll
+        for (int r = 0; r < NR; r++) mine[r] = 0;
+        E mn = (E)~(E)0;
+        uint32_t ovf = 0;
+        const int nfull = nvec / 512;                         // groups of 8 whole iterations
+        auto group = [&](int g, bool full) {
+            typename VecT<E, VEC>::type x[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int vi = (g * 8 + u) * 64 + lane;
+                x[u] = full ? load_vec<E, VEC>(row, vi) : load_vec_or0<E, VEC>(row, vi, nvec);
+            }
+            uint64_t s[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                uint64_t a = 0;
+#pragma unroll
+                for (int j = 0; j < VEC; j++) {
+                    const E e = vget<E, VEC>(x[u], j);
+                    a = add_ovf<W>(a, (uint64_t)e, ovf);
+                    const E m1 = e - 1;
+                    mn = m1 < mn ? m1 : mn;
+                }
+                s[u] = a;
+            }
+            const uint64_t tot = wave_sum8_u64<W>(s, ovf);    // lane l: iteration g*8 + (l & 7)
+            const bool mylane = (lane >> 3) == (g & 7);
+#pragma unroll
+            for (int r = 0; r < NR; r++)
+                if (r == (g >> 3) && mylane) mine[r] = tot;
+        };
+        for (int g = 0; g < nfull; g++) group(g, true);
+        if (nfull < ngrp) group(nfull, false);
+        uint64_t minp;
+        if constexpr (W) minp = wave_min_u64(mn) + 1;
+        else minp = (uint64_t)wave_min_u32(mn) + 1;
+        uint64_t incl[NR];
+        u128 lsum = 0;
+        uint64_t base = 0;
+#pragma unroll
+        for (int r = 0; r < NR; r++) {
+            lsum += mine[r];
+            incl[r] = base + wave_incl_scan_u64(mine[r]);     // exact once T < 2^64 is checked
+            base = readlane_u64(incl[r], 63);
+        }
+        const u128 acc128 = W ? wave_sum_u128(lsum) : (u128)base;
+        int err = 0;
+        if (__any(ovf) || (acc128 >> 64) || acc128 == 0) err = LAC_E_TABLE;
+        int64_t s = -1;
+        if (!err) {
+            auto find_chunk = [&](uint64_t tgt, int64_t *cv0, int *G, uint64_t *cb) {
+#pragma unroll
+                for (int r = 0; r < NR; r++) {
+                    const uint64_t ex = incl[r] - mine[r];
+                    const bool hit = r * 64 + lane < nit && ex <= tgt && tgt < incl[r];
+                    const uint64_t mask = __ballot(hit);
+                    if (mask) {
+                        const int src = __ffsll((unsigned long long)mask) - 1;
+                        *cv0 = (int64_t)(r * 64 + src) * 64;
+                        *G = 1;
+                        *cb = readlane_u64(ex, src);
+                        return true;
+                    }
+                }
+                return false;
+            };
+            err = decode_symbol<E, VEC>(st, row, V, (uint64_t)acc128, minp, prec, mapping, mybits, mynbits,
+                                        find_chunk, &s);
+        }
+        if (err) {
+            st.err = err;
+            st.err_step = st.nsym;
+        }
+        if (lane == 0) *out = err ? -1 : (int32_t)s;
+    }
+    if (lane == 0) states[b] = st;
+}
+
 // ---------------------------------------------------------- decode, stats path
 // Few streams: the per-step kernels above leave the chip idle (one stream's row
 // per step) and pay a launch per step.  The row statistics a decode step needs
@@ -1023,8 +1208,7 @@ __global__ __launch_bounds__(256) void k_dec_stats(const E *__restrict__ pmf, in
 #pragma unroll
             for (int u = 0; u < U; u++) {
                 const int64_t vi = (c * CI + g0 + u) * 64 + lane;
-                if (vi < nvec) x[u] = load_vec<E, VEC>(row, vi);
-                else x[u] = (typename VecT<E, VEC>::type)0;
+                x[u] = load_vec_or0<E, VEC>(row, vi, nvec);
             }
 #pragma unroll
             for (int u = 0; u < U; u++) {
@@ -1257,19 +1441,6 @@ __device__ inline uint64_t wave_multi_sum(uint64_t (&v)[R]) {
 #pragma unroll
     for (int k = 32 / R; k >= 1; k >>= 1) r += shfl_xor_u64(r, k);
     return r;
-}
-
-// Partner exchange across lane bit BIT inside a 16-lane row, on DPP:
-// bits 0/1 by quad_perm, bits 2/3 by row_shl/row_shr (each lane reads l ^ (1 << BIT)).
-template <int BIT>
-__device__ inline uint32_t xor_dpp(uint32_t x) {
-    if constexpr (BIT == 0) return dpp32<kDppXor1>(x);
-    else if constexpr (BIT == 1) return dpp32<kDppXor2>(x);
-    else {
-        const uint32_t up = dpp32<0x100 + (1 << BIT)>(x);    // row_shl: lane l reads l + 2^BIT
-        const uint32_t dn = dpp32<0x110 + (1 << BIT)>(x);    // row_shr: lane l reads l - 2^BIT
-        return ((lane_id() >> BIT) & 1) ? dn : up;
-    }
 }
 
 template <int R, int BIT>
@@ -1641,6 +1812,7 @@ struct lac_ctx {
     int64_t chunk_steps = 64;           // split path: steps per row-stats launch
     int dpath = LAC_PATH_AUTO;          // decode kernel path
     int64_t wave_decode_min_streams = 2048;   // measured: the stats path wins at 1024 streams
+    int fine_decode = 1;                // one-wave decode: per-iteration totals (k_decode_wave_fine)
     int mapping = LAC_MAP_CEIL;         // symbol_to_range flavour (lac_set_option)
     int term = LAC_TERM_FLUSH;          // stream termination flavour
     int cus = 256;                      // compute units (persistent grids)
@@ -1802,9 +1974,24 @@ template <typename E, int VEC>
 static int decode_wave_launch(lac_ctx *c, const E *pmf, int64_t step_stride, int64_t stream_stride, int64_t steps,
                               int32_t *out, hipStream_t st) {
     ProfScope ps(c, KID_DECODE_WAVE, st);
-    k_decode_wave<E, VEC><<<(unsigned)((c->B + kWavesPerBlock - 1) / kWavesPerBlock), 64 * kWavesPerBlock, 0, st>>>(
-        pmf, step_stride, stream_stride, steps, c->V, c->prec, c->dec, c->dbits, c->dstride, c->dnbits, out, c->B,
-        c->mapping);
+    const unsigned blocks = (unsigned)((c->B + kWavesPerBlock - 1) / kWavesPerBlock);
+    const int64_t nit = (c->V / VEC + 63) / 64;               // 64-vector iterations per row
+#define LAC_FINE(NR)                                                                                              \
+    k_decode_wave_fine<E, VEC, NR><<<blocks, 64 * kWavesPerBlock, 0, st>>>(                                      \
+        pmf, step_stride, stream_stride, steps, c->V, c->prec, c->dec, c->dbits, c->dstride, c->dnbits, out, c->B, \
+        c->mapping)
+    bool fine = false;
+    if constexpr (VEC > 1) {
+        fine = c->fine_decode && nit <= 512;
+        if (fine && nit <= 128) LAC_FINE(2);
+        else if (fine && nit <= 256) LAC_FINE(4);
+        else if (fine) LAC_FINE(8);
+    }
+    if (!fine)
+        k_decode_wave<E, VEC><<<blocks, 64 * kWavesPerBlock, 0, st>>>(
+            pmf, step_stride, stream_stride, steps, c->V, c->prec, c->dec, c->dbits, c->dstride, c->dnbits, out, c->B,
+            c->mapping);
+#undef LAC_FINE
     CHECK_LAUNCH();
     return LAC_OK;
 }
@@ -2125,6 +2312,10 @@ int lac_set_option(lac_ctx *c, int option, int64_t value) {
     case LAC_OPT_DECODE_PATH:
         if (value < LAC_PATH_AUTO || value > LAC_PATH_STATS) return fail(LAC_E_ARG, "bad decode path");
         c->dpath = (int)value;
+        return LAC_OK;
+    case LAC_OPT_DECODE_FINE:
+        if (value != 0 && value != 1) return fail(LAC_E_ARG, "decode_fine must be 0 or 1");
+        c->fine_decode = (int)value;
         return LAC_OK;
     case LAC_OPT_Q1_SHAPE:
         if (value < 0 || value > 10) return fail(LAC_E_ARG, "bad q1 shape");

@@ -52,7 +52,7 @@ def _gpu_encode(pmf_np, sym_np, prec, trace=False, path="auto", job=False):
     return c, pmf, data, n, tr
 
 
-DECODE_PATHS = ("split", "fused", "stats")
+DECODE_PATHS = ("split", "fused", "fused_chunk", "stats")
 
 
 def _decode_both(c, dpmf):
@@ -408,3 +408,32 @@ def test_stats_decode_spans_step_chunks():
         dets.append(c.determined())
     assert all((d == dets[0]).all() for d in dets[1:])
     c.raise_on_error()
+
+
+# ------------------------------------------------- one-wave decode granularity
+@pytest.mark.gpu
+@pytest.mark.parametrize("V,bits", [(32000, 32), (32004, 32), (32768, 32), (33024, 32), (65540, 32),
+                                    (128256, 32), (131076, 32), (16000, 64), (32000, 64), (65538, 64)])
+def test_decode_wave_granularity(V, bits):
+    """k_decode_wave_fine (per-iteration totals; register counts 2/4/8 and the
+    fallback beyond 512 iterations) against the chunk-total kernel, the per-step
+    kernel and the symbols, on ragged and exact row lengths, u32 and unfudged u64."""
+    from oracle import oracle as coracle
+    B, steps, prec = 16, 3, 48
+    pmf, sym = synth.softmax_tables(steps, B, V, seed=77 + V, device=DEV)
+    if bits == 64:
+        pmf = pmf.to(torch.int64)
+    c = _coder(V, B, prec, bits=bits, cap=steps * (prec + 2) + 256)
+    c.encode_job(pmf, sym)
+    data, n = c.to_bytes()
+    host = pmf[:, :4, :].cpu().numpy()
+    host = host.view(np.uint32) if bits == 32 else host.view(np.uint64)
+    out, nb, _, rc = coracle.encode_batch(host, sym[:, :4].cpu().numpy(), prec, nthreads=4)
+    assert rc == 0
+    for b in range(4):
+        assert data[b] == out[b, :(int(nb[b]) + 7) // 8].tobytes()
+    for path in ("fused", "fused_chunk", "split"):
+        c.set_decode_path(path)
+        c.decode_open()
+        assert torch.equal(c.decode(pmf), sym), path
+    c.close()
