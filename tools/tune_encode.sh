@@ -11,7 +11,7 @@ if [ "${1:-}" = build ]; then
         case $v in
           base) f="";;
           enc4) f="-DLAC_ENC_MINW=4";; enc3) f="-DLAC_ENC_MINW=3";;
-          dec0) f="-DLAC_DEC_MINW=0";; dec3) f="-DLAC_DEC_MINW=3";;
+          dec0) f="-DLAC_DEC_MINW=0";; dec3) f="-DLAC_DEC_MINW=3";; dec2) f="-DLAC_DEC_MINW=2";; decf4) f="-DLAC_DECF_MINW=4";; decf3) f="-DLAC_DECF_MINW=3";;
           u8_nt) f="-DLAC_UNROLL=8 -DLAC_NT=1";; u16_nt) f="-DLAC_UNROLL=16 -DLAC_NT=1";;
           u8_plain) f="-DLAC_UNROLL=8 -DLAC_NT=0";; u16_plain) f="-DLAC_UNROLL=16 -DLAC_NT=0";;
           u4_nt) f="-DLAC_UNROLL=4 -DLAC_NT=1";;
