@@ -1327,6 +1327,15 @@ __constant__ uint32_t c_q1_tab[LAC_Q1_TAB_SIZE] = LAC_Q1_TAB_INIT;
 #endif
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+__device__ inline s16x2 as_s16x2(uint32_t w) {
+    s16x2 r;
+    __builtin_memcpy(&r, &w, 4);
+    return r;
+}
+#ifndef LAC_Q1_IMAX
+#define LAC_Q1_IMAX 1            // bf16 row max on packed int16 bit patterns (k_q1_stats)
+#endif
 
 template <typename LT> struct LogitN { static constexpr int N = 16 / sizeof(LT); };
 
@@ -1526,9 +1535,11 @@ __global__ __launch_bounds__(64 * NWB, 4) void k_q1_stats(const LT *__restrict__
                                                               uint64_t *__restrict__ chunks,
                                                               float *__restrict__ mrow) {
     constexpr int N = LogitN<LT>::N, NT = 64 * RW, NR = NWB / RW;
+    constexpr bool IMAX = LAC_Q1_IMAX && sizeof(LT) == 2 && NR == 1 && !MULTI;
     static_assert(R * N <= 128, "lane sums must fit 32 bits");
     __shared__ uint32_t tabr[LAC_Q1_TAB_SIZE * kQ1Rep];
     __shared__ float smax[NWB];
+    __shared__ int smaxi[NWB];
     __shared__ uint64_t ssum[NWB][2];
     __shared__ uint32_t sps[NR];
     __shared__ unsigned long long bins[DEC ? NR : 1][64];
@@ -1563,18 +1574,61 @@ __global__ __launch_bounds__(64 * NWB, 4) void k_q1_stats(const LT *__restrict__
             }
         } else {
             if (!PF) q1_load_tile<LT, R>(x, row, valid, 0, gt, NT, nvec);   // PF: loaded during the last row
+            if constexpr (!IMAX) {
 #pragma unroll
-            for (int j = 0; j < R; j++)
+                for (int j = 0; j < R; j++)
 #pragma unroll
-                for (int e = 0; e < N; e++) mx = fmaxf(mx, logit_at<LT>(x[j], e));
+                    for (int e = 0; e < N; e++) mx = fmaxf(mx, logit_at<LT>(x[j], e));
+            }
         }
-        mx = wave_max_f32(mx);
-        if (lane == 0) smax[w] = mx;
-        if (!DEC && gt == 0) sps[g] = 0;
-        __syncthreads();
-        float m = smax[g * RW];
+        float m;
+        if constexpr (IMAX) {
+            // bf16 rows owned by the whole block: the maximum over the raw bit patterns
+            // as int16 (one v_pk_max_i16 per two logits) is the float maximum whenever
+            // the row has a positive, non-NaN maximum (sign-magnitude: positives order
+            // as integers and beat every negative).  Other rows (all negative, or a
+            // positive NaN) redo it exactly in floats from the same registers.
+            s16x2 pm = {(short)-32768, (short)-32768};
 #pragma unroll
-        for (int i = 1; i < RW; i++) m = fmaxf(m, smax[g * RW + i]);
+            for (int j = 0; j < R; j++) {          // (.x/.y/.z/.w: a bit_cast of x[j][k] lost 3 of 4 words)
+                pm = __builtin_elementwise_max(pm, as_s16x2(x[j].x));
+                pm = __builtin_elementwise_max(pm, as_s16x2(x[j].y));
+                pm = __builtin_elementwise_max(pm, as_s16x2(x[j].z));
+                pm = __builtin_elementwise_max(pm, as_s16x2(x[j].w));
+            }
+            const int li = pm.x > pm.y ? (int)pm.x : (int)pm.y;
+            const int wi = (int)wave_reduce((uint32_t)li, [](uint32_t a, uint32_t b) {
+                return (uint32_t)((int)a > (int)b ? (int)a : (int)b);
+            });
+            if (lane == 0) smaxi[w] = wi;
+            if (!DEC && gt == 0) sps[g] = 0;
+            __syncthreads();
+            int bi = smaxi[0];
+#pragma unroll
+            for (int i = 1; i < NWB; i++) bi = smaxi[i] > bi ? smaxi[i] : bi;
+            if (bi >= 0 && bi <= 0x7F80) {                    // block-uniform
+                m = __uint_as_float((uint32_t)bi << 16);
+            } else {
+#pragma unroll
+                for (int j = 0; j < R; j++)
+#pragma unroll
+                    for (int e = 0; e < N; e++) mx = fmaxf(mx, logit_at<LT>(x[j], e));
+                mx = wave_max_f32(mx);
+                if (lane == 0) smax[w] = mx;
+                __syncthreads();
+                m = smax[0];
+#pragma unroll
+                for (int i = 1; i < NWB; i++) m = fmaxf(m, smax[i]);
+            }
+        } else {
+            mx = wave_max_f32(mx);
+            if (lane == 0) smax[w] = mx;
+            if (!DEC && gt == 0) sps[g] = 0;
+            __syncthreads();
+            m = smax[g * RW];
+#pragma unroll
+            for (int i = 1; i < RW; i++) m = fmaxf(m, smax[g * RW + i]);
+        }
         const bool fast = q1_fast_row(m);
         const float c = q1_c(m);
         int sfull = -1, sr = 0;

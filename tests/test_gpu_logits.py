@@ -37,6 +37,15 @@ def _logits(seed, steps, B, V, scale=3.0, specials=False):
             x[2, 0, 9] = 262143.5 - 3.0
             x[2, B - 1, 3] = 3.0e5                                # just past it: capped (slow) path
             x[2, B - 1, 4] = 3.0e5 - 0.25
+        if steps > 3 and B > 2:
+            # row maxima the bf16 packed-int16 max must hand to the exact float path
+            x[3, 0, :] = -np.abs(x[3, 0, :]) - 1.0                   # all negative
+            x[3, 1, :] = -np.abs(x[3, 1, :]) - 1.0
+            x[3, 1, 6] = -0.0                                     # max -0.0
+            x[3, 2, :] = -np.abs(x[3, 2, :]) - 1.0
+            x[3, 2, 11] = 0.0                                     # max +0.0, all else negative
+            x[3, B - 1, 2] = np.float32(-np.nan)                  # negative NaN in a normal row
+            x[1, B - 1, 8] = np.float32(np.nan)                   # positive NaN in a normal row
     return x
 
 

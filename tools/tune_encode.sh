@@ -15,6 +15,7 @@ if [ "${1:-}" = build ]; then
           u8_nt) f="-DLAC_UNROLL=8 -DLAC_NT=1";; u16_nt) f="-DLAC_UNROLL=16 -DLAC_NT=1";;
           u8_plain) f="-DLAC_UNROLL=8 -DLAC_NT=0";; u16_plain) f="-DLAC_UNROLL=16 -DLAC_NT=0";;
           u4_nt) f="-DLAC_UNROLL=4 -DLAC_NT=1";;
+          imax0) f="-DLAC_Q1_IMAX=0";;
           q1u4) f="-DLAC_Q1_UNROLL=4";; q1u2) f="-DLAC_Q1_UNROLL=2";; q1u16) f="-DLAC_Q1_UNROLL=16";;
           q1nt1) f="-DLAC_Q1_NT1=1";; q1plain) f="-DLAC_Q1_NT2=0";; q1w2) f="-DLAC_Q1_MINW=2";;
           q1u4w2) f="-DLAC_Q1_UNROLL=4 -DLAC_Q1_MINW=2";; q1u4w3) f="-DLAC_Q1_UNROLL=4 -DLAC_Q1_MINW=3";;
