@@ -42,9 +42,10 @@ def read_traffic(cfg, kernel):
             d = json.load(f)
     except (OSError, ValueError):
         return None
-    keys = ("vocab", "streams", "tokens", "pmf_bits")
-    if all(d.get(k) == cfg.get(k) for k in keys):
-        return d.get("bytes_per_launch", {}).get(kernel)
+    keys = ("vocab", "streams", "tokens", "pmf_bits", "input")
+    for e in d.get("entries", []):
+        if all(e.get(k) == cfg.get(k) for k in keys):
+            return e.get("bytes_per_launch", {}).get(kernel)
     return None
 
 

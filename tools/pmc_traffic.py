@@ -3,7 +3,8 @@
 
     rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc -o run --output-format csv \
         -- python3 bench.py --steps 3 --warmup 1 --cpu-baseline off
-    python tools/pmc_traffic.py gpurun_out/pmc > profiles/pmc_traffic.json
+    python tools/pmc_traffic.py gpurun_out/pmc [--input pmf|logits-bf16|logits-f32] [--vocab V --tokens T]
+        (adds / replaces this configuration's entry in profiles/pmc_traffic.json)
 
 FETCH_SIZE is reported in KiB.  On gfx950 it reads exactly half of the bytes of
 a wide (16 B/lane) coalesced streaming read (MI355X_MICROARCH.md, HBM section),
@@ -17,17 +18,18 @@ import os
 import statistics
 import sys
 
-STREAMING = ("k_encode_fused", "k_row_stats", "k_decode_step")
+STREAMING = ("k_encode_fused", "k_row_stats", "k_decode_step", "k_decode_wave_fine", "k_decode_wave",
+             "k_q1_stats", "k_dec_stats")
 
 
 def short(name):
-    for k in STREAMING + ("k_encode", "k_finish"):
+    for k in STREAMING + ("k_encode", "k_finish", "k_q1_decode"):
         if f"::{k}<" in name or f"::{k}(" in name:
             return k
     return None
 
 
-def main(d, vocab=32000, streams=4096, tokens=16, pmf_bits=32):
+def main(d, vocab=32000, streams=4096, tokens=16, pmf_bits=32, inp="pmf", out_path=None):
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     if not files:
         sys.exit(f"no counter_collection.csv under {d}")
@@ -40,16 +42,38 @@ def main(d, vocab=32000, streams=4096, tokens=16, pmf_bits=32):
                 k = short(row.get("Kernel_Name", ""))
                 if k:
                     per.setdefault(k, []).append(float(row["Counter_Value"]))
-    out = {"vocab": vocab, "streams": streams, "tokens": tokens, "pmf_bits": pmf_bits,
+    ent = {"vocab": vocab, "streams": streams, "tokens": tokens, "pmf_bits": pmf_bits, "input": inp,
            "counter": "FETCH_SIZE (KiB), x1024 x2 gfx950 wide-read correction", "bytes_per_launch": {},
            "raw_fetch_kib_median": {}, "dispatches": {}}
     for k, v in per.items():
         med = statistics.median(v)
-        out["raw_fetch_kib_median"][k] = med
-        out["dispatches"][k] = len(v)
-        out["bytes_per_launch"][k] = med * 1024 * (2 if k in STREAMING else 1)
-    print(json.dumps(out, indent=1))
+        ent["raw_fetch_kib_median"][k] = med
+        ent["dispatches"][k] = len(v)
+        ent["bytes_per_launch"][k] = med * 1024 * (2 if k in STREAMING else 1)
+    doc = {"entries": []}
+    if out_path and os.path.exists(out_path):
+        with open(out_path) as fh:
+            old = json.load(fh)
+        doc["entries"] = [e for e in old.get("entries", [])
+                          if any(e.get(k) != ent[k] for k in ("vocab", "streams", "tokens", "pmf_bits", "input"))]
+    doc["entries"].append(ent)
+    text = json.dumps(doc, indent=1)
+    if out_path:
+        with open(out_path, "w") as fh:
+            fh.write(text + "\n")
+    print(text)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc")
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir", nargs="?", default="gpurun_out/pmc")
+    ap.add_argument("--vocab", type=int, default=32000)
+    ap.add_argument("--streams", type=int, default=4096)
+    ap.add_argument("--tokens", type=int, default=16)
+    ap.add_argument("--pmf-bits", type=int, default=32)
+    ap.add_argument("--input", default="pmf")
+    ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles",
+                                                  "pmc_traffic.json"))
+    a = ap.parse_args()
+    main(a.dir, a.vocab, a.streams, a.tokens, a.pmf_bits, a.input, a.out)
