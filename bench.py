@@ -252,7 +252,7 @@ def main():
         rows = (f"{args.input[7:]} logit rows, q1 tables in-kernel" if logits_in else f"uint{args.pmf_bits} pmf rows")
         cfg = {"workload": f"c3: vocab={V}, {B} streams/GPU, {T} symbols/stream per job, prec={P}, {rows}",
                "vocab": V, "streams": B, "tokens": T, "prec": P, "pmf_bits": args.pmf_bits, "input": args.input,
-               "parallelism": f"streams sharded over {world} GPU(s)" + (", RCCL bitstream all-gather" if world > 1 else "")}
+               "parallelism": f"streams sharded over {world} GPU(s)" + (f", {'RCCL' if backend == 'nccl' else backend} bitstream all-gather" if world > 1 else "")}
         value = world * B * T * args.steps / dt
         line = {
             "metric": METRIC, "value": value, "unit": "symbols/s", "n_gpus": world, "steps": args.steps,
