@@ -65,7 +65,8 @@ def main():
     ap.add_argument("--cpu-streams", type=int, default=0, help="oracle sample streams (0 = all)")
     ap.add_argument("--path", default="auto", choices=("auto", "split", "fused"), help="encode kernel path")
     ap.add_argument("--q1-shape", type=int, default=0, help="logits row-stats block shape (tuning)")
-    ap.add_argument("--decode-path", default="auto", choices=("auto", "split", "fused", "fused_chunk", "stats"))
+    ap.add_argument("--decode-path", default="auto", choices=("auto", "split", "fused", "fused_chunk", "stats", "block"))
+    ap.add_argument("--block-waves", type=int, default=0, help="block decode path: waves per stream (tuning)")
     ap.add_argument("--input", default="pmf", choices=("pmf", "logits-bf16", "logits-f32"),
                     help="pmf rows (BASELINE c3, default) or raw logits quantised in-kernel (q1, SURVEY §8(f)1)")
     args = ap.parse_args()
@@ -120,6 +121,8 @@ def main():
         coder.set_q1_shape(args.q1_shape)
     if args.decode_path != "auto":
         coder.set_decode_path(args.decode_path)
+    if args.block_waves:
+        coder.set_block_waves(args.block_waves)
 
     # N > 1: each job's bitstreams are all-gathered over RCCL into fixed-width slots,
     # asynchronously (overlapping the next job's encode), double-buffered

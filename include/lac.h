@@ -69,16 +69,18 @@ enum {                       /* lac_set_option */
     LAC_OPT_TERMINATION = 4,       /* LAC_TERM_*: how a stream is closed */
     LAC_OPT_DECODE_PATH = 5,       /* LAC_PATH_*: SPLIT = one 4-wave workgroup per stream and step,
                                       FUSED = one wave per stream, all steps of a call in one launch;
-                                      STATS = see LAC_PATH_STATS; AUTO = FUSED from 2048 streams,
-                                      else STATS */
+                                      STATS, BLOCK = see LAC_PATH_STATS / LAC_PATH_BLOCK;
+                                      AUTO = FUSED from 2048 streams, BLOCK from 4, else STATS */
     LAC_OPT_Q1_SHAPE = 6,          /* logits path row-stats shape: 0 = auto (default), 1..7 = (waves per
                                       row, vectors/thread, rolling prefetch) (1,4,n) (2,8,n) (4,8,n)
                                       (8,8,n) (8,16,n) (8,8,y) (8,4,y), 8 = tiles of (8,8,n),
                                       9 = 16-wave (16,16,n), 10 = tiles of 9; identical results,
                                       only speed differs */
-    LAC_OPT_DECODE_FINE = 7        /* one-wave decode (FUSED path): 1 = one total per 64 vectors of
+    LAC_OPT_DECODE_FINE = 7,       /* one-wave decode (FUSED path): 1 = one total per 64 vectors of
                                       the row, so only 1 KB is re-read after the search (default,
                                       rows <= 131072 u32 / 65536 u64 entries); 0 = <= 64 chunk totals */
+    LAC_OPT_BLOCK_WAVES = 8        /* BLOCK decode path: waves per stream (4, 8, 16; 0 = by stream
+                                      count, the default) */
 };
 enum {
     LAC_MAP_CEIL = 0,              /* CDFPredictor.symbol_to_range + fudged_dist (arith_code.py:83-110) */
@@ -94,9 +96,13 @@ enum {
     LAC_PATH_AUTO = 0,             /* fused if streams >= fused_min_streams, else split */
     LAC_PATH_SPLIT = 1,            /* row-stats kernel over all (step, stream) rows + coder kernel */
     LAC_PATH_FUSED = 2,            /* one wave per stream: row scan + coder in one kernel */
-    LAC_PATH_STATS = 3             /* decode only: chunk totals of every (step, stream) row in one
+    LAC_PATH_STATS = 3,            /* decode only: chunk totals of every (step, stream) row in one
                                       full-chip kernel, then a per-stream sequential kernel that
-                                      re-reads one chunk per step (AUTO below 2048 streams) */
+                                      re-reads one chunk per step */
+    LAC_PATH_BLOCK = 4             /* decode only: one 4/8/16-wave workgroup per stream, all steps in
+                                      one launch; the other waves stream row t+1 while wave 0 decodes
+                                      step t (AUTO from 4 to 2047 streams; rows <= 512 iterations of
+                                      64 16-B vectors, 16-B aligned, else STATS) */
 };
 
 /* Library identification and the last error message of this thread. */

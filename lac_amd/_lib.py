@@ -69,12 +69,13 @@ KERNEL_IDS = {"row_stats": 0, "encode": 1, "finish": 2, "decode_step": 3, "encod
 LAC_LOGITS_BF16, LAC_LOGITS_F32 = 1, 2
 LAC_OPT_ENCODE_PATH = 1
 LAC_OPT_FUSED_MIN_STREAMS = 2
-LAC_PATH_AUTO, LAC_PATH_SPLIT, LAC_PATH_FUSED, LAC_PATH_STATS = 0, 1, 2, 3
+LAC_PATH_AUTO, LAC_PATH_SPLIT, LAC_PATH_FUSED, LAC_PATH_STATS, LAC_PATH_BLOCK = 0, 1, 2, 3, 4
 LAC_OPT_MAPPING = 3
 LAC_OPT_TERMINATION = 4
 LAC_OPT_DECODE_PATH = 5
 LAC_OPT_Q1_SHAPE = 6
 LAC_OPT_DECODE_FINE = 7
+LAC_OPT_BLOCK_WAVES = 8
 LAC_MAP_CEIL, LAC_MAP_FLOOR = 0, 1
 LAC_TERM_FLUSH, LAC_TERM_ACSAMPLER = 0, 1
 

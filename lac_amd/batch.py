@@ -161,12 +161,17 @@ class BatchCoder:
     def set_decode_path(self, path):
         """'auto', 'split' (one workgroup per stream per step), 'fused' (one wave per
         stream, one launch; per-iteration row totals), 'fused_chunk' (the same with
-        <= 64 chunk totals per row) or 'stats' (all rows' chunk totals at once, then
-        a sequential per-stream kernel); identical results."""
+        <= 64 chunk totals per row), 'stats' (all rows' chunk totals at once, then
+        a sequential per-stream kernel) or 'block' (one workgroup per stream, the
+        row scans pipelined a step ahead of the coder wave); identical results."""
         v = {"auto": _lib.LAC_PATH_AUTO, "split": _lib.LAC_PATH_SPLIT, "fused": _lib.LAC_PATH_FUSED,
-             "fused_chunk": _lib.LAC_PATH_FUSED, "stats": _lib.LAC_PATH_STATS}[path]
+             "fused_chunk": _lib.LAC_PATH_FUSED, "stats": _lib.LAC_PATH_STATS, "block": _lib.LAC_PATH_BLOCK}[path]
         check(self.lib.lac_set_option(self.ctx, _lib.LAC_OPT_DECODE_PATH, v))
         check(self.lib.lac_set_option(self.ctx, _lib.LAC_OPT_DECODE_FINE, 0 if path == "fused_chunk" else 1))
+
+    def set_block_waves(self, n: int):
+        """Waves per stream of the 'block' decode path: 4, 8, 16 (0 = by stream count)."""
+        check(self.lib.lac_set_option(self.ctx, _lib.LAC_OPT_BLOCK_WAVES, int(n)))
 
     def set_path(self, path):
         """'auto', 'split' or 'fused' encode kernels (bit-identical results)."""

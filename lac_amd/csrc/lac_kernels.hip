@@ -1166,6 +1166,140 @@ __global__ __launch_bounds__(256, LAC_DECF_MINW) void k_decode_wave_fine(const E
     if (lane == 0) states[b] = st;
 }
 
+// ---------------------------------------------------------- decode, block path
+// Fewer streams than fill the chip with one wave each: one NW-wave workgroup
+// per stream, pipelined.  Waves 1..NW-1 ("streamers") stream row t+1 into
+// per-iteration totals in LDS (groups of 8 iterations, k_decode_wave_fine's
+// butterfly) while wave 0 (the coder) finishes step t from row t's totals:
+// search, the one 16-B-per-lane re-read, renormalisation.  The rows do not
+// depend on the decoder state, so only the totals cross between waves, double
+// buffered, with one workgroup barrier per step.  NW = 4/8/16 keeps ~16 waves
+// per CU from 1024 down to 256 streams.
+template <typename E, int VEC, int NW>
+__global__ __launch_bounds__(64 * NW) void k_decode_block(const E *__restrict__ pmf, int64_t step_stride,
+                                                          int64_t stream_stride, int64_t nsteps, int64_t V, int prec,
+                                                          DecState *states, const uint8_t *bits, uint64_t stride,
+                                                          const uint64_t *nbits, int32_t *sym_out, int64_t B,
+                                                          int mapping) {
+    constexpr bool W = sizeof(E) == 8;
+    constexpr int S = NW - 1, NRMAX = 8;                      // streamer waves; <= 512 iterations per row
+    __shared__ uint64_t tot[2][64 * NRMAX];
+    __shared__ uint64_t smin[2][S];
+    __shared__ uint32_t sovf[2][S];
+    __shared__ int32_t serr;
+    const int lane = (int)lane_id(), w = wave_in_block();
+    const int64_t b = blockIdx.x;
+    const int nvec = (int)(V / VEC), nit = (nvec + 63) / 64, ngrp = (nit + 7) / 8;
+    if (threadIdx.x == 0) serr = states[b].err;
+
+    // streamer s (1..S): groups s-1, s-1+S, ... of step t into buffer t & 1
+    auto stream_row = [&](int64_t t) {
+        const E *row = pmf + t * step_stride + b * stream_stride;
+        const int buf = (int)(t & 1);
+        E mn = (E)~(E)0;
+        uint32_t ovf = 0;
+        for (int g = w - 1; g < ngrp; g += S) {
+            typename VecT<E, VEC>::type x[8];
+            const bool full = (g + 1) * 512 <= nvec;
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int vi = (g * 8 + u) * 64 + lane;
+                x[u] = full ? load_vec<E, VEC>(row, vi) : load_vec_or0<E, VEC>(row, vi, nvec);
+            }
+            uint64_t s8[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                uint64_t a = 0;
+#pragma unroll
+                for (int j = 0; j < VEC; j++) {
+                    const E e = vget<E, VEC>(x[u], j);
+                    a = add_ovf<W>(a, (uint64_t)e, ovf);
+                    const E m1 = e - 1;
+                    mn = m1 < mn ? m1 : mn;
+                }
+                s8[u] = a;
+            }
+            const uint64_t gt = wave_sum8_u64<W>(s8, ovf);     // lane l: iteration g*8 + (l & 7)
+            if (lane < 8 && g * 8 + lane < nit) tot[buf][g * 8 + lane] = gt;
+        }
+        uint64_t m64;
+        if constexpr (W) m64 = wave_min_u64(mn);
+        else m64 = wave_min_u32(mn);
+        const uint32_t o = (uint32_t)__any(ovf);
+        if (lane == 0) { smin[buf][w - 1] = m64; sovf[buf][w - 1] = o; }
+    };
+
+    DecState st;
+    const uint8_t *mybits = bits + b * stride;
+    uint64_t mynbits = 0;
+    if (w == 0) { st = states[b]; mynbits = nbits[b]; }
+    __syncthreads();
+    const bool dead = serr != 0;                              // an errored stream stays errored
+    if (w > 0 && !dead && nsteps > 0) stream_row(0);
+    __syncthreads();
+    for (int64_t t = 0; t < nsteps; t++) {
+        if (w > 0) {
+            if (!dead && t + 1 < nsteps) stream_row(t + 1);
+        } else {
+            int32_t *out = sym_out + t * B + b;
+            if (st.err) {
+                if (lane == 0) *out = -1;
+            } else {
+                const int buf = (int)(t & 1);
+                const E *row = pmf + t * step_stride + b * stream_stride;
+                uint64_t mine[NRMAX], incl[NRMAX];
+                u128 lsum = 0;
+                uint64_t base = 0, mn = ~0ull;
+                uint32_t ovf = 0;
+#pragma unroll
+                for (int i = 0; i < S; i++) {
+                    mn = smin[buf][i] < mn ? smin[buf][i] : mn;
+                    ovf |= sovf[buf][i];
+                }
+#pragma unroll
+                for (int r = 0; r < NRMAX; r++) {
+                    const int p = r * 64 + lane;
+                    mine[r] = (r * 64 < nit && p < nit) ? tot[buf][p] : 0;
+                    lsum += mine[r];
+                    incl[r] = base + wave_incl_scan_u64(mine[r]);
+                    base = readlane_u64(incl[r], 63);
+                }
+                const u128 acc128 = W ? wave_sum_u128(lsum) : (u128)base;
+                int err = 0;
+                if (ovf || (acc128 >> 64) || acc128 == 0) err = LAC_E_TABLE;
+                int64_t s = -1;
+                if (!err) {
+                    auto find_chunk = [&](uint64_t tgt, int64_t *cv0, int *G, uint64_t *cb) {
+#pragma unroll
+                        for (int r = 0; r < NRMAX; r++) {
+                            const uint64_t ex = incl[r] - mine[r];
+                            const bool hit = r * 64 + lane < nit && ex <= tgt && tgt < incl[r];
+                            const uint64_t mask = __ballot(hit);
+                            if (mask) {
+                                const int src = __ffsll((unsigned long long)mask) - 1;
+                                *cv0 = (int64_t)(r * 64 + src) * 64;
+                                *G = 1;
+                                *cb = readlane_u64(ex, src);
+                                return true;
+                            }
+                        }
+                        return false;
+                    };
+                    err = decode_symbol<E, VEC>(st, row, V, (uint64_t)acc128, mn + 1, prec, mapping, mybits, mynbits,
+                                                find_chunk, &s);
+                }
+                if (err) {
+                    st.err = err;
+                    st.err_step = st.nsym;
+                }
+                if (lane == 0) *out = err ? -1 : (int32_t)s;
+            }
+        }
+        __syncthreads();
+    }
+    if (w == 0 && lane == 0) states[b] = st;
+}
+
 // ---------------------------------------------------------- decode, stats path
 // Few streams: the per-step kernels above leave the chip idle (one stream's row
 // per step) and pay a launch per step.  The row statistics a decode step needs
@@ -1872,6 +2006,9 @@ struct lac_ctx {
     int dpath = LAC_PATH_AUTO;          // decode kernel path
     int64_t wave_decode_min_streams = 2048;   // measured: the stats path wins at 1024 streams
     int fine_decode = 1;                // one-wave decode: per-iteration totals (k_decode_wave_fine)
+    int64_t block_decode_min_streams = 4;     // AUTO below wave_decode_min_streams: block path from here
+                                              // (measured: stats path wins at 1 stream, block from 4)
+    int block_waves = 0;                // block path waves per stream (0 = by stream count)
     int mapping = LAC_MAP_CEIL;         // symbol_to_range flavour (lac_set_option)
     int term = LAC_TERM_FLUSH;          // stream termination flavour
     int cus = 256;                      // compute units (persistent grids)
@@ -2083,13 +2220,37 @@ static int decode_stats_path(lac_ctx *c, const E *pmf, int64_t step_stride, int6
     return LAC_OK;
 }
 
+template <typename E, int VEC>
+static int decode_block_launch(lac_ctx *c, const E *pmf, int64_t step_stride, int64_t stream_stride, int64_t steps,
+                               int32_t *out, hipStream_t st) {
+    ProfScope ps(c, KID_DECODE_WAVE, st);
+    const int nw = c->block_waves ? c->block_waves : (c->B >= 1024 ? 4 : c->B >= 512 ? 8 : 16);
+#define LAC_BLK(NW)                                                                                              \
+    k_decode_block<E, VEC, NW><<<(unsigned)c->B, 64 * NW, 0, st>>>(pmf, step_stride, stream_stride, steps, c->V,  \
+                                                                  c->prec, c->dec, c->dbits, c->dstride, c->dnbits, \
+                                                                  out, c->B, c->mapping)
+    if (nw == 4) LAC_BLK(4);
+    else if (nw == 8) LAC_BLK(8);
+    else LAC_BLK(16);
+#undef LAC_BLK
+    CHECK_LAUNCH();
+    return LAC_OK;
+}
+
 static int decode_dispatch(lac_ctx *c, const void *pmf, int64_t step_stride, int64_t stream_stride, int64_t steps,
                            int32_t *out, hipStream_t st) {
     const uintptr_t p = (uintptr_t)pmf;
     const bool wave = c->dpath == LAC_PATH_FUSED || (c->dpath == LAC_PATH_AUTO && c->B >= c->wave_decode_min_streams);
     const int vw = c->pmf_bits == 32 ? 4 : 2;
     const bool vec = (p % 16 == 0) && c->V % vw == 0 && step_stride % vw == 0 && stream_stride % vw == 0;
-    if (c->dpath == LAC_PATH_STATS || (c->dpath == LAC_PATH_AUTO && !wave)) {
+    const bool blockable = vec && (c->V / vw + 63) / 64 <= 512;        // per-iteration totals fit LDS
+    if (blockable && (c->dpath == LAC_PATH_BLOCK || (c->dpath == LAC_PATH_AUTO && !wave &&
+                                                     c->B >= c->block_decode_min_streams))) {
+        if (c->pmf_bits == 32)
+            return decode_block_launch<uint32_t, 4>(c, (const uint32_t *)pmf, step_stride, stream_stride, steps, out, st);
+        return decode_block_launch<uint64_t, 2>(c, (const uint64_t *)pmf, step_stride, stream_stride, steps, out, st);
+    }
+    if (c->dpath == LAC_PATH_STATS || c->dpath == LAC_PATH_BLOCK || (c->dpath == LAC_PATH_AUTO && !wave)) {
         if (c->pmf_bits == 32)
             return vec ? decode_stats_path<uint32_t, 4>(c, (const uint32_t *)pmf, step_stride, stream_stride, steps, out, st)
                        : decode_stats_path<uint32_t, 1>(c, (const uint32_t *)pmf, step_stride, stream_stride, steps, out, st);
@@ -2369,8 +2530,12 @@ int lac_set_option(lac_ctx *c, int option, int64_t value) {
         c->fused_min_streams = value;
         return LAC_OK;
     case LAC_OPT_DECODE_PATH:
-        if (value < LAC_PATH_AUTO || value > LAC_PATH_STATS) return fail(LAC_E_ARG, "bad decode path");
+        if (value < LAC_PATH_AUTO || value > LAC_PATH_BLOCK) return fail(LAC_E_ARG, "bad decode path");
         c->dpath = (int)value;
+        return LAC_OK;
+    case LAC_OPT_BLOCK_WAVES:
+        if (value != 0 && value != 4 && value != 8 && value != 16) return fail(LAC_E_ARG, "block waves: 0, 4, 8 or 16");
+        c->block_waves = (int)value;
         return LAC_OK;
     case LAC_OPT_DECODE_FINE:
         if (value != 0 && value != 1) return fail(LAC_E_ARG, "decode_fine must be 0 or 1");

@@ -52,7 +52,7 @@ def _gpu_encode(pmf_np, sym_np, prec, trace=False, path="auto", job=False):
     return c, pmf, data, n, tr
 
 
-DECODE_PATHS = ("split", "fused", "fused_chunk", "stats")
+DECODE_PATHS = ("split", "fused", "fused_chunk", "stats", "block")
 
 
 def _decode_both(c, dpmf):
@@ -432,8 +432,13 @@ def test_decode_wave_granularity(V, bits):
     assert rc == 0
     for b in range(4):
         assert data[b] == out[b, :(int(nb[b]) + 7) // 8].tobytes()
-    for path in ("fused", "fused_chunk", "split"):
+    for path in ("fused", "fused_chunk", "split", "block"):
         c.set_decode_path(path)
         c.decode_open()
         assert torch.equal(c.decode(pmf), sym), path
+    for nw in (4, 8, 16):
+        c.set_decode_path("block")
+        c.set_block_waves(nw)
+        c.decode_open()
+        assert torch.equal(c.decode(pmf), sym), nw
     c.close()

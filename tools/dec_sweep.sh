@@ -6,7 +6,8 @@ mkdir -p gpurun_out/dec
 for spec in "$@"; do
     set -- $spec
     B=$1; T=$2; P=$3; shift 3
-    out=gpurun_out/dec/B${B}_T${T}_${P}.json
+    tag=$(echo "$*" | tr -c 'A-Za-z0-9' '_')
+    out=gpurun_out/dec/B${B}_T${T}_${P}${tag:+_$tag}.json
     timeout -k 10 180 python3 bench.py --streams "$B" --tokens "$T" --decode-path "$P" --steps 3 --warmup 1 \
         --cpu-baseline off "$@" > "$out" 2> "${out%.json}.err"
     rc=$?
