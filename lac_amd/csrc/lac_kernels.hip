@@ -2346,7 +2346,8 @@ static int q1_stats_launch(lac_ctx *c, const Q1Args &a, hipStream_t st) {
 // in registers (measured on MI355X, c3 shape: encode bf16 (8,8,y) 0.75 ms vs
 // (8,8,n) 0.79 ms; decode (8,8,n) 70 M sym/s vs 46 M for the spilling (8,8,y)),
 // else tiles of (8, 8); LAC_OPT_Q1_SHAPE forces one for both directions (tuning;
-// identical results).
+// identical results).  Shapes 9-12 are one 16-wave block per CU: 9 = (16,16,n),
+// 10 = tiles of 9, 11 = (16,8,y), 12 = (16,8,n).
 static const int kQ1Shapes[][3] = {{1, 4, 0}, {2, 8, 0}, {4, 8, 0}, {8, 8, 0}, {8, 16, 0}, {8, 8, 1}, {8, 4, 1}};
 
 template <typename LT, bool DEC>
@@ -2356,14 +2357,20 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
     auto holds = [&](int i) { return nvec <= 64 * kQ1Shapes[i - 1][0] * kQ1Shapes[i - 1][1]; };
     if (sh == 0) {                     // decode: the prefetching (8,8) spills around the multi-sum
         static const int enc_order[] = {1, 2, 3, 6, 5}, dec_order[] = {1, 2, 3, 4, 5};
-        for (int i : DEC ? dec_order : enc_order)
+        for (int i : DEC ? dec_order : enc_order) {
+            // f32 encode rows of 4097..8192 vectors: one 16-wave block per CU with rolling
+            // prefetch, (16,8,y) = shape 11, before (8,16,n) (c3 f32: 1.33 vs 1.39 ms)
+            if (!DEC && sizeof(LT) == 4 && i == 5 && nvec <= 64 * 16 * 8) { sh = 11; break; }
             if (holds(i)) { sh = i; break; }
+        }
         if (sh == 0) sh = nvec <= 64 * 16 * 16 ? 9 : (DEC ? 10 : 8);   // measured at V = 128256 f32
     }
     // one 16-wave block per CU (LDS: one table copy), 16 vectors per thread: a bf16 row
     // of up to 131072 entries in registers (c4's V = 128256) -- one pass, no re-read
     if (sh == 9 && nvec <= 64 * 16 * 16) return q1_stats_launch<LT, 16, 16, DEC, false, false, 16>(c, a, st);
     if (sh == 10) return q1_stats_launch<LT, 16, 16, DEC, true, false, 16>(c, a, st);   // tiles of 16384
+    if (sh == 11 && nvec <= 64 * 16 * 8) return q1_stats_launch<LT, 16, 8, DEC, false, true, 16>(c, a, st);
+    if (sh == 12 && nvec <= 64 * 16 * 8) return q1_stats_launch<LT, 16, 8, DEC, false, false, 16>(c, a, st);
     if (sh == 8) return q1_stats_launch<LT, 8, 8, DEC, true, false>(c, a, st);      // tiles of 4096 vectors
     if (!holds(sh)) return fail(LAC_E_ARG, "q1 shape %d does not hold a row of %lld vectors", sh, (long long)nvec);
     switch (sh) {
@@ -2542,7 +2549,7 @@ int lac_set_option(lac_ctx *c, int option, int64_t value) {
         c->fine_decode = (int)value;
         return LAC_OK;
     case LAC_OPT_Q1_SHAPE:
-        if (value < 0 || value > 10) return fail(LAC_E_ARG, "bad q1 shape");
+        if (value < 0 || value > 12) return fail(LAC_E_ARG, "bad q1 shape");
         c->q1_shape = (int)value;
         return LAC_OK;
     case LAC_OPT_MAPPING:

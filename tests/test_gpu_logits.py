@@ -229,3 +229,33 @@ def test_incremental_logits_encode_mixes_with_pmf_steps():
     c2.finish()
     two, n2 = c2.to_bytes()
     assert (n1 == n2).all() and one == two
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f32"])
+def test_every_q1_shape_gives_the_same_bits(dtype):
+    """Every forced row-stats shape (8/16-wave blocks, tiles, rolling prefetch)
+    yields the AUTO shape's bytes and decodes; shapes that cannot hold the row
+    are refused with LAC_E_ARG."""
+    from lac_amd._lib import LacError
+    V, B, steps, prec = 32000, 12, 3, 48
+    x = _logits(777, steps, B, V, specials=True)
+    dl = _device_logits(x, dtype)
+    c = _coder(V, B, prec, cap=steps * (prec + 2) + 256)
+    pmf = c.quantize_logits(dl).cpu().numpy().view(np.uint32)
+    sym = torch.from_numpy(_sample(pmf, 5)).to(DEV)
+    c.encode_logits_job(dl, sym)
+    want, wn = c.to_bytes()
+    ran = 0
+    for sh in range(1, 13):
+        c.set_q1_shape(sh)
+        try:
+            c.encode_logits_job(dl, sym)
+        except LacError:
+            continue
+        got, gn = c.to_bytes()
+        assert got == want and (gn == wn).all(), sh
+        c.decode_open()
+        assert torch.equal(c.decode_logits(dl), sym), sh
+        ran += 1
+    assert ran >= 6
+    c.close()
