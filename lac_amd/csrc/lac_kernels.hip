@@ -1689,22 +1689,33 @@ __global__ __launch_bounds__(64 * NWB, 4) void k_q1_stats(const LT *__restrict__
     const int64_t stride = (int64_t)gridDim.x * NR;
     auto row_of = [&](int64_t r) { return lg + (t0 + r / B) * step_stride + (r % B) * stream_stride; };
     u32x4 x[R];
-    if (PF && !MULTI) {
+    if (PF) {                                                  // first tile of the block's first row
         const int64_t r0 = (int64_t)blockIdx.x * NR + g;
         q1_load_tile<LT, R>(x, r0 < rows ? row_of(r0) : lg, r0 < rows, 0, gt, NT, nvec);
     }
+    // one 16-B vector of a tile (neutral -inf beyond the row), for the rolling prefetches
+    auto ld_vec = [&](const LT *rw, bool ok, int tile, int j) {
+        const int vi = tile * NT * R + gt + NT * j;
+        return ok && vi < nvec ? ld16(rw, vi, LAC_Q1_NT) : neg_inf16(sizeof(LT));
+    };
     for (int64_t rb = (int64_t)blockIdx.x * NR; rb < rows; rb += stride) {
         const int64_t r = rb + g;
         const bool valid = r < rows;
         const LT *row = valid ? row_of(r) : lg;
         float mx = -INFINITY;
         if (MULTI) {
+            // PF: tile k+1's vector j loads into x[j] as soon as tile k's max has used it
             for (int tile = 0; tile < ntiles; tile++) {
-                q1_load_tile<LT, R>(x, row, valid, tile * NT * R, gt, NT, nvec);
+                if (!PF) q1_load_tile<LT, R>(x, row, valid, tile * NT * R, gt, NT, nvec);
 #pragma unroll
-                for (int j = 0; j < R; j++)
+                for (int j = 0; j < R; j++) {
 #pragma unroll
                     for (int e = 0; e < N; e++) mx = fmaxf(mx, logit_at<LT>(x[j], e));
+                    if (PF && tile + 1 < ntiles) {
+                        x[j] = ld_vec(row, valid, tile + 1, j);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                }
             }
         } else {
             if (!PF) q1_load_tile<LT, R>(x, row, valid, 0, gt, NT, nvec);   // PF: loaded during the last row
@@ -1780,7 +1791,7 @@ __global__ __launch_bounds__(64 * NWB, 4) void k_q1_stats(const LT *__restrict__
             for (int j = 0; j < R; j++) asm volatile("" : "+v"(x[j]));
         }
         for (int tile = ntiles - 1; tile >= 0; tile--) {
-            if (MULTI && tile != ntiles - 1) q1_load_tile<LT, R>(x, row, valid, tile * NT * R, gt, NT, nvec);
+            if (MULTI && !PF && tile != ntiles - 1) q1_load_tile<LT, R>(x, row, valid, tile * NT * R, gt, NT, nvec);
             uint32_t sv[R];
             auto take = [&](int j, uint32_t sl) {
                 const int vi = tile * NT * R + gt + NT * j;
@@ -1809,9 +1820,8 @@ __global__ __launch_bounds__(64 * NWB, 4) void k_q1_stats(const LT *__restrict__
             const bool nvalid = rn < rows;
             const LT *nrow = nvalid ? row_of(rn) : lg;
             auto roll = [&](int j) {
-                if (PF && !MULTI) {
-                    const int vi = gt + NT * j;
-                    x[j] = nvalid && vi < nvec ? ld16(nrow, vi, LAC_Q1_NT) : neg_inf16(sizeof(LT));
+                if (PF) {                                      // tiles walk down: tile - 1, then the next row's tile 0
+                    x[j] = (MULTI && tile > 0) ? ld_vec(row, valid, tile - 1, j) : ld_vec(nrow, nvalid, 0, j);
                     __builtin_amdgcn_sched_barrier(0);         // keep the load after vector j's use
                 }
             };
@@ -2347,7 +2357,9 @@ static int q1_stats_launch(lac_ctx *c, const Q1Args &a, hipStream_t st) {
 // (8,8,n) 0.79 ms; decode (8,8,n) 70 M sym/s vs 46 M for the spilling (8,8,y)),
 // else tiles of (8, 8); LAC_OPT_Q1_SHAPE forces one for both directions (tuning;
 // identical results).  Shapes 9-12 are one 16-wave block per CU: 9 = (16,16,n),
-// 10 = tiles of 9, 11 = (16,8,y), 12 = (16,8,n).
+// 10 = tiles of 9, 11 = (16,8,y), 12 = (16,8,n); 13 / 14 = tiles of (8,8) / (16,8)
+// with a rolling prefetch that walks the tiles (pass 1 up, pass 2 down, then the
+// next row's first tile).
 static const int kQ1Shapes[][3] = {{1, 4, 0}, {2, 8, 0}, {4, 8, 0}, {8, 8, 0}, {8, 16, 0}, {8, 8, 1}, {8, 4, 1}};
 
 template <typename LT, bool DEC>
@@ -2363,7 +2375,9 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
             if (!DEC && sizeof(LT) == 4 && i == 5 && nvec <= 64 * 16 * 8) { sh = 11; break; }
             if (holds(i)) { sh = i; break; }
         }
-        if (sh == 0) sh = nvec <= 64 * 16 * 16 ? 9 : (DEC ? 10 : 8);   // measured at V = 128256 f32
+        // measured at V = 128256 f32: encode tiles of (16,8) with the tile-rolling
+        // prefetch 1.98 ms vs 2.18 for tiles of (8,8) (shape 13, its (8,8) form: 2.20)
+        if (sh == 0) sh = nvec <= 64 * 16 * 16 ? 9 : (DEC ? 10 : (sizeof(LT) == 4 ? 14 : 8));
     }
     // one 16-wave block per CU (LDS: one table copy), 16 vectors per thread: a bf16 row
     // of up to 131072 entries in registers (c4's V = 128256) -- one pass, no re-read
@@ -2371,6 +2385,8 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
     if (sh == 10) return q1_stats_launch<LT, 16, 16, DEC, true, false, 16>(c, a, st);   // tiles of 16384
     if (sh == 11 && nvec <= 64 * 16 * 8) return q1_stats_launch<LT, 16, 8, DEC, false, true, 16>(c, a, st);
     if (sh == 12 && nvec <= 64 * 16 * 8) return q1_stats_launch<LT, 16, 8, DEC, false, false, 16>(c, a, st);
+    if (sh == 13) return q1_stats_launch<LT, 8, 8, DEC, true, true>(c, a, st);         // tiles of (8,8,y)
+    if (sh == 14) return q1_stats_launch<LT, 16, 8, DEC, true, true, 16>(c, a, st);    // tiles of (16,8,y)
     if (sh == 8) return q1_stats_launch<LT, 8, 8, DEC, true, false>(c, a, st);      // tiles of 4096 vectors
     if (!holds(sh)) return fail(LAC_E_ARG, "q1 shape %d does not hold a row of %lld vectors", sh, (long long)nvec);
     switch (sh) {
@@ -2549,7 +2565,7 @@ int lac_set_option(lac_ctx *c, int option, int64_t value) {
         c->fine_decode = (int)value;
         return LAC_OK;
     case LAC_OPT_Q1_SHAPE:
-        if (value < 0 || value > 12) return fail(LAC_E_ARG, "bad q1 shape");
+        if (value < 0 || value > 14) return fail(LAC_E_ARG, "bad q1 shape");
         c->q1_shape = (int)value;
         return LAC_OK;
     case LAC_OPT_MAPPING:
