@@ -2490,14 +2490,17 @@ int lac_open(int device, int prec, int64_t vocab, int64_t streams, int pmf_bits,
     e = e ? e : hipMalloc(&c->planeA, sizeof(uint64_t) * (c->cap_words * streams + 1));
     e = e ? e : hipMalloc(&c->planeC, sizeof(uint64_t) * (c->cap_words * streams + 1));
     e = e ? e : hipMalloc(&c->nbits, sizeof(uint64_t) * streams);
+    e = e ? e : hipMemset(c->nbits, 0, sizeof(uint64_t) * streams);
     if (e != hipSuccess) {
         lac_close(c);
-        return fail(LAC_E_HIP, "hipMalloc: %s", hipGetErrorString(e));
+        return fail(LAC_E_HIP, "device allocation: %s", hipGetErrorString(e));
     }
-    HIPCHK(hipMemset(c->nbits, 0, sizeof(uint64_t) * streams));
     int rc = lac_encode_reset(c, nullptr);
     if (rc) { lac_close(c); return rc; }
-    HIPCHK(hipDeviceSynchronize());
+    if ((e = hipDeviceSynchronize()) != hipSuccess) {
+        lac_close(c);
+        return fail(LAC_E_HIP, "hipDeviceSynchronize: %s", hipGetErrorString(e));
+    }
     *out = c;
     return LAC_OK;
 }
