@@ -135,6 +135,30 @@ __host__ __device__ inline void unfudged_range_inv(uint64_t lo, uint64_t hi, uin
     *b = div_floor_inv((u128)hi * w + (T - 1), T, inv);
 }
 
+// Row fractions for the sequential coder step of the split path.  For a row with
+// total T < 2^63 and a cumulative count 0 <= c <= T, f = floor(c * 2^63 / T)
+// (c == T gives exactly 2^63).  They depend only on the row, so k_encode computes
+// them for 64 steps at once (one lane per step) and the serial step is left with
+// multiplications.  kNoFrac marks rows with T >= 2^63: those divide as before.
+constexpr uint64_t kNoFrac = ~0ull;
+__host__ __device__ inline uint64_t row_frac(uint64_t c, uint64_t T) {
+    if (T == 0 || (T >> 63)) return kNoFrac;
+    if (c >= T) return 1ull << 63;
+    return div_floor((u128)c << 63, T);                   // c < T: quotient < 2^63
+}
+
+// floor(c*w/T) (ceil when `ceil`) from f = row_frac(c, T), for w <= 2^61 (prec
+// <= 61) and T < 2^63.  f*w/2^63 lies within w/2^63 <= 1/4 below c*w/T, so
+// q = floor(f*w/2^63) is the floor or one less; the remainder c*w - q*T is then
+// in [0, 2T), below 2^64, so wrapping 64-bit arithmetic computes it exactly.
+__host__ __device__ inline uint64_t frac_mul_div(uint64_t f, uint64_t c, uint64_t w, uint64_t T, bool ceil) {
+    const u128 p = (u128)f * w;
+    uint64_t q = (uint64_t)(p >> 63);
+    uint64_t r = c * w - q * T;
+    if (r >= T) { q += 1; r -= T; }
+    return q + (uint64_t)(ceil && r != 0);
+}
+
 // Floor mapping of Predictor.symbol_to_range (arith_code.py:69-70) and of
 // ACSampler's Region.map/step (arithmetic_coding.py:160-168):
 // a = floor(lo*w/T), b = floor(hi*w/T).  No fudge exists on these paths.

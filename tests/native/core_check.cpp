@@ -21,6 +21,12 @@ uint64_t cc_div_floor_inv(uint64_t nh, uint64_t nl, uint64_t d) {
     return div_floor_inv(((u128)nh << 64) | nl, d, 1.0 / (double)d);
 }
 
+// floor/ceil(c*w/T) through the row fraction (~0 for rows without one).
+uint64_t cc_frac_mul_div(uint64_t c, uint64_t w, uint64_t T, int ceil) {
+    const uint64_t f = row_frac(c, T);
+    return f == kNoFrac ? ~0ull : frac_mul_div(f, c, w, T, ceil != 0);
+}
+
 // pmf rows [steps][V] (eb = 4 or 8 bytes), one stream.  Returns status, writes
 // MSB-first bytes and the bit count.
 int cc_encode(const void *pmf, int eb, int64_t V, int64_t steps, int64_t step_stride, const int32_t *syms, int prec,
@@ -47,7 +53,11 @@ int cc_encode(const void *pmf, int eb, int64_t V, int64_t steps, int64_t step_st
         const uint64_t hi = (uint64_t)lo + at(s);
         const uint64_t w = (uint64_t)(h - l + 1);
         uint64_t a, b;
-        if (!is_fudged((uint64_t)T, w, minp)) {
+        const uint64_t flo = row_frac((uint64_t)lo, (uint64_t)T), fhi = row_frac(hi, (uint64_t)T);
+        if (!is_fudged((uint64_t)T, w, minp) && flo != kNoFrac) {         // k_encode's split-path form
+            a = frac_mul_div(flo, (uint64_t)lo, w, (uint64_t)T, true);
+            b = frac_mul_div(fhi, hi, w, (uint64_t)T, true);
+        } else if (!is_fudged((uint64_t)T, w, minp)) {
             unfudged_range((uint64_t)lo, hi, (uint64_t)T, w, &a, &b);
         } else {
             i128 xprev = (i128)((u128)1 << 127);

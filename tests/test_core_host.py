@@ -61,6 +61,24 @@ def test_div_floor_exact(core):
         assert core.cc_div_floor_inv(N >> 64, N & ((1 << 64) - 1), d) == q
 
 
+def test_frac_mul_div_exact(core):
+    """The split-path coder step's row-fraction division (lac_core.h frac_mul_div)
+    against exact big-int floor/ceil, including c == T, c == 0 and T near 2^63."""
+    core.cc_frac_mul_div.restype = C.c_uint64
+    core.cc_frac_mul_div.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_int]
+    rng = random.Random(11)
+    for i in range(40000):
+        T = rng.choice([1, 2, 3, rng.randrange(1, 1 << 20), rng.randrange(1, 1 << 40), rng.randrange(1, 1 << 63),
+                        (1 << 63) - rng.randrange(1, 1000)])
+        c = rng.choice([0, T, rng.randrange(0, T + 1), T - 1 if T > 1 else 0])
+        prec = rng.randint(2, 61)
+        w = rng.randrange((1 << (prec - 1)) + 1, (1 << prec) + 1)
+        ceil = i & 1
+        want = -(-(c * w) // T) if ceil else (c * w) // T
+        assert core.cc_frac_mul_div(c, w, T, ceil) == want, (c, w, T, ceil)
+    assert core.cc_frac_mul_div(5, 1 << 47, 1 << 63, 1) == (1 << 64) - 1     # T >= 2^63: no fraction
+
+
 def test_core_matches_golden(core):
     for kind in ("static", "perstep"):
         for c in load_golden("small_cases.json")[kind]:
