@@ -199,10 +199,10 @@ int lac_decode_steps(lac_ctx *ctx, const void *pmf_dev, int64_t step_stride, int
  * (include/lac_q1_table.h; DESIGN.md "logits path"), with
  * k = lac_q1_k(prec, vocab) = min(24, prec - 1 - ceil(log2 vocab)) so that
  * T <= 2^(prec-1) and no row is ever fudged.  It replaces the float64 numpy
- * quantiser of llama_compress.py:29-36 (whose output is platform-dependent)
+ * quantiser of llama_compress.py:24-30 (whose output is platform-dependent)
  * with a rule both the GPU and the C oracle reproduce bit for bit; the coder
  * semantics are those of CDFPredictor + A_to_bin / A_from_bin
- * (arith_code.py:17-92, 199-299).  Logit rows: bf16 (uint16 bit patterns) or
+ * (arith_code.py:76-110, 156-334).  Logit rows: bf16 (uint16 bit patterns) or
  * f32, 16-byte aligned, vocab and strides (in elements) multiples of 8 (bf16)
  * or 4 (f32).  Requires the CEIL mapping and FLUSH termination. */
 #define LAC_LOGITS_BF16 1

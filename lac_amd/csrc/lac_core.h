@@ -144,7 +144,10 @@ constexpr uint64_t kNoFrac = ~0ull;
 __host__ __device__ inline uint64_t row_frac(uint64_t c, uint64_t T) {
     if (T == 0 || (T >> 63)) return kNoFrac;
     if (c >= T) return 1ull << 63;
-    return div_floor((u128)c << 63, T);                   // c < T: quotient < 2^63
+    // c < T: quotient < 2^63.  A correctly rounded 1/T (IEEE divide, not the
+    // approximate v_rcp_f64 of recip()): with quotients this close to 2^63 the
+    // reciprocal's error sets how many correction steps div_floor_inv loops.
+    return div_floor_inv((u128)c << 63, T, 1.0 / (double)T);
 }
 
 // floor(c*w/T) (ceil when `ceil`) from f = row_frac(c, T), for w <= 2^61 (prec

@@ -14,10 +14,14 @@
 // lac_encode_finish runs k_finish (flush :193-202, carry resolution of bits()
 // :227-246, MSB-first byte packing of group_bits :336-347), one lane per stream.
 //
-// Decode (A_from_bin, :248-334) is k_decode_step: one workgroup per stream and
-// step.  Pass 1 streams the row into per-chunk sums held in LDS; wave 0 scans the
-// chunk sums, finds the chunk holding floor((x-l)*T/w), re-reads only that chunk
-// (L2-hot) and scans it to the symbol (val_to_symbol's bisect_right, :94-97).
+// At >= 2048 streams both directions are one launch per job with one wave per
+// stream (k_encode_fused, k_decode_wave_fine); fewer streams take the split
+// encode above and the block / stats decode paths.
+//
+// Decode (A_from_bin, :248-334): per step the row is streamed into totals, the
+// search finds the chunk holding floor((x-l)*T/w), only that chunk is re-read
+// and scanned to the symbol (val_to_symbol's bisect_right, :94-97), and the
+// value window advances by the renormalisation (emit_bit, :284-291).
 #include <hip/hip_runtime.h>
 
 #include <stdarg.h>
@@ -360,17 +364,31 @@ __device__ inline void div_pair(uint64_t n0, uint64_t n1, uint64_t m, uint64_t a
     *q1 = readlane_u64(q, 1);
 }
 
+// The same pair through precomputed row fractions (lac_core.h frac_mul_div):
+// three 64-bit multiplies and one correction instead of two quotient estimates.
+__device__ inline void frac_pair(uint64_t f0, uint64_t f1, uint64_t c0, uint64_t c1, uint64_t w, uint64_t T,
+                                 bool ceil, uint64_t *q0, uint64_t *q1) {
+    const bool first = lane_id() == 0;
+    const uint64_t q = frac_mul_div(first ? f0 : f1, first ? c0 : c1, w, T, ceil);
+    *q0 = readlane_u64(q, 0);
+    *q1 = readlane_u64(q, 1);
+}
+
 template <typename E>
 __device__ inline bool coder_step(EncState &st, int64_t &l, int64_t &h, uint64_t lo, uint64_t hi, uint64_t T,
                                   uint64_t minp, int64_t s, const E *row, int64_t V, int prec, uint64_t *pa,
                                   uint64_t *pc, uint64_t cap_words, uint64_t *trace_slot, int lane, int mapping,
-                                  double inv_T = 0.0, bool allow_fudge = true) {
+                                  double inv_T = 0.0, bool allow_fudge = true, uint64_t flo = kNoFrac,
+                                  uint64_t fhi = kNoFrac) {
     if (s < 0 || s >= V) { st.err = LAC_E_SYMBOL_RANGE; return false; }   // arith_code.py:100-101
     if (T == 0) { st.err = LAC_E_TABLE; return false; }
     const uint64_t w = (uint64_t)(h - l + 1);
     uint64_t a, bb;
     if (mapping == LAC_MAP_FLOOR || !is_fudged(T, w, minp)) {  // floor: Predictor/ACSampler; else ceil
-        div_pair(lo, hi, w, mapping == LAC_MAP_FLOOR ? 0 : T - 1, T, inv_T != 0.0 ? inv_T : recip(T), &a, &bb);
+        if (flo != kNoFrac)
+            frac_pair(flo, fhi, lo, hi, w, T, mapping != LAC_MAP_FLOOR, &a, &bb);
+        else
+            div_pair(lo, hi, w, mapping == LAC_MAP_FLOOR ? 0 : T - 1, T, inv_T != 0.0 ? inv_T : recip(T), &a, &bb);
     } else {                                                  // CDFPredictor.fudged_dist
         if (!allow_fudge) { st.err = LAC_E_TABLE; return false; }
         const i128 xprev = s > 0 ? wave_xmax_prefix<E>(row, s, w, T) : kI128Min;
@@ -518,16 +536,20 @@ __global__ __launch_bounds__(256) void k_encode(const RowStats *__restrict__ sta
             my = stats[(g0 + lane) * B + b];
             mys = sym[(t0 + g0 + lane) * B + b];
         }
+        // the 64 steps' row fractions at once, one lane each: off the serial chain
+        const uint64_t flo = lane < n ? row_frac(my.lo, my.tot) : kNoFrac;
+        const uint64_t fhi = lane < n ? row_frac(my.hi, my.tot) : kNoFrac;
         for (int i = 0; i < n; i++) {
             const uint64_t lo = readlane_u64(my.lo, i), hi = readlane_u64(my.hi, i);
             const uint64_t T = readlane_u64(my.tot, i), minp = readlane_u64(my.minp, i);
             const uint64_t invb = readlane_u64(__builtin_bit_cast(uint64_t, my.inv_tot), i);
+            const uint64_t fl = readlane_u64(flo, i), fh = readlane_u64(fhi, i);
             const int64_t s = __builtin_amdgcn_readlane(mys, i);
             const int64_t t = t0 + g0 + i;
             const E *row = pmf + t * step_stride + b * stream_stride;
             if (!coder_step<E>(st, l, h, lo, hi, T, minp, s, row, V, prec, pa, pc, cap_words,
                                trace ? trace + 2 * (t * B + b) : nullptr, lane, mapping,
-                               __builtin_bit_cast(double, invb), allow_fudge)) {
+                               __builtin_bit_cast(double, invb), allow_fudge, fl, fh)) {
                 ok = false;
                 break;
             }
@@ -618,6 +640,34 @@ __device__ inline uint64_t read_bits(const uint8_t *bits, uint64_t nbits, uint64
     return v;
 }
 
+// The two stream words the next renormalisation can read (bits pos .. pos+127),
+// loaded at the top of a decode step so their latency hides under the search;
+// window_bits then equals read_bits(bits, nbits, pos, k) for any k <= 64.
+// Indices are clamped into the stream (an empty stream reads a zero word), so
+// the loads are unconditional.
+struct BitWin {
+    uint64_t w0, w1;
+};
+__device__ const uint64_t g_zero_words[1] = {0};
+__device__ inline BitWin bit_window(const uint8_t *bits, uint64_t nbits, uint64_t pos) {
+    const uint64_t nw = (nbits + 63) >> 6, wi = pos >> 6;
+    const uint64_t *wp = nw ? reinterpret_cast<const uint64_t *>(bits) : g_zero_words;
+    const uint64_t last = nw ? nw - 1 : 0;
+    return BitWin{wp[wi < last ? wi : last], wp[wi + 1 < last ? wi + 1 : last]};
+}
+__device__ inline uint64_t window_bits(const BitWin &win, uint64_t nbits, uint64_t pos, int k) {
+    if (k <= 0 || pos >= nbits) return 0;
+    const int off = (int)(pos & 63);
+    uint64_t v = bswap64(win.w0) << off;
+    if (off && ((pos >> 6) + 1) * 64 < nbits) v |= bswap64(win.w1) >> (64 - off);
+    v >>= (64 - k);
+    if (pos + (uint64_t)k > nbits) {
+        const int drop = (int)(pos + (uint64_t)k - nbits);
+        v = (v >> drop) << drop;
+    }
+    return v;
+}
+
 __global__ void k_dec_init(DecState *states, int64_t B, int prec, const uint8_t *bits, uint64_t stride,
                            const uint64_t *nbits) {
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -638,44 +688,53 @@ __global__ void k_dec_init(DecState *states, int64_t B, int prec, const uint8_t 
 // ---- decode building blocks (one wave; all values wave-uniform unless noted)
 
 // Re-scan one chunk (vectors cv0 + 64*g + lane, g < G) from cumulative base cb:
-// count of entries with c_i <= tgt, and the bracketing c_{s-1}, c_s.
+// count of entries with c_i <= tgt, and the bracketing c_{s-1}, c_s.  The CDF is
+// nondecreasing along the chunk, so the entries <= tgt are a prefix and the
+// first lane whose last entry exceeds tgt holds the crossing: one ballot per
+// vector finds it and that lane's own count and bracket are read out -- no
+// wave-wide reductions on the serial path.  Needs cb <= tgt < cb + the chunk's
+// total (find_chunk guarantees it; zero-filled vectors past the row end then
+// cannot be the first to exceed); returns false otherwise.
 template <typename E, int VEC>
-__device__ inline void scan_chunk(const E *row, int64_t nvec, int64_t cv0, int G, uint64_t cb, uint64_t tgt,
+__device__ inline bool scan_chunk(const E *row, int64_t nvec, int64_t cv0, int G, uint64_t cb, uint64_t tgt,
                                   uint64_t *cnt_out, uint64_t *lo_out, uint64_t *hi_out) {
-    const int lane = (int)lane_id();
-    uint64_t lo_c = cb, hi_c = ~0ull, cnt = 0;
     constexpr int PF = 4;                                     // loads in flight: the scan is latency-bound
-    bool done = false;
-    for (int g0 = 0; g0 < G && !done; g0 += PF) {
+    for (int g0 = 0; g0 < G; g0 += PF) {
         typename VecT<E, VEC>::type xs[PF];
 #pragma unroll
         for (int u = 0; u < PF; u++) {
-            const int64_t vi = cv0 + (int64_t)(g0 + u) * 64 + lane;
+            const int64_t vi = cv0 + (int64_t)(g0 + u) * 64 + (int64_t)lane_id();
             xs[u] = load_vec_or0<E, VEC>(row, g0 + u < G ? vi : nvec, nvec);
         }
 #pragma unroll
         for (int u = 0; u < PF; u++) {
             if (g0 + u >= G) break;
-            const int64_t vi = cv0 + (int64_t)(g0 + u) * 64 + lane;
             uint64_t loc[VEC], ls = 0;
 #pragma unroll
             for (int j = 0; j < VEC; j++) { ls += (uint64_t)vget<E, VEC>(xs[u], j); loc[j] = ls; }
             const uint64_t in = wave_incl_scan_u64(ls);
-            const uint64_t ex = cb + in - ls;
+            const uint64_t ex = cb + in - ls;                 // c just before this lane's entries
+            const uint64_t mask = __ballot(ex + ls > tgt);
+            if (mask) {
+                const int L = __ffsll((unsigned long long)mask) - 1;
+                uint64_t k = 0, lo = ex, hi = ~0ull;
 #pragma unroll
-            for (int j = 0; j < VEC; j++) {
-                const uint64_t ce = ex + loc[j];
-                const bool valid = vi < nvec;
-                if (valid && ce <= tgt) { cnt++; lo_c = ce > lo_c ? ce : lo_c; }
-                if (valid && ce > tgt) hi_c = ce < hi_c ? ce : hi_c;
+                for (int j = 0; j < VEC; j++) {
+                    const uint64_t ce = ex + loc[j];
+                    const bool le = ce <= tgt;
+                    k += le ? 1 : 0;
+                    lo = le ? ce : lo;
+                    hi = (!le && ce < hi) ? ce : hi;
+                }
+                *cnt_out = (uint64_t)((g0 + u) * 64 + L) * VEC + readlane_u64(k, L);
+                *lo_out = readlane_u64(lo, L);
+                *hi_out = readlane_u64(hi, L);
+                return true;
             }
             cb += readlane_u64(in, 63);
-            if (cb > tgt) { done = true; break; }             // later entries all exceed tgt
         }
     }
-    *cnt_out = wave_sum_u64(cnt);
-    *lo_out = wave_max_u64(lo_c);
-    *hi_out = wave_min_u64(hi_c);
+    return false;
 }
 
 // Fudged val_to_symbol + symbol_to_range (fudged_dist closed form).  f is
@@ -735,7 +794,7 @@ __device__ inline int decode_fudged(const E *row, int64_t V, uint64_t w, uint64_
 
 // Narrow to symbol s and renormalise, pulling k fresh bits into x
 // (emit_symbol + emit_bit, arith_code.py:274-291, value form).
-__device__ inline int decode_advance(DecState &st, uint64_t a, uint64_t bb, const uint8_t *bits, uint64_t nbits,
+__device__ inline int decode_advance(DecState &st, uint64_t a, uint64_t bb, const BitWin &win, uint64_t nbits,
                                      int prec) {
     const int64_t l = st.l, x = st.x;
     if (!((l + (int64_t)a) <= x && x <= l + (int64_t)bb - 1)) return LAC_E_DECODE_RANGE;  // :277-278
@@ -746,7 +805,7 @@ __device__ inline int decode_advance(DecState &st, uint64_t a, uint64_t bb, cons
     int64_t nx = x;
     if (k > 0) {
         const int sh = prec - k;
-        nx = (int64_t)((((uint64_t)x - (Ev << sh)) << k) | read_bits(bits, nbits, st.pos, k));
+        nx = (int64_t)((((uint64_t)x - (Ev << sh)) << k) | window_bits(win, nbits, st.pos, k));
         st.pos += (uint64_t)k;
     }
     st.l = nl;
@@ -762,6 +821,7 @@ template <typename E, int VEC, typename FindChunk>
 __device__ inline int decode_symbol(DecState &st, const E *row, int64_t V, uint64_t T, uint64_t minp, int prec,
                                     int mapping, const uint8_t *bits, uint64_t nbits, FindChunk find_chunk,
                                     int64_t *s_out) {
+    const BitWin win = bit_window(bits, nbits, st.pos);       // in flight during the search
     const int64_t l = st.l, h = st.h, x = st.x;
     if (x < l || x > h) return LAC_E_DECODE_RANGE;            // corrupted state / bits
     const uint64_t w = (uint64_t)(h - l + 1), v = (uint64_t)(x - l);
@@ -783,7 +843,7 @@ __device__ inline int decode_symbol(DecState &st, const E *row, int64_t V, uint6
         uint64_t cb;
         if (!find_chunk(tgt, &cv0, &G, &cb)) return LAC_E_DECODE_RANGE;
         uint64_t cnt, lo_c, hi_c;
-        scan_chunk<E, VEC>(row, V / VEC, cv0, G, cb, tgt, &cnt, &lo_c, &hi_c);
+        if (!scan_chunk<E, VEC>(row, V / VEC, cv0, G, cb, tgt, &cnt, &lo_c, &hi_c)) return LAC_E_DECODE_RANGE;
         s = cv0 * VEC + (int64_t)cnt;
         div_pair(lo_c, hi_c, w, mapping == LAC_MAP_FLOOR ? 0 : T - 1, T, recip(T), &a, &bb);
         det = vhi < w && thi < hi_c;                          // bisect_right(cdf, t_hi) == s
@@ -795,7 +855,7 @@ __device__ inline int decode_symbol(DecState &st, const E *row, int64_t V, uint6
     if (st.det && det) st.ndet++;
     else st.det = 0;
     *s_out = s;
-    return decode_advance(st, a, bb, bits, nbits, prec);
+    return decode_advance(st, a, bb, win, nbits, prec);
 }
 
 // One decode step for every stream, NW waves per stream (small stream counts:
@@ -1314,12 +1374,13 @@ struct DecRowMeta {
     uint64_t minp;
 };
 
+// Chunks of CI = ceil(iterations / 64) 64-vector iterations, the finest that
+// keeps <= 64 totals (V = 32000 u32: 63 chunks of 2 iterations, so the per-step
+// re-read is 2 vectors per lane, one round of loads).
 template <typename E, int VEC>
 __device__ inline void dec_chunk_layout(int64_t V, int64_t *CI, int64_t *nch) {
-    constexpr int U = 8;
     const int64_t nvec = V / VEC, nit = (nvec + 63) / 64;
-    int64_t ci = (nit + 63) / 64;
-    ci = ((ci + U - 1) / U) * U;
+    const int64_t ci = nit ? (nit + 63) / 64 : 1;
     *CI = ci;
     *nch = (nit + ci - 1) / ci;
 }
@@ -1333,52 +1394,41 @@ __global__ __launch_bounds__(256) void k_dec_stats(const E *__restrict__ pmf, in
     const int64_t r = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
     if (r >= rows) return;
     const E *row = pmf + (t0 + r / B) * step_stride + (r % B) * stream_stride;
-    constexpr int U = 8;
-    const int64_t nvec = V / VEC;
+    constexpr bool W = sizeof(E) == 8;
+    const int64_t nvec = V / VEC, nit = (nvec + 63) / 64, ngrp = (nit + 7) / 8;
     int64_t CI, nch;
     dec_chunk_layout<E, VEC>(V, &CI, &nch);
     uint64_t mine = 0;
     E mn = (E)~(E)0;
     uint32_t ovf = 0;
-    for (int64_t c = 0; c < nch; c++) {
-        uint64_t acc = 0;
-        for (int64_t g0 = 0; g0 < CI; g0 += U) {
-            typename VecT<E, VEC>::type x[U];
+    // groups of 8 iterations (8 loads in flight per lane), their 8 totals from one
+    // butterfly, each added into the lane of its chunk (chunk = iteration / CI)
+    int64_t chunk = 0, left = CI;
+    for (int64_t g = 0; g < ngrp; g++) {
+        typename VecT<E, VEC>::type x[8];
 #pragma unroll
-            for (int u = 0; u < U; u++) {
-                const int64_t vi = (c * CI + g0 + u) * 64 + lane;
-                x[u] = load_vec_or0<E, VEC>(row, vi, nvec);
+        for (int u = 0; u < 8; u++) x[u] = load_vec_or0<E, VEC>(row, (g * 8 + u) * 64 + lane, nvec);
+        uint64_t s8[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            uint64_t a = 0;
+#pragma unroll
+            for (int j = 0; j < VEC; j++) {
+                const E e = vget<E, VEC>(x[u], j);
+                a = add_ovf<W>(a, (uint64_t)e, ovf);
+                const E m1 = e - 1;
+                mn = m1 < mn ? m1 : mn;
             }
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-#pragma unroll
-                for (int j = 0; j < VEC; j++) {
-                    const E e = vget<E, VEC>(x[u], j);
-                    if constexpr (sizeof(E) == 8) {
-                        const uint64_t n2 = acc + e;
-                        ovf |= n2 < acc;
-                        acc = n2;
-                    } else {
-                        acc += e;
-                    }
-                    const E m1 = e - 1;
-                    mn = m1 < (E)mn ? m1 : (E)mn;
-                }
-            }
+            s8[u] = a;
         }
-        uint64_t tsum = acc;
-        if constexpr (sizeof(E) == 8) {
+        const uint64_t tot = wave_sum8_u64<W>(s8, ovf);       // lane l: iteration g*8 + (l & 7)
 #pragma unroll
-            for (int m = 32; m >= 1; m >>= 1) {
-                const uint64_t o = shfl_xor_u64(tsum, m);
-                const uint64_t n2 = tsum + o;
-                ovf |= n2 < tsum;
-                tsum = n2;
-            }
-        } else {
-            tsum = wave_sum_u64(tsum);
+        for (int u = 0; u < 8; u++) {
+            if (g * 8 + u >= nit) break;
+            const uint64_t v = readlane_u64(tot, u);
+            if (lane == chunk) mine = add_ovf<W>(mine, v, ovf);
+            if (--left == 0) { chunk++; left = CI; }
         }
-        if (lane == c) mine = tsum;
     }
     uint64_t minp;
     if constexpr (sizeof(E) == 8) minp = wave_min_u64(mn) + 1;
@@ -1898,6 +1948,7 @@ __global__ LAC_DEC_BOUNDS void k_q1_decode(const LT *__restrict__ lg, int64_t st
             continue;
         }
         const LT *row = lg + t * step_stride + b * stream_stride;
+        const BitWin win = bit_window(mybits, mynbits, st.pos);    // in flight during the search
         const float c = q1_c(mrow[r]);
         const uint64_t T = wave_sum_u64(mine);
         const uint64_t incl = wave_incl_scan_u64(mine);
@@ -1955,7 +2006,7 @@ __global__ LAC_DEC_BOUNDS void k_q1_decode(const LT *__restrict__ lg, int64_t st
                 const bool det = vhi < w && thi < hi_c;
                 if (st.det && det) st.ndet++;
                 else st.det = 0;
-                err = decode_advance(st, a, bb, mybits, mynbits, prec);
+                err = decode_advance(st, a, bb, win, mynbits, prec);
             }
         }
         if (err) {

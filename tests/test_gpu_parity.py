@@ -432,7 +432,7 @@ def test_decode_wave_granularity(V, bits):
     assert rc == 0
     for b in range(4):
         assert data[b] == out[b, :(int(nb[b]) + 7) // 8].tobytes()
-    for path in ("fused", "fused_chunk", "split", "block"):
+    for path in ("fused", "fused_chunk", "split", "block", "stats"):
         c.set_decode_path(path)
         c.decode_open()
         assert torch.equal(c.decode(pmf), sym), path
