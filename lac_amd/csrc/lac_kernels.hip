@@ -2067,8 +2067,10 @@ struct lac_ctx {
     int dpath = LAC_PATH_AUTO;          // decode kernel path
     int64_t wave_decode_min_streams = 2048;   // measured: the stats path wins at 1024 streams
     int fine_decode = 1;                // one-wave decode: per-iteration totals (k_decode_wave_fine)
-    int64_t block_decode_min_streams = 4;     // AUTO below wave_decode_min_streams: block path from here
-                                              // (measured: stats path wins at 1 stream, block from 4)
+    int64_t block_decode_min_streams = 1536;  // AUTO below wave_decode_min_streams: block path from here
+                                              // (measured after the serial-step rework: the stats path wins
+                                              // at 4-1024 streams except 256, block at 1536;
+                                              // profiles/r01/decode_paths_v2/)
     int block_waves = 0;                // block path waves per stream (0 = by stream count)
     int mapping = LAC_MAP_CEIL;         // symbol_to_range flavour (lac_set_option)
     int term = LAC_TERM_FLUSH;          // stream termination flavour
