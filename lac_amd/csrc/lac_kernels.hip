@@ -1973,40 +1973,54 @@ __global__ LAC_DEC_BOUNDS void k_q1_decode(const LT *__restrict__ lg, int64_t st
                 const int src = __ffsll((unsigned long long)mask) - 1;
                 uint64_t cb = readlane_u64(ex, src);
                 const int64_t cv0 = (int64_t)src * G * 64;
+                // the crossing lane by ballot, as scan_chunk (entries <= tgt are a prefix)
                 uint64_t lo_c = cb, hi_c = ~0ull, cnt = 0;
-                for (int64_t g = 0; g < G; g++) {
+                bool found = false;
+                for (int64_t g = 0; g < G && !found; g++) {
                     const int64_t vi = cv0 + g * 64 + lane;
-                    const u32x4 xv = vi < nvec ? ld16(row, vi, false) : u32x4{0, 0, 0, 0};
+                    const bool valid = vi < nvec;
+                    const u32x4 xv = ld16(row, valid ? vi : nvec - 1, false);
                     uint64_t loc[N], ls = 0;
 #pragma unroll
                     for (int j = 0; j < N; j++) {
-                        ls += vi < nvec ? q1_val(logit_at<LT>(xv, j), c, tab) : 0u;
+                        ls += valid ? q1_val(logit_at<LT>(xv, j), c, tab) : 0u;
                         loc[j] = ls;
                     }
                     const uint64_t in = wave_incl_scan_u64(ls);
                     const uint64_t exb = cb + in - ls;
+                    const uint64_t m = __ballot(exb + ls > tgt);
+                    if (m) {
+                        const int L = __ffsll((unsigned long long)m) - 1;
+                        uint64_t k = 0, lo = exb, hi = ~0ull;
 #pragma unroll
-                    for (int j = 0; j < N; j++) {
-                        const uint64_t ce = exb + loc[j];
-                        if (vi < nvec && ce <= tgt) { cnt++; lo_c = ce > lo_c ? ce : lo_c; }
-                        if (vi < nvec && ce > tgt) hi_c = ce < hi_c ? ce : hi_c;
+                        for (int j = 0; j < N; j++) {
+                            const uint64_t ce = exb + loc[j];
+                            const bool le = ce <= tgt;
+                            k += le ? 1 : 0;
+                            lo = le ? ce : lo;
+                            hi = (!le && ce < hi) ? ce : hi;
+                        }
+                        cnt = (uint64_t)(g * 64 + L) * N + readlane_u64(k, L);
+                        lo_c = readlane_u64(lo, L);
+                        hi_c = readlane_u64(hi, L);
+                        found = true;
                     }
                     cb += readlane_u64(in, 63);
-                    if (cb > tgt) break;
                 }
-                cnt = wave_sum_u64(cnt);
-                lo_c = wave_max_u64(lo_c);
-                hi_c = wave_min_u64(hi_c);
-                s = cv0 * N + (int64_t)cnt;
-                uint64_t a, bb;
-                div_pair(lo_c, hi_c, w, T - 1, T, recip(T), &a, &bb);
-                const uint64_t past = st.pos > mynbits ? st.pos - mynbits : 0;
-                const int u = past < (uint64_t)prec ? (int)past : prec;
-                const uint64_t vhi = v + ((1ull << u) - 1);
-                const bool det = vhi < w && thi < hi_c;
-                if (st.det && det) st.ndet++;
-                else st.det = 0;
-                err = decode_advance(st, a, bb, win, mynbits, prec);
+                if (!found) {
+                    err = LAC_E_DECODE_RANGE;                  // corrupt state: tgt outside the chunk
+                } else {
+                    s = cv0 * N + (int64_t)cnt;
+                    uint64_t a, bb;
+                    div_pair(lo_c, hi_c, w, T - 1, T, recip(T), &a, &bb);
+                    const uint64_t past = st.pos > mynbits ? st.pos - mynbits : 0;
+                    const int u = past < (uint64_t)prec ? (int)past : prec;
+                    const uint64_t vhi = v + ((1ull << u) - 1);
+                    const bool det = vhi < w && thi < hi_c;
+                    if (st.det && det) st.ndet++;
+                    else st.det = 0;
+                    err = decode_advance(st, a, bb, win, mynbits, prec);
+                }
             }
         }
         if (err) {
