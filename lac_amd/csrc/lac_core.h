@@ -74,7 +74,8 @@ __host__ __device__ inline double recip(uint64_t d) {
 #endif
 }
 
-// floor(N / d) for d > 0 when the quotient is known to be < 2^63.  Two rounds of
+// floor(N / d) for d > 0 when the quotient is known to be < 2^64 (the decode target
+// floor(v*T/w) reaches 2^64 - 1 for u64 tables with totals near 2^64).  Two rounds of
 // float64 quotient estimates plus an exact 128-bit remainder correction: no
 // shift-subtract loop (the generic __int128 division is ~5k cycles on gfx950).
 __host__ __device__ inline uint64_t div_floor(u128 N, uint64_t d) {
@@ -85,7 +86,7 @@ __host__ __device__ inline uint64_t div_floor(u128 N, uint64_t d) {
     const double dd = (double)d;
     const double dn = (double)(uint64_t)(N >> 64) * two64 + (double)(uint64_t)N;
     double qd = dn / dd;
-    uint64_t q = qd >= 9.2e18 ? (uint64_t)9.2e18 : (uint64_t)qd;
+    uint64_t q = qd >= 1.8e19 ? (uint64_t)1.8e19 : (uint64_t)qd;
     i128 r = (i128)(N - (u128)q * d);
     const double rd = (double)(int64_t)(r >> 64) * two64 + (double)(uint64_t)r;
     const int64_t adj = (int64_t)(rd / dd);
@@ -106,7 +107,7 @@ __host__ __device__ inline uint64_t div_floor_inv(u128 N, uint64_t d, double inv
     const double two64 = 18446744073709551616.0;
     const double dn = (double)(uint64_t)(N >> 64) * two64 + (double)(uint64_t)N;
     double qd = dn * inv;
-    uint64_t q = qd >= 9.2e18 ? (uint64_t)9.2e18 : (uint64_t)qd;
+    uint64_t q = qd >= 1.8e19 ? (uint64_t)1.8e19 : (uint64_t)qd;
     i128 r = (i128)(N - (u128)q * d);
     const double rd = (double)(int64_t)(r >> 64) * two64 + (double)(uint64_t)r;
     const int64_t adj = (int64_t)(rd * inv);

@@ -52,7 +52,7 @@ def test_div_floor_exact(core):
     rng = random.Random(5)
     for _ in range(20000):
         d = rng.choice([1, 2, 3, rng.randrange(1, 1 << 20), rng.randrange(1, 1 << 47), rng.randrange(1, 1 << 64)])
-        q = rng.randrange(0, 1 << rng.choice([8, 32, 47, 61, 62]))
+        q = rng.randrange(0, 1 << rng.choice([8, 32, 47, 61, 62, 63, 64]))
         r = rng.randrange(0, d)
         N = q * d + r
         if N >> 128:

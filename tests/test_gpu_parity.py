@@ -394,6 +394,32 @@ def test_edge_u64_total_overflow_is_an_error():
     assert err.tolist() == [-5, 0]
 
 
+@pytest.mark.parametrize("path", ["split", "fused"])
+def test_edge_u64_totals_near_2_63(path):
+    """u64 rows whose totals straddle 2^63: below it the split path's coder step
+    divides through row fractions, from it on (no fraction fits) it falls back to
+    the quotient estimates -- both bit-exact vs the oracle, at prec 61 where w
+    reaches 2^61, with zero entries and unfudged / fudged rows mixed."""
+    from oracle import oracle as coracle
+    rng = np.random.default_rng(63)
+    V, B, steps, prec = 6, 12, 40, 61
+    pmf = np.zeros((steps, B, V), dtype=np.uint64)
+    for b in range(B):
+        hi = (1 << 63) // V * (40 + b - 3) // 40                # totals just below / above 2^63
+        pmf[:, b, :] = rng.integers(hi // 8 * 7, hi, size=(steps, V), dtype=np.uint64)
+    pmf[::7, :, 2] = 0                                          # zero-probability entries
+    sym = rng.integers(0, V, size=(steps, B)).astype(np.int32)
+    sym[::7][sym[::7] == 2] = 3
+    tot = pmf.astype(object).sum(axis=2)
+    assert (tot < (1 << 64)).all() and (tot >= (1 << 63)).any() and (tot < (1 << 63)).any()
+    c, dpmf, data, n, tr = _gpu_encode(pmf, sym, prec, path=path)
+    out, nb, status, rc = coracle.encode_batch(pmf, sym, prec, nthreads=4)
+    assert rc == 0
+    for b in range(B):
+        assert int(n[b]) == int(nb[b]) and data[b] == out[b, :(int(nb[b]) + 7) // 8].tobytes(), b
+    assert (_decode_both(c, dpmf) == sym).all()
+
+
 def test_stats_decode_spans_step_chunks():
     """600 streams x 150 steps: the stats-path decode (AUTO below 2048 streams)
     runs in 64-step chunks; symbols and determined counts match the other paths."""
