@@ -408,6 +408,7 @@ def test_edge_u64_totals_near_2_63(path):
         hi = (1 << 63) // V * (40 + b - 3) // 40                # totals just below / above 2^63
         pmf[:, b, :] = rng.integers(hi // 8 * 7, hi, size=(steps, V), dtype=np.uint64)
     pmf[::7, :, 2] = 0                                          # zero-probability entries
+    pmf[::3, ::3, 5] = 1                                        # minp 1: those rows take fudged_dist
     sym = rng.integers(0, V, size=(steps, B)).astype(np.int32)
     sym[::7][sym[::7] == 2] = 3
     tot = pmf.astype(object).sum(axis=2)
