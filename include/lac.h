@@ -70,7 +70,7 @@ enum {                       /* lac_set_option */
     LAC_OPT_DECODE_PATH = 5,       /* LAC_PATH_*: SPLIT = one 4-wave workgroup per stream and step,
                                       FUSED = one wave per stream, all steps of a call in one launch;
                                       STATS, BLOCK = see LAC_PATH_STATS / LAC_PATH_BLOCK;
-                                      AUTO = FUSED from 2048 streams, BLOCK from 1536, else STATS */
+                                      AUTO = FUSED from 2048 streams, BLOCK at 160-256 and from 1536, else STATS */
     LAC_OPT_Q1_SHAPE = 6,          /* logits path row-stats shape: 0 = auto (default), 1..7 = (waves per
                                       row, vectors/thread, rolling prefetch) (1,4,n) (2,8,n) (4,8,n)
                                       (8,8,n) (8,16,n) (8,8,y) (8,4,y), 8 = tiles of (8,8,n),
@@ -102,7 +102,7 @@ enum {
                                       re-reads one chunk per step */
     LAC_PATH_BLOCK = 4             /* decode only: one 4/8/16-wave workgroup per stream, all steps in
                                       one launch; the other waves stream row t+1 while wave 0 decodes
-                                      step t (AUTO from 1536 to 2047 streams; rows <= 512 iterations of
+                                      step t (AUTO at 160-256 and 1536-2047 streams; rows <= 512 iterations of
                                       64 16-B vectors, 16-B aligned, else STATS) */
 };
 

@@ -2083,8 +2083,9 @@ struct lac_ctx {
     int fine_decode = 1;                // one-wave decode: per-iteration totals (k_decode_wave_fine)
     int64_t block_decode_min_streams = 1536;  // AUTO below wave_decode_min_streams: block path from here
                                               // (measured after the serial-step rework: the stats path wins
-                                              // at 4-1024 streams except 256, block at 1536;
-                                              // profiles/r01/decode_paths_v2/)
+                                              // at 4-128 and 288-1024 streams, block at 160-256 -- its
+                                              // 16-wave groups fill the chip in one round up to 256
+                                              // streams -- and at 1536; profiles/r01/decode_paths_v2/)
     int block_waves = 0;                // block path waves per stream (0 = by stream count)
     int mapping = LAC_MAP_CEIL;         // symbol_to_range flavour (lac_set_option)
     int term = LAC_TERM_FLUSH;          // stream termination flavour
@@ -2322,7 +2323,8 @@ static int decode_dispatch(lac_ctx *c, const void *pmf, int64_t step_stride, int
     const bool vec = (p % 16 == 0) && c->V % vw == 0 && step_stride % vw == 0 && stream_stride % vw == 0;
     const bool blockable = vec && (c->V / vw + 63) / 64 <= 512;        // per-iteration totals fit LDS
     if (blockable && (c->dpath == LAC_PATH_BLOCK || (c->dpath == LAC_PATH_AUTO && !wave &&
-                                                     c->B >= c->block_decode_min_streams))) {
+                                                     ((c->B >= 160 && c->B <= 256) ||
+                                                      c->B >= c->block_decode_min_streams)))) {
         if (c->pmf_bits == 32)
             return decode_block_launch<uint32_t, 4>(c, (const uint32_t *)pmf, step_stride, stream_stride, steps, out, st);
         return decode_block_launch<uint64_t, 2>(c, (const uint64_t *)pmf, step_stride, stream_stride, steps, out, st);
