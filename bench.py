@@ -193,7 +193,8 @@ def main():
     coder.lib.lac_profile_read(coder.ctx, C.cast(dms, C.c_void_p), C.cast(dcnt, C.c_void_p), 1)
     dkids = [k for k in (3, 5, 6, 7) if dcnt[k]]              # decode_step|stats path, decode_wave, q1 pair
     dstep_ms = sum(dms[k] for k in dkids) / max(T, 1)
-    names = {3: "k_decode_step or k_dec_stats+k_decode_seq", 5: "k_decode_wave", 6: "k_q1_stats", 7: "k_q1_decode"}
+    names = {3: "k_decode_step or k_dec_stats+k_decode_seq", 5: "k_decode_wave(_fine) or k_decode_block", 6: "k_q1_stats",
+             7: "k_q1_decode"}
     decode_info = {"symbols_per_s": B * T / (d1 - d0), "kernel": "+".join(names[k] for k in dkids),
                    "kernel_ms_per_step": dstep_ms,
                    "achieved_GBps": B * (V * ebytes + 4) / (dstep_ms * 1e-3) / 1e9 if dkids else None}
