@@ -1440,7 +1440,9 @@ __global__ __launch_bounds__(256) void k_dec_stats(const E *__restrict__ pmf, in
 }
 
 template <typename E, int VEC>
-__global__ LAC_DEC_BOUNDS void k_decode_seq(const E *__restrict__ pmf, int64_t step_stride, int64_t stream_stride,
+// No occupancy bound: it runs one wave per stream for few streams (the stats path), where the
+// serial chain, not residency, sets the pace; the 4-waves/SIMD cap spilled the u64 form.
+__global__ __launch_bounds__(256) void k_decode_seq(const E *__restrict__ pmf, int64_t step_stride, int64_t stream_stride,
                                             int64_t t0, int64_t nsteps, int64_t V, int prec,
                                             const uint64_t *__restrict__ chunks,
                                             const DecRowMeta *__restrict__ meta, DecState *states,
