@@ -1,4 +1,8 @@
 # A/B of the round's start library vs the current one: c3 pmf and bf16 logits, encode + decode, same box
+# tools/ab/liblac_old.so: the round-start library, built by
+#   git --work-tree=/tmp/old checkout 9369c7c -- lac_amd/csrc include && git reset -q HEAD -- lac_amd/csrc include
+#   hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -I /tmp/old/include -I /tmp/old/lac_amd/csrc \
+#         /tmp/old/lac_amd/csrc/lac_kernels.hip -o tools/ab/liblac_old.so
 set -u
 cd "${GRAFT_REPO_ROOT}"
 mkdir -p gpurun_out/ab
