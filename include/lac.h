@@ -70,7 +70,8 @@ enum {                       /* lac_set_option */
     LAC_OPT_DECODE_PATH = 5,       /* LAC_PATH_*: SPLIT = one 4-wave workgroup per stream and step,
                                       FUSED = one wave per stream, all steps of a call in one launch;
                                       STATS, BLOCK = see LAC_PATH_STATS / LAC_PATH_BLOCK;
-                                      AUTO = FUSED from 2048 streams, BLOCK at 160-256 and from 1536, else STATS */
+                                      AUTO = FUSED from 2048 streams, BLOCK at 5/8 CUs .. CUs streams
+                                      (160-256 on MI355X) and from 1536, else STATS */
     LAC_OPT_Q1_SHAPE = 6,          /* logits path row-stats shape: 0 = auto (default), 1..7 = (waves per
                                       row, vectors/thread, rolling prefetch) (1,4,n) (2,8,n) (4,8,n)
                                       (8,8,n) (8,16,n) (8,8,y) (8,4,y), 8 = tiles of (8,8,n),
@@ -102,7 +103,7 @@ enum {
                                       re-reads one chunk per step */
     LAC_PATH_BLOCK = 4             /* decode only: one 4/8/16-wave workgroup per stream, all steps in
                                       one launch; the other waves stream row t+1 while wave 0 decodes
-                                      step t (AUTO at 160-256 and 1536-2047 streams; rows <= 512 iterations of
+                                      step t (AUTO at 5/8 CUs .. CUs and 1536-2047 streams; rows <= 512 iterations of
                                       64 16-B vectors, 16-B aligned, else STATS) */
 };
 
@@ -140,6 +141,14 @@ int lac_encode(lac_ctx *ctx, const void *pmf_dev, int64_t step_stride, int64_t s
 int lac_encode_job(lac_ctx *ctx, const void *pmf_dev, int64_t step_stride, int64_t stream_stride,
                    const int32_t *sym_dev, int64_t steps, uint64_t *trace_dev, void *stream);
 
+/* Keep each stream's registers but drop its completed output words, so the
+ * stream continues in at most 64 bits of its capacity.  For callers that read
+ * every symbol's digits from trace_dev (A_to_bin.step/run, arith_code.py:
+ * 187-211, which yield digits as they go): after a rebase the packed output of
+ * lac_encode_finish holds only the tail, while lac_flush_digits stays exact.
+ * Asynchronous on `stream`. */
+int lac_encode_rebase(lac_ctx *ctx, void *stream);
+
 /* Flush every stream and resolve carries into packed bytes (asynchronous). */
 int lac_encode_finish(lac_ctx *ctx, void *stream);
 
@@ -176,7 +185,9 @@ int lac_flush_digits(lac_ctx *ctx, int8_t *digits_host, int32_t *count_host, voi
 /* Start decoding: stream b reads nbits_dev[b] bits at bits_dev + b*stride_bytes
  * (bits_dev == NULL: this context's own encoded streams).  The buffers are
  * borrowed until the next lac_decode_open / lac_close.  stride_bytes must be a
- * multiple of 8 and every stream's region readable up to it. */
+ * multiple of 8 and every stream's region readable up to it; a stream with
+ * nbits_dev[b] > 8 * stride_bytes fails with a sticky LAC_E_ARG (lac_stream_status)
+ * and reads nothing. */
 int lac_decode_open(lac_ctx *ctx, const uint8_t *bits_dev, uint64_t stride_bytes,
                     const uint64_t *nbits_dev, void *stream);
 

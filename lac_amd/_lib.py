@@ -43,6 +43,7 @@ PROTOTYPES = [
     ("lac_encode_job", _i, [_vp, _vp, _i64, _i64, _vp, _i64, _vp, _vp]),
     ("lac_set_option", _i, [_vp, _i, _i64]),
     ("lac_encode_finish", _i, [_vp, _vp]),
+    ("lac_encode_rebase", _i, [_vp, _vp]),
     ("lac_stream_status", _i, [_vp, _vp, _vp, _vp]),
     ("lac_encoded_lengths", _i, [_vp, _vp, _vp]),
     ("lac_encoded_device", _i, [_vp, C.POINTER(_vp), C.POINTER(_u64), C.POINTER(_vp)]),

@@ -99,6 +99,13 @@ class BatchCoder:
         if pmf.stride(-1) != 1:
             raise ValueError("pmf rows must be contiguous")
 
+    def _check_out(self, out, steps):
+        torch = _torch()
+        if out.dtype != torch.int32 or out.device != self.device:
+            raise TypeError("out must be an int32 tensor on the coder's device")
+        if tuple(out.shape) != (steps, self.streams) or not out.is_contiguous():
+            raise ValueError(f"out must be a contiguous [{steps}, {self.streams}] tensor")
+
     # ------------------------------------------------------------ encode
     def reset(self):
         check(self.lib.lac_encode_reset(self.ctx, self._stream))
@@ -180,6 +187,12 @@ class BatchCoder:
 
     def finish(self):
         check(self.lib.lac_encode_finish(self.ctx, self._stream))
+
+    def rebase(self):
+        """Drop every stream's completed output words, keeping its registers
+        (include/lac.h lac_encode_rebase): for callers that take the digits from
+        ``trace`` and only need the coder state to continue."""
+        check(self.lib.lac_encode_rebase(self.ctx, self._stream))
 
     def status(self):
         err = np.zeros(self.streams, dtype=np.int32)
@@ -271,8 +284,18 @@ class BatchCoder:
             check(self.lib.lac_decode_open(self.ctx, None, 0, None, self._stream))
             self._dec_keep = None
             return
+        torch = _torch()
+        if bits.dtype != torch.uint8 or bits.device != self.device:
+            raise TypeError("bits must be a uint8 tensor on the coder's device")
         if bits.dim() != 2 or bits.shape[0] != self.streams or bits.stride(1) != 1:
             raise ValueError("bits must be [streams, stride] with contiguous rows")
+        if bits.stride(0) % 8 or bits.data_ptr() % 8:
+            raise ValueError("bits rows must be 8-byte aligned (row stride a multiple of 8 bytes)")
+        if nbits is None or nbits.dtype not in (torch.int64, torch.uint64) or nbits.device != self.device:
+            raise TypeError("nbits must be an int64/uint64 tensor on the coder's device")
+        if tuple(nbits.shape) != (self.streams,) or not nbits.is_contiguous():
+            raise ValueError(f"nbits must be a contiguous [{self.streams}] tensor")
+        # nbits[b] > 8 * stride fails that stream with a sticky LAC_E_ARG in the library
         self._dec_keep = (bits, nbits)                        # borrowed by the library
         check(self.lib.lac_decode_open(self.ctx, C.c_void_p(bits.data_ptr()), bits.stride(0),
                                        C.c_void_p(nbits.data_ptr()), self._stream))
@@ -290,13 +313,17 @@ class BatchCoder:
         self._check_pmf(pmf)
         if pmf.dim() == 2:
             pmf = pmf.unsqueeze(0)
-        if pmf.dim() == 1:
+        if pmf.dim() != 3:
             raise ValueError("give decode a [steps, streams, V] (or expanded) table")
+        if pmf.shape[1] not in (1, self.streams):
+            raise ValueError(f"pmf must be [steps, {self.streams} or 1, {self.vocab}], got {tuple(pmf.shape)}")
         steps = pmf.shape[0]
         step_stride = pmf.stride(0) if steps > 1 else 0
         stream_stride = pmf.stride(1) if pmf.shape[1] > 1 else 0
         if out is None:
             out = torch.empty((steps, self.streams), dtype=torch.int32, device=self.device)
+        else:
+            self._check_out(out, steps)
         check(self.lib.lac_decode_steps(self.ctx, C.c_void_p(pmf.data_ptr()), step_stride, stream_stride, steps,
                                         C.c_void_p(out.data_ptr()), self._stream))
         return out
@@ -361,6 +388,8 @@ class BatchCoder:
         typ, ss, bs, steps, logits = self._logits_args(logits)
         if out is None:
             out = torch.empty((steps, self.streams), dtype=torch.int32, device=self.device)
+        else:
+            self._check_out(out, steps)
         check(self.lib.lac_decode_logits_steps(self.ctx, C.c_void_p(logits.data_ptr()), typ, ss, bs, steps,
                                                C.c_void_p(out.data_ptr()), self._stream))
         return out
@@ -380,7 +409,7 @@ class BatchCoder:
         check(self.lib.lac_set_option(self.ctx, _lib.LAC_OPT_Q1_SHAPE, int(shape)))
 
     def q1_k(self):
-        """The q1 table scale: max entry 2^k, k = min(31, prec - 1 - ceil(log2 V))."""
+        """The q1 table scale: max entry 2^k, k = min(24, prec - 1 - ceil(log2 V)) (lac.h lac_q1_k)."""
         return int(self.lib.lac_q1_k(self.prec, self.vocab))
 
 

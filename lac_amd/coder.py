@@ -206,23 +206,63 @@ class A_to_bin:
         self.debug_log = None
         self._coder = None
         self._V = None
+        self._plane_bits = 0          # output bits held in the device planes since the last reset
+        self._nsym = 0                # symbols coded since the last reset
 
     # -- device plumbing
-    def _ensure(self, V, steps_hint=1):
-        need = (self.emitted_bits + (steps_hint + 2) * (self.precision + 2) + 256)
-        if self._coder is None or self._V != V or self._coder.capacity_bits < need:
-            if self._coder is not None and self.emitted_bits:
-                raise RuntimeError("table size or capacity changed mid-stream; use run() for long inputs")
-            self._coder = BatchCoder(V, 1, prec=self.precision, pmf_bits=64,
-                                     capacity_bits=max(need * 2, 1 << 12))
-            self._coder.set_mapping(_Tables(self.predictor).mapping)
-            self._V = V
+    # Digits reach the caller through the per-symbol trace, so the device's own
+    # output planes only have to hold what was coded since the last reset (or
+    # rebase, which keeps the registers and drops finished words): a stream of
+    # any length -- step() loops, repeated run() calls, reuse after flush() --
+    # fits a fixed capacity.
+    _SLACK = 256                      # flush digits + the word a rebase keeps
 
-    def _encode_rows(self, rows, syms, trace=True):
+    def _ensure(self, V, steps):
+        per = self.precision + 1      # one symbol emits at most prec digits (renorm)
+        need = (steps + 2) * per + self._SLACK
+        if self._coder is not None and self._V == V:
+            return
+        if self._coder is not None and self._plane_bits:
+            raise RuntimeError(f"table size changed mid-stream ({self._V} -> {V} symbols); flush() first")
+        if self._coder is not None:
+            self._coder.close()
+        self._coder = BatchCoder(V, 1, prec=self.precision, pmf_bits=64, capacity_bits=max(need * 2, 1 << 12))
+        self._coder.set_mapping(_Tables(self.predictor).mapping)
+        self._V = V
+        self._plane_bits = 0
+        self._nsym = 0
+
+    def _encode_rows(self, rows, syms):
+        """Encode rows/syms (chunked to the coder's capacity); -> (digit lists, (rc, n_ok))."""
+        steps = len(syms)
+        V = len(rows[0])
+        if self._coder is not None and self._V == V and self._plane_bits == 0:
+            per = self.precision + 1
+            if self._coder.capacity_bits < (steps + 2) * per + self._SLACK:
+                self._coder.close()
+                self._coder = None    # empty planes: reallocate at the new size
+        self._ensure(V, steps)
+        per = self.precision + 1
+        out = []
+        i = 0
+        while i < steps:
+            room = (self._coder.capacity_bits - self._plane_bits - self._SLACK) // per
+            if room < 1:
+                self._coder.rebase()
+                self._plane_bits = 64
+                continue
+            n = min(room, steps - i)
+            digs, rc, n_ok = self._encode_chunk(rows[i:i + n], syms[i:i + n])
+            out.extend(digs)
+            if rc:
+                return out, (rc, i + n_ok)
+            i += n
+        return out, (0, steps)
+
+    def _encode_chunk(self, rows, syms):
         import torch
         steps = len(syms)
         V = len(rows[0])
-        self._ensure(V, steps)
         dev = self._coder.device
         pmf = torch.from_numpy(np.stack(rows).astype(np.uint64).view(np.int64).reshape(steps, 1, V)).to(dev)
         sym = torch.tensor([int(s) if 0 <= int(s) < 2 ** 31 else -1 for s in syms], dtype=torch.int32,
@@ -231,11 +271,14 @@ class A_to_bin:
         self._coder.encode(pmf, sym, trace=tr)
         rc, err, step = self._coder.status()
         t = tr.cpu().numpy()
-        n_ok = steps if rc == 0 else int(step[0])
+        # err_step counts symbols since the last reset: the failing one's index in this chunk
+        n_ok = steps if rc == 0 else min(max(int(step[0]) - self._nsym, 0), steps)
+        self._nsym += n_ok
         digs = [digits_of(int(E), int(k)) for E, k in t[:n_ok, 0]]
         for d in digs:
             self.emitted_bits += len(d)
-        return digs, (rc, n_ok)
+            self._plane_bits += len(d)
+        return digs, rc, n_ok
 
     # -- registers (reference attributes)
     @property
@@ -269,7 +312,7 @@ class A_to_bin:
     def flush(self):
         if self._coder is None:
             tab = _Tables(self.predictor)
-            self._ensure(len(tab.row()))
+            self._ensure(len(tab.row()), 0)
         self._coder.finish()
         rc, err, step = self._coder.status()
         if rc:
@@ -278,6 +321,8 @@ class A_to_bin:
         self.emitted_bits += len(fd)
         yield from fd
         self._coder.reset()
+        self._plane_bits = 0
+        self._nsym = 0
 
     def _collect(self, symbols):
         tab = _Tables(self.predictor)

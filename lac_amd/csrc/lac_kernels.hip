@@ -617,6 +617,20 @@ __global__ __launch_bounds__(256) void k_finish(EncState *states, uint64_t *plan
     states[b] = st;
 }
 
+// Drop every completed plane word of each stream, keeping the registers and the
+// word that holds bit L-1 (the only bit a later carry can land on): L becomes
+// ((L-1) mod 64) + 1.  For callers that take each symbol's digits from the
+// trace (A_to_bin.step / run in lac_amd/coder.py) so a stream of any length
+// fits a fixed capacity; the packed output of lac_encode_finish then holds
+// only the tail, but the flush digits are exact.
+__global__ void k_enc_rebase(EncState *states, int64_t B) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    EncState st = states[b];
+    if (st.L > 64) st.L = ((st.L - 1) & 63) + 1;
+    states[b] = st;
+}
+
 __global__ void k_enc_reset(EncState *states, int64_t B, int prec) {
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= B) return;
@@ -676,11 +690,19 @@ __global__ void k_dec_init(DecState *states, int64_t B, int prec, const uint8_t 
     memset(&st, 0, sizeof(st));
     st.l = 0;
     st.h = ((int64_t)1 << prec) - 1;
-    st.x = (int64_t)read_bits(bits + b * stride, nbits[b], 0, prec);
     st.pos = (uint64_t)prec;
     st.err_step = -1;
     st.det = 1;
     st.ndet = 0;
+    // A stream claiming more bits than its row holds would make every later
+    // bit-window load run past the row (and past the buffer for the last
+    // stream): it fails with a sticky LAC_E_ARG before anything is read.
+    if (nbits[b] > stride * 8) {
+        st.err = LAC_E_ARG;
+        st.err_step = 0;
+    } else {
+        st.x = (int64_t)read_bits(bits + b * stride, nbits[b], 0, prec);
+    }
     states[b] = st;
 }
 
@@ -2088,6 +2110,9 @@ struct lac_ctx {
                                               // at 4-128 and 288-1024 streams, block at 160-256 -- its
                                               // 16-wave groups fill the chip in one round up to 256
                                               // streams -- and at 1536; profiles/r01/decode_paths_v2/)
+    int64_t block_window_lo = 160, block_window_hi = 256;   // AUTO: block path inside this window too --
+                                              // one 16-wave group per stream fills the chip in one round
+                                              // while streams <= CUs; set from the CU count at open
     int block_waves = 0;                // block path waves per stream (0 = by stream count)
     int mapping = LAC_MAP_CEIL;         // symbol_to_range flavour (lac_set_option)
     int term = LAC_TERM_FLUSH;          // stream termination flavour
@@ -2325,7 +2350,7 @@ static int decode_dispatch(lac_ctx *c, const void *pmf, int64_t step_stride, int
     const bool vec = (p % 16 == 0) && c->V % vw == 0 && step_stride % vw == 0 && stream_stride % vw == 0;
     const bool blockable = vec && (c->V / vw + 63) / 64 <= 512;        // per-iteration totals fit LDS
     if (blockable && (c->dpath == LAC_PATH_BLOCK || (c->dpath == LAC_PATH_AUTO && !wave &&
-                                                     ((c->B >= 160 && c->B <= 256) ||
+                                                     ((c->B >= c->block_window_lo && c->B <= c->block_window_hi) ||
                                                       c->B >= c->block_decode_min_streams)))) {
         if (c->pmf_bits == 32)
             return decode_block_launch<uint32_t, 4>(c, (const uint32_t *)pmf, step_stride, stream_stride, steps, out, st);
@@ -2546,6 +2571,8 @@ int lac_open(int device, int prec, int64_t vocab, int64_t streams, int pmf_bits,
     c->device = device;
     if (hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || c->cus < 1)
         c->cus = 256;
+    c->block_window_hi = c->cus;                      // 256 on MI355X
+    c->block_window_lo = (c->cus * 5) / 8;            // 160 on MI355X (measured, profiles/r01/decode_paths_v2/)
     c->prec = prec;
     c->pmf_bits = pmf_bits;
     c->V = vocab;
@@ -2599,6 +2626,15 @@ int lac_encode_reset(lac_ctx *c, void *stream) {
     HIPCHK(hipSetDevice(c->device));
     c->mode = 0;
     k_enc_reset<<<(unsigned)((c->B + 255) / 256), 256, 0, S(stream)>>>(c->enc, c->B, c->prec);
+    CHECK_LAUNCH();
+    return LAC_OK;
+}
+
+int lac_encode_rebase(lac_ctx *c, void *stream) {
+    if (!c) return fail(LAC_E_ARG, "ctx is NULL");
+    if (c->mode != 0) return fail(LAC_E_STATE, "context is decoding");
+    HIPCHK(hipSetDevice(c->device));
+    k_enc_rebase<<<(unsigned)((c->B + 255) / 256), 256, 0, S(stream)>>>(c->enc, c->B);
     CHECK_LAUNCH();
     return LAC_OK;
 }

@@ -238,3 +238,108 @@ def test_quantiser_matches_reference_numpy_ops():
     pdf /= np.sum(pdf)
     want = np.cumsum(np.clip((pdf * (1 << 60)).astype(float), 2, None)).astype(int)
     assert (quantise_logits(logits) == want).all()
+
+
+def _static_case(V=300, n=10000, seed=7):
+    rng = np.random.default_rng(seed)
+    pmf = rng.integers(1, 1000, V).astype(np.uint64)
+    syms = rng.choice(V, size=n, p=pmf / pmf.sum()).tolist()
+    return pmf, syms
+
+
+def test_step_loop_10k_symbols_matches_oracle():
+    """A_to_bin.step/__call__ one symbol at a time for 10k symbols (far beyond the
+    first coder's capacity): digits == the C oracle's (capacity was
+    sized by the cumulative emitted bits)."""
+    from lac_amd.coder import AC, CDFPredictor
+    from oracle import oracle as coracle
+    pmf, syms = _static_case()
+    prec = 48
+    _, _, want = coracle.encode(pmf, syms, prec, static=True)
+    enc = AC(CDFPredictor(np.cumsum(pmf).tolist()), prec).to_bin
+    got = []
+    for s in syms:
+        got.extend(enc(s))
+    got.extend(enc(None))
+    assert got == want
+    assert enc.emitted_bits == len(want)
+
+
+def test_encoder_reuse_after_flush_longer_input():
+    """run() again on a flushed encoder with a longer input (reference: the coder
+    restarts from l=0, h=2^prec-1 after flush, arith_code.py:193-202)."""
+    from lac_amd.coder import AC, CDFPredictor
+    from oracle import oracle as coracle
+    pmf, syms = _static_case(n=20000, seed=8)
+    prec = 40
+    enc = AC(CDFPredictor(np.cumsum(pmf).tolist()), prec).to_bin
+    for n in (10, 3000, 20000, 5):
+        _, _, want = coracle.encode(pmf, syms[:n], prec, static=True)
+        assert list(enc.run(syms[:n])) == want, n
+
+
+def test_run_then_steps_then_long_run_without_flush():
+    """Mixing run(stop=0), step() and a long run() on one stream: the capacity is
+    recovered by rebasing the device planes, the digits stay exact."""
+    from lac_amd.coder import AC, CDFPredictor
+    from oracle import restate
+    pmf, syms = _static_case(V=50, n=12000, seed=9)
+    prec = 32
+    enc = AC(CDFPredictor(np.cumsum(pmf).tolist()), prec).to_bin
+    got = list(enc.run(syms[:100], stop=0))
+    for s in syms[100:200]:
+        got.extend(enc.step(s))
+    got.extend(enc.run(syms[200:], stop=1))
+    assert got == restate.encode_digits([pmf.tolist()], syms, prec)
+
+
+def test_batch_decode_rejects_bad_shapes():
+    """BatchCoder.decode / decode_open validate tables, outputs and bit buffers
+    instead of letting the kernels read or write out of bounds."""
+    from lac_amd.batch import BatchCoder
+    dev = "cuda:0"
+    V, B = 64, 4
+    coder = BatchCoder(V, B, prec=24, device=dev)
+    pmf = torch.ones((3, B, V), dtype=torch.int32, device=dev)
+    coder.encode(pmf, torch.zeros((3, B), dtype=torch.int32, device=dev))
+    coder.finish()
+    coder.decode_open()
+    with pytest.raises(ValueError):
+        coder.decode(torch.ones((3, B - 1, V), dtype=torch.int32, device=dev))
+    with pytest.raises(ValueError):
+        coder.decode(pmf, out=torch.empty((2, B), dtype=torch.int32, device=dev))
+    with pytest.raises(TypeError):
+        coder.decode(pmf, out=torch.empty((3, B), dtype=torch.int64, device=dev))
+    bits = torch.zeros((B, 16), dtype=torch.uint8, device=dev)
+    with pytest.raises(TypeError):
+        coder.decode_open(bits.view(torch.int64), torch.zeros(B, dtype=torch.int64, device=dev))
+    with pytest.raises(TypeError):
+        coder.decode_open(bits, torch.zeros(B, dtype=torch.int32, device=dev))
+    with pytest.raises(ValueError):
+        coder.decode_open(bits, torch.zeros(B + 1, dtype=torch.int64, device=dev))
+    # nbits beyond the row: that stream fails (sticky LAC_E_ARG), the others decode
+    nb = torch.tensor([8, 16 * 8, 16 * 8 + 1, 0], dtype=torch.int64, device=dev)
+    coder.decode_open(bits, nb)
+    out = coder.decode(pmf)
+    rc, err, _ = coder.status()
+    assert err.tolist() == [0, 0, -1, 0]
+    assert (out[:, 2] == -1).all() and (out[:, [0, 1, 3]] >= 0).all()
+    coder.close()
+
+
+def test_acsampler_per_token_pdfs_bits_and_entropy():
+    """ACSampler with a new float pdf per token: GPU bits and bits_per_token ==
+    the reference's (tests/golden/acsampler_cb.json); the host Region mirror
+    agrees with the GPU coder's registers at flush."""
+    from lac_amd.sampler import ACSampler
+    for case in load_golden("acsampler_cb.json")["cases"]:
+        s = ACSampler(48)
+        bits, ent = [], []
+        s.compress_tokens = iter(case["tokens"])
+        s.compress_output = bits.append
+        s.bits_per_token = ent.append
+        for pdf in case["pdfs"]:
+            s.sample(pdf)
+        s.flush_compress()
+        assert "".join(map(str, bits)) == case["bits"]
+        assert ent == case["entropy"]

@@ -209,6 +209,55 @@ def acsampler_nonuniform(rng):
     return cases
 
 
+def acsampler_callbacks(seed=20261016):
+    """ACSampler with a different float pdf per token: the bits, every
+    bits_per_token value (Region.entropy_of at the current span) and the
+    unencodable-token assertion (arithmetic_coding.py:73-95, :155-157)."""
+    import arithmetic_coding as acd
+    rng = np.random.default_rng(seed)
+    cases = []
+    for k in range(5):
+        V = int(rng.choice([2, 7, 256, 1000]))
+        n = int(rng.integers(1, 120))
+        pdfs = [(rng.random(V) ** 4 * 50 + 1e-12).tolist() for _ in range(n)]
+        toks = [int(rng.integers(0, V)) for _ in range(n)]
+        s = acd.ACSampler(48)
+        bits, ent = [], []
+        s.compress_tokens = iter(toks)
+        s.compress_output = bits.append
+        s.bits_per_token = ent.append
+
+        def done(s=s):
+            s.on_compress_done = None
+            s.flush_compress()
+            s.compress_output = None
+        s.on_compress_done = done
+        i = 0
+        while not s.compress_done:
+            s.sample(pdfs[min(i, n - 1)])
+            i += 1
+        # the phantom token after exhaustion also reports an entropy: keep the
+        # per-token values of the real tokens only
+        cases.append({"pdfs": pdfs, "tokens": toks, "bits": "".join(map(str, bits)), "entropy": ent[:n]})
+    # scaled cdfs the reference rejects: a token whose floor-mapped width is 0
+    bad = []
+    for cdf, pre in (([1, 2, 1 << 48], []), ([1, 2, 1 << 50], []), ([5, 5, 9], []),
+                     ([1 << 40, (1 << 40) + 1, 1 << 48], [1, 2]), ([1 << 40, (1 << 40) + 1, 1 << 48], [1, 1, 2]),
+                     ([1, 2, 1 << 48], [0, 1]), ([1, 2, 1 << 48], [2, 0, 1])):
+        s = acd.ACSampler(48)
+        s.compress_tokens = iter(pre + [0])
+        s.compress_output = lambda b: None
+        good = np.array([3 << 44, 7 << 44, 10 << 44], dtype=np.uint64)
+        for t in pre:
+            s.sample_scaled_cdf(good)
+        try:
+            s.sample_scaled_cdf(np.array(cdf, dtype=np.uint64))
+            bad.append({"cdf": cdf, "pre": pre, "raises": None})
+        except AssertionError as e:
+            bad.append({"cdf": cdf, "pre": pre, "raises": str(e)})
+    return {"cases": cases, "unencodable": bad}
+
+
 def deterministic():
     """Rows with a single positive entry: the encoder emits nothing for them."""
     out = []
@@ -244,8 +293,13 @@ def errors():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--kat", action="store_true", help="also run the 1 MiB KATs (~2 min)")
+    ap.add_argument("--only", choices=["acsampler_cb"], help="write just this fixture file")
     a = ap.parse_args()
     os.makedirs(GOLDEN, exist_ok=True)
+    if a.only == "acsampler_cb":
+        with open(os.path.join(GOLDEN, "acsampler_cb.json"), "w") as f:
+            json.dump(acsampler_callbacks(), f, separators=(",", ":"))
+        return
     rng = random.Random(20261015)
     small = {"static": small_cases(rng, 250, perstep=False),
              "perstep": small_cases(rng, 250, perstep=True)}
