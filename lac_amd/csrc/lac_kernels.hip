@@ -305,6 +305,106 @@ __device__ inline RowSums row_reduce(const E *row, int64_t V, int64_t s) {
     return r;
 }
 
+// The same reduction, software-pipelined across groups and rows.  A row is
+// streamed in groups of U = LAC_UNROLL vectors per lane; `buf` holds the group
+// being consumed while the next one is in flight (LAC_PIPE 1: the next group's
+// loads are issued before the current group is consumed, 2 x U vectors in
+// registers; LAC_PIPE 0: issued right after it).  After the row's last group,
+// `next` (the wave's following row, or nullptr) gets its first group issued, so
+// the per-step tail -- wave reductions, the coder step -- runs with loads in
+// flight instead of with the wave's memory pipe idle.  On entry `buf` must hold
+// group 0 of `row` (row_group_load(buf, row, 0, nvec)).
+#ifndef LAC_PIPE
+#define LAC_PIPE 0
+#endif
+// Measured on MI355X (same box, c3): no gain for the fused encoder -- u32
+// 1.214 (off) vs 1.219 ms/job, u64 2.43 (off) vs 2.50 ms with a 2-wave bound
+// (3.07 ms unbounded: one wave per SIMD) -- so it is off by default; the
+// decoder, whose tail holds a dependent re-read, gains (LAC_DEC_XPF).
+#ifndef LAC_XPF                    // issue the next row's first group before the step's tail
+#define LAC_XPF 0
+#endif
+template <typename E, int VEC> struct RowGroup { typename VecT<E, VEC>::type x[LAC_UNROLL]; };
+
+template <typename E, int VEC>
+__device__ inline void row_group_load(RowGroup<E, VEC> &g, const E *row, int64_t base, int64_t nvec) {
+    constexpr int U = LAC_UNROLL;
+    const int64_t vi = base + (int64_t)lane_id();
+    if (base + 64 * U <= nvec) {                              // wave-uniform: the whole group is in the row
+#pragma unroll
+        for (int u = 0; u < U; u++) g.x[u] = load_vec<E, VEC>(row, vi + 64 * u);
+    } else {
+#pragma unroll
+        for (int u = 0; u < U; u++) g.x[u] = load_vec_or0<E, VEC>(row, vi + 64 * u, nvec);
+    }
+}
+
+template <typename E, int VEC>
+__device__ inline RowSums row_reduce_pf(const E *row, int64_t V, int64_t s, RowGroup<E, VEC> &buf, const E *next) {
+    const int lane = (int)lane_id();
+    const int64_t sc = s < 0 ? 0 : (s > V ? V : s);
+    const int64_t nvec = V / VEC, sfull = sc / VEC;
+    const int sr = (int)(sc - sfull * VEC);
+    constexpr bool W = sizeof(E) == 8;
+    constexpr int U = LAC_UNROLL;
+    uint64_t tot = 0, lo = 0, tot_h = 0, lo_h = 0, ps = 0;
+    E mn = (E)~(E)0;
+    auto take = [&](const typename VecT<E, VEC>::type &x, int64_t v) {
+        uint64_t sl = 0, sh = 0;
+#pragma unroll
+        for (int j = 0; j < VEC; j++) {
+            const E e = vget<E, VEC>(x, j);
+            if constexpr (W) { sl += (uint32_t)e; sh += (uint64_t)e >> 32; } else { sl += e; }
+            const E m1 = e - 1;
+            mn = m1 < mn ? m1 : mn;
+        }
+        tot += sl;
+        tot_h += sh;
+        if (v < sfull) { lo += sl; lo_h += sh; }
+        if (v == sfull) {
+#pragma unroll
+            for (int j = 0; j < VEC; j++) {
+                const E e = vget<E, VEC>(x, j);
+                if (j < sr) {
+                    if constexpr (W) { lo += (uint32_t)e; lo_h += (uint64_t)e >> 32; } else { lo += e; }
+                }
+                if (j == sr) ps = (uint64_t)e;
+            }
+        }
+    };
+    const int64_t gw = 64 * U, ngrp = (nvec + gw - 1) / gw;
+    for (int64_t g = 0; g < ngrp; g++) {
+        const int64_t base = g * gw;
+#if LAC_PIPE
+        const RowGroup<E, VEC> cur = buf;
+        if (g + 1 < ngrp) row_group_load<E, VEC>(buf, row, base + gw, nvec);
+        else if (next) row_group_load<E, VEC>(buf, next, 0, nvec);
+#pragma unroll
+        for (int u = 0; u < U; u++) take(cur.x[u], base + 64 * u + lane);
+#else
+#pragma unroll
+        for (int u = 0; u < U; u++) take(buf.x[u], base + 64 * u + lane);
+        if (g + 1 < ngrp) row_group_load<E, VEC>(buf, row, base + gw, nvec);
+        else if (next) row_group_load<E, VEC>(buf, next, 0, nvec);
+#endif
+    }
+    RowSums r;
+    tot = wave_sum_u64(tot);
+    lo = wave_sum_u64(lo);
+    ps = wave_sum_u64(ps);
+    if constexpr (W) {
+        tot_h = wave_sum_u64(tot_h);
+        lo_h = wave_sum_u64(lo_h);
+        r.minp = wave_min_u64(mn) + 1;
+    } else {
+        r.minp = (uint64_t)wave_min_u32(mn) + 1;
+    }
+    r.T = (u128)tot + ((u128)tot_h << 32);
+    r.lo = (u128)lo + ((u128)lo_h << 32);
+    r.ps = ps;
+    return r;
+}
+
 // ------------------------------------------------------------------ fudge scan
 // max_{j<n} (c_j*w - j*T) over the first n entries of a row, by one wave;
 // *csum (optional) receives c_{n-1}.
@@ -588,11 +688,19 @@ __global__ LAC_ENC_BOUNDS void k_encode_fused(const E *__restrict__ pmf, int64_t
         return;
     }
     int64_t l = st.l, h = st.h;
+    RowGroup<E, VEC> buf;
+    if (LAC_XPF && nsteps > 0) row_group_load<E, VEC>(buf, pmf + t0 * step_stride + b * stream_stride, 0, V / VEC);
     for (int64_t i = 0; i < nsteps; i++) {
         const int64_t t = t0 + i;
         const E *row = pmf + t * step_stride + b * stream_stride;
+#if LAC_XPF
+        const E *next = i + 1 < nsteps ? row + step_stride : nullptr;
+#else
+        const E *next = nullptr;
+        row_group_load<E, VEC>(buf, row, 0, V / VEC);
+#endif
         const int64_t s = sym[t * B + b];
-        const RowSums rs = row_reduce<E, VEC>(row, V, s);
+        const RowSums rs = row_reduce_pf<E, VEC>(row, V, s, buf, next);
         if (rs.T >> 64) { st.err = LAC_E_TABLE; break; }
         const uint64_t lo = (uint64_t)rs.lo;
         if (!coder_step<E>(st, l, h, lo, lo + rs.ps, (uint64_t)rs.T, rs.minp, s, row, V, prec, pa, pc, cap_words,
@@ -1098,6 +1206,40 @@ __device__ inline uint64_t xor_lane_u64(uint64_t x) {
     if constexpr (BIT < 4) return ((uint64_t)xor_dpp<BIT>((uint32_t)(x >> 32)) << 32) | xor_dpp<BIT>((uint32_t)x);
     else return shfl_xor_u64(x, 1 << BIT);
 }
+// ---- row totals and minp without 64-bit compares on the streaming loop
+// u64 rows: the total is accumulated wrapping mod 2^64 next to H = the sum of the
+// entries' high words (exact).  T lies in [2^32 H, 2^32 (H + V)) and V <= 2^31,
+// so T = S + k 2^64 with k in {0, 1} (S the wrapped sum), and T < 2^64 iff
+// H < 2^32 and S >= 2^32 H.  While T < 2^64 every partial sum is exact.
+__device__ inline bool u64_total_overflows(uint64_t S, uint64_t H) { return (H >> 32) || S < (H << 32); }
+
+// minp key: e - 1 (0 wraps to the max, as CDFPredictor.minp skips zeros,
+// arith_code.py:79-82); for u64 entries >= 2^32 the key saturates, so one 32-bit
+// min per entry finds every minp below 2^32 exactly.
+template <typename E> __device__ inline uint32_t min_key(E e);
+template <> __device__ inline uint32_t min_key<uint32_t>(uint32_t e) { return e - 1u; }
+template <> __device__ inline uint32_t min_key<uint64_t>(uint64_t e) {
+    return (e >> 32) ? 0xFFFFFFFFu : (uint32_t)e - 1u;
+}
+
+// minp from the row's minimum key (wave-uniform).  Exact, except that a u64 row
+// whose positive entries are all >= 2^32 reports 2^32: minp only enters the
+// fudge test T > w * minp (arith_code.py:84), which 2^32 decides exactly unless
+// T > w * 2^32 (possible below prec 34 only) -- then the row is re-scanned with
+// 64-bit mins (cold).
+template <typename E>
+__device__ inline uint64_t row_minp(const E *row, int64_t V, uint32_t kmin, uint64_t T, uint64_t w) {
+    if constexpr (sizeof(E) == 8) {
+        if (kmin == 0xFFFFFFFFu && (u128)T > ((u128)w << 32)) {
+            uint64_t m = ~0ull;
+            for (int64_t i = lane_id(); i < V; i += 64) { const uint64_t e = row[i] - 1; m = e < m ? e : m; }
+            return wave_min_u64(m) + 1;
+        }
+    }
+    (void)row; (void)V; (void)T; (void)w;
+    return (uint64_t)kmin + 1;
+}
+
 template <bool CHK>
 __device__ inline uint64_t add_ovf(uint64_t a, uint64_t b, uint32_t &ovf) {
     const uint64_t s = a + b;
@@ -1143,6 +1285,14 @@ __device__ inline uint64_t wave_sum8_u64(const uint64_t (&s)[8], uint32_t &ovf) 
     return r;
 }
 
+#ifndef LAC_DEC_XPF                // k_decode_wave_fine: next group in flight while one is consumed,
+                                   // and the next row's first group over the step's tail (+2.5 %)
+#define LAC_DEC_XPF 1
+#endif
+#ifndef LAC_DEC_STREAM_ONLY        // timing experiment only: skip the search (wrong symbols)
+#define LAC_DEC_STREAM_ONLY 0
+#endif
+
 // k_decode_wave with one total per 64-vector iteration of the row instead of per
 // <= 64-iteration chunk (rows of <= 512 iterations: V <= 131072 u32 / 65536 u64
 // entries).  Iteration p's total lives in lane p % 64 of register p / 64, the
@@ -1162,6 +1312,15 @@ __global__ __launch_bounds__(256, LAC_DECF_MINW) void k_decode_wave_fine(const E
     const uint8_t *mybits = bits + b * stride;
     const uint64_t mynbits = nbits[b];
     const int nvec = (int)(V / VEC), nit = (nvec + 63) / 64, ngrp = (nit + 7) / 8;
+#if LAC_DEC_XPF
+    typename VecT<E, VEC>::type xb[8];
+    if (nsteps > 0) {
+        const E *row0 = pmf + b * stream_stride;
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+            xb[u] = nvec >= 512 ? load_vec<E, VEC>(row0, u * 64 + lane) : load_vec_or0<E, VEC>(row0, u * 64 + lane, nvec);
+    }
+#endif
     for (int64_t t = 0; t < nsteps; t++) {
         int32_t *out = sym_out + t * B + b;
         if (st.err) {
@@ -1172,16 +1331,32 @@ __global__ __launch_bounds__(256, LAC_DECF_MINW) void k_decode_wave_fine(const E
         uint64_t mine[NR];
 #pragma unroll
         for (int r = 0; r < NR; r++) mine[r] = 0;
-        E mn = (E)~(E)0;
-        uint32_t ovf = 0;
+        uint32_t mn = ~0u;                                    // min over min_key (0 -> max)
+        uint64_t hh = 0;                                      // u64 rows: sum of the high words
+        uint32_t ovf = 0;                                     // (unused: totals wrap, see u64_total_overflows)
         const int nfull = nvec / 512;                         // groups of 8 whole iterations
         auto group = [&](int g, bool full) {
+#if LAC_DEC_XPF
+            // x holds group g (issued after group g-1, or before the previous step's tail)
+            typename VecT<E, VEC>::type x[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) x[u] = xb[u];
+            if (g + 1 < ngrp) {
+                const bool nf = g + 1 < nfull;
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const int vi = ((g + 1) * 8 + u) * 64 + lane;
+                    xb[u] = nf ? load_vec<E, VEC>(row, vi) : load_vec_or0<E, VEC>(row, vi, nvec);
+                }
+            }
+#else
             typename VecT<E, VEC>::type x[8];
 #pragma unroll
             for (int u = 0; u < 8; u++) {
                 const int vi = (g * 8 + u) * 64 + lane;
                 x[u] = full ? load_vec<E, VEC>(row, vi) : load_vec_or0<E, VEC>(row, vi, nvec);
             }
+#endif
             uint64_t s[8];
 #pragma unroll
             for (int u = 0; u < 8; u++) {
@@ -1189,13 +1364,13 @@ __global__ __launch_bounds__(256, LAC_DECF_MINW) void k_decode_wave_fine(const E
 #pragma unroll
                 for (int j = 0; j < VEC; j++) {
                     const E e = vget<E, VEC>(x[u], j);
-                    a = add_ovf<W>(a, (uint64_t)e, ovf);
-                    const E m1 = e - 1;
-                    mn = m1 < mn ? m1 : mn;
+                    a += (uint64_t)e;                         // wraps only if T >= 2^64 (detected below)
+                    if constexpr (W) hh += (uint64_t)e >> 32;
+                    mn = min(mn, min_key<E>(e));
                 }
                 s[u] = a;
             }
-            const uint64_t tot = wave_sum8_u64<W>(s, ovf);    // lane l: iteration g*8 + (l & 7)
+            const uint64_t tot = wave_sum8_u64<false>(s, ovf);   // lane l: iteration g*8 + (l & 7)
             const bool mylane = (lane >> 3) == (g & 7);
 #pragma unroll
             for (int r = 0; r < NR; r++)
@@ -1203,21 +1378,28 @@ __global__ __launch_bounds__(256, LAC_DECF_MINW) void k_decode_wave_fine(const E
         };
         for (int g = 0; g < nfull; g++) group(g, true);
         if (nfull < ngrp) group(nfull, false);
-        uint64_t minp;
-        if constexpr (W) minp = wave_min_u64(mn) + 1;
-        else minp = (uint64_t)wave_min_u32(mn) + 1;
+#if LAC_DEC_XPF
+        if (t + 1 < nsteps) {                                 // next row's group 0, in flight over the tail
+            const E *nrow = row + step_stride;
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int vi = u * 64 + lane;
+                xb[u] = nfull > 0 ? load_vec<E, VEC>(nrow, vi) : load_vec_or0<E, VEC>(nrow, vi, nvec);
+            }
+        }
+#endif
         uint64_t incl[NR];
-        u128 lsum = 0;
         uint64_t base = 0;
 #pragma unroll
         for (int r = 0; r < NR; r++) {
-            lsum += mine[r];
             incl[r] = base + wave_incl_scan_u64(mine[r]);     // exact once T < 2^64 is checked
             base = readlane_u64(incl[r], 63);
         }
-        const u128 acc128 = W ? wave_sum_u128(lsum) : (u128)base;
+        const uint64_t T = base;
         int err = 0;
-        if (__any(ovf) || (acc128 >> 64) || acc128 == 0) err = LAC_E_TABLE;
+        if (T == 0) err = LAC_E_TABLE;
+        if constexpr (W) { if (u64_total_overflows(T, wave_sum_u64(hh))) err = LAC_E_TABLE; }
+        const uint64_t minp = err ? 1 : row_minp<E>(row, V, wave_min_u32(mn), T, (uint64_t)(st.h - st.l + 1));
         int64_t s = -1;
         if (!err) {
             auto find_chunk = [&](uint64_t tgt, int64_t *cv0, int *G, uint64_t *cb) {
@@ -1236,8 +1418,8 @@ __global__ __launch_bounds__(256, LAC_DECF_MINW) void k_decode_wave_fine(const E
                 }
                 return false;
             };
-            err = decode_symbol<E, VEC>(st, row, V, (uint64_t)acc128, minp, prec, mapping, mybits, mynbits,
-                                        find_chunk, &s);
+            if (LAC_DEC_STREAM_ONLY) s = (int64_t)(minp & 1);
+            else err = decode_symbol<E, VEC>(st, row, V, T, minp, prec, mapping, mybits, mynbits, find_chunk, &s);
         }
         if (err) {
             st.err = err;

@@ -16,6 +16,9 @@ if [ "${1:-}" = build ]; then
           u8_plain) f="-DLAC_UNROLL=8 -DLAC_NT=0";; u16_plain) f="-DLAC_UNROLL=16 -DLAC_NT=0";;
           u4_nt) f="-DLAC_UNROLL=4 -DLAC_NT=1";;
           imax0) f="-DLAC_Q1_IMAX=0";;
+          xpf0) f="-DLAC_XPF=0";; xpf1) f="-DLAC_XPF=1 -DLAC_PIPE=0";; xpf1w2) f="-DLAC_XPF=1 -DLAC_PIPE=0 -DLAC_ENC_MINW=2";;
+          dxpf) f="-DLAC_DEC_XPF=1";; dstream) f="-DLAC_DEC_STREAM_ONLY=1";; dxpfw2) f="-DLAC_DEC_XPF=1 -DLAC_DECF_MINW=2";;
+          pipe1w2) f="-DLAC_XPF=1 -DLAC_PIPE=1 -DLAC_ENC_MINW=2";;
           q1u4) f="-DLAC_Q1_UNROLL=4";; q1u2) f="-DLAC_Q1_UNROLL=2";; q1u16) f="-DLAC_Q1_UNROLL=16";;
           q1nt1) f="-DLAC_Q1_NT1=1";; q1plain) f="-DLAC_Q1_NT2=0";; q1w2) f="-DLAC_Q1_MINW=2";;
           q1u4w2) f="-DLAC_Q1_UNROLL=4 -DLAC_Q1_MINW=2";; q1u4w3) f="-DLAC_Q1_UNROLL=4 -DLAC_Q1_MINW=3";;
