@@ -469,3 +469,48 @@ def test_decode_wave_granularity(V, bits):
         c.decode_open()
         assert torch.equal(c.decode(pmf), sym), nw
     c.close()
+
+
+@pytest.mark.parametrize("prec", [20, 33, 34, 48])
+def test_edge_u64_large_entries_minp_beyond_32_bits(prec):
+    """u64 rows whose smallest positive entry is >= 2^32: the decoders find minp
+    with 32-bit keys, so such rows take the exact 64-bit re-scan exactly when the
+    fudge test could flip (T > w * 2^32, below prec 34).  Fudged and unfudged
+    rows, every decode path, against the C oracle."""
+    from oracle import oracle as coracle
+    rng = np.random.default_rng(prec)
+    V, B, steps = 16, 8, 12
+    pmf = rng.integers(1 << 32, 1 << 40, size=(steps, B, V), dtype=np.uint64)
+    pmf[:, ::2, 3] = rng.integers(1 << 58, 1 << 59, size=(steps, B // 2), dtype=np.uint64)
+    pmf[::4, :, 5] = 0
+    pmf[:, 1, 7] = (1 << 32) - 1                                 # minp just below 2^32
+    sym = rng.integers(0, V, size=(steps, B)).astype(np.int32)
+    sym[::4][sym[::4] == 5] = 6
+    c, dpmf, data, n, tr = _gpu_encode(pmf, sym, prec)
+    out, nb, status, rc = coracle.encode_batch(pmf, sym, prec, nthreads=4)
+    assert rc == 0
+    for b in range(B):
+        assert int(n[b]) == int(nb[b]) and data[b] == out[b, :(int(nb[b]) + 7) // 8].tobytes(), b
+    assert (_decode_both(c, dpmf) == sym).all()
+
+
+def test_edge_u64_decode_total_at_2_64():
+    """Decoding against u64 rows whose totals are 2^64 - 1 (valid), exactly 2^64
+    with every high word summing below 2^32, and 2^64 + 5: the two overflowing
+    streams fail with LAC_E_TABLE on every decode path (the wrapped-total test)."""
+    V, B = 2, 3
+    rows = [[0x7FFFFFFFFFFFFFFF, 0x8000000000000001],           # T = 2^64, high words 2^32 - 1
+            [1 << 63, (1 << 63) - 1],                            # T = 2^64 - 1
+            [(1 << 63) + 3, (1 << 63) + 2]]                      # T = 2^64 + 5
+    pmf = np.array([rows], dtype=np.uint64)
+    bits = torch.zeros((B, 16), dtype=torch.uint8, device=DEV)
+    nbits = torch.full((B,), 64, dtype=torch.int64, device=DEV)
+    for path in DECODE_PATHS:
+        c = _coder(V, B, 48, bits=64)
+        c.set_decode_path(path)
+        c.decode_open(bits, nbits)
+        out = c.decode(_dev_pmf(pmf)).cpu().numpy()
+        rc, err, step = c.status()
+        assert err.tolist() == [-5, 0, -5], path
+        assert out[0].tolist()[0] == -1 and out[0].tolist()[2] == -1 and out[0].tolist()[1] >= 0, path
+        c.close()
