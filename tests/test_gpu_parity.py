@@ -223,6 +223,37 @@ def test_headline_shape_softmax_tables():
             assert data[b][-1] & ((1 << (8 - L % 8)) - 1) == 0
 
 
+def test_c4_shape_softmax_tables():
+    """SURVEY c4 at full size (V=128256 Llama-3 vocab, 4096 streams, u32 rows of
+    513 KB): fused and split encoders byte-identical, sampled streams bit-exact
+    against the C oracle, every stream round-trips through the AUTO decoder and the
+    per-step decoder, and the bit counts sum to the same total both ways."""
+    from oracle import oracle as coracle
+    V, B, steps, prec = 128256, 4096, 2, 48
+    pmf, sym = synth.softmax_tables(steps, B, V, seed=4242, device=DEV)
+    c = _coder(V, B, prec, cap=steps * (prec + 2) + 256)
+    c.encode_job(pmf, sym)
+    data, n = c.to_bytes()
+    c2 = _coder(V, B, prec, cap=steps * (prec + 2) + 256)
+    c2.set_path("split")
+    c2.encode(pmf, sym)
+    c2.finish()
+    d2, n2 = c2.to_bytes()
+    assert d2 == data and (n2 == n).all()
+    c2.close()
+    sample = list(range(0, B, 331)) + [B - 1]
+    sub = pmf[:, sample, :].cpu().numpy().view(np.uint32)
+    out, nb, status, rc = coracle.encode_batch(sub, sym[:, sample].cpu().numpy(), prec, nthreads=16)
+    assert rc == 0
+    for i, b in enumerate(sample):
+        assert int(n[b]) == int(nb[i]) and data[b] == out[i, :(int(nb[i]) + 7) // 8].tobytes(), b
+    for path in ("auto", "split"):
+        c.set_decode_path(path)
+        c.decode_open()
+        assert torch.equal(c.decode(pmf), sym), path
+    c.close()
+
+
 # ---------------------------------------------------------------- errors
 @pytest.mark.parametrize("path", ["split", "fused"])
 def test_error_symbol_range(path):
