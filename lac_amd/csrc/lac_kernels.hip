@@ -1888,10 +1888,43 @@ __device__ inline int q_index(int lane) {                   // lane bit b -> ind
     return idx;
 }
 
+
+// Row loads of k_q1_stats, two forms (RowSrc<BUF>):
+//  BUF: a buffer load off one resource per row (wave-uniform row base in SGPRs,
+//    one 32-bit offset VGPR per load instead of a 64-bit address), always issued:
+//    lanes beyond the row load the row's last vector.  A predicated load
+//    (`vi < nvec ? load : -inf`) compiles to an exec-masked branch, or a select
+//    the compiler sinks below later loads; either way it ends in a vmcnt(0) that
+//    waits for every load in flight -- it serialised the rolling prefetch behind
+//    its own loads.  No select is needed: a duplicate of a row element cannot
+//    change the row maximum, and the sums mask out-of-row vectors themselves
+//    (take()).  Measured c3 bf16 0.710 -> 0.660 ms, f32 1.33 -> 1.25 ms.
+//  !BUF: the predicated global load with the neutral -inf.  Kept for the
+//    16-vector-per-thread shapes (V = 128256), which sit at the 128-VGPR cap:
+//    there the buffer form's extra live offsets spill (3.35 -> 3.57 ms, bf16 c4).
+// Callers pass a valid (uniform) row base for rows past the job.
 __device__ inline u32x4 neg_inf16(int type_bytes) {
     const uint32_t w = type_bytes == 2 ? 0xFF80FF80u : 0xFF800000u;
     return u32x4{w, w, w, w};
 }
+template <bool BUF, int TB> struct RowSrc;
+template <int TB> struct RowSrc<true, TB> {
+    __amdgpu_buffer_rsrc_t rs;
+    int nvec;
+    __device__ RowSrc(const void *row, bool, int nv)
+        : rs(__builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(row), 0, nv * 16, 0x00020000)), nvec(nv) {}
+    __device__ u32x4 operator()(int vi) const {
+        const uint32_t v = (uint32_t)(vi < nvec ? vi : nvec - 1);
+        return __builtin_amdgcn_raw_buffer_load_b128(rs, v * 16u, 0, LAC_Q1_NT ? 2 : 0);   // 2 = nt (gfx950)
+    }
+};
+template <int TB> struct RowSrc<false, TB> {
+    const void *row;
+    bool ok;
+    int nvec;
+    __device__ RowSrc(const void *r, bool v, int nv) : row(r), ok(v), nvec(nv) {}
+    __device__ u32x4 operator()(int vi) const { return ok && vi < nvec ? ld16(row, vi, LAC_Q1_NT) : neg_inf16(TB); }
+};
 
 // k_q1_stats: the q1 row statistics.  Persistent blocks of 8 waves (two per CU:
 // the replicated table takes 68 KB of LDS per block) walk the rows r = t*B + b;
@@ -1908,13 +1941,10 @@ __device__ inline u32x4 neg_inf16(int type_bytes) {
 // in parallel and the sequential kernels only touch a few bytes per step.
 constexpr int kQ1Waves = 8;
 
-template <typename LT, int R>
-__device__ inline void q1_load_tile(u32x4 (&x)[R], const LT *row, bool valid, int base, int gt, int NT, int nvec) {
+template <int R, typename Src>
+__device__ inline void q1_load_tile(u32x4 (&x)[R], const Src &src, int base, int gt, int NT) {
 #pragma unroll
-    for (int j = 0; j < R; j++) {
-        const int vi = base + gt + NT * j;
-        x[j] = valid && vi < nvec ? ld16(row, vi, LAC_Q1_NT) : neg_inf16(sizeof(LT));
-    }
+    for (int j = 0; j < R; j++) x[j] = src(base + gt + NT * j);
 }
 
 template <typename LT, int RW, int R, bool DEC, bool MULTI, bool PF, int NWB>
@@ -1926,6 +1956,8 @@ __global__ __launch_bounds__(64 * NWB, 4) void k_q1_stats(const LT *__restrict__
                                                               float *__restrict__ mrow) {
     constexpr int N = LogitN<LT>::N, NT = 64 * RW, NR = NWB / RW;
     constexpr bool IMAX = LAC_Q1_IMAX && sizeof(LT) == 2 && NR == 1 && !MULTI;
+    constexpr bool BUF = R <= 8 && !MULTI;                    // row-load form (RowSrc)
+    typedef RowSrc<BUF, sizeof(LT)> Src;
     static_assert(R * N <= 128, "lane sums must fit 32 bits");
     __shared__ uint32_t tabr[LAC_Q1_TAB_SIZE * kQ1Rep];
     __shared__ float smax[NWB];
@@ -1935,7 +1967,7 @@ __global__ __launch_bounds__(64 * NWB, 4) void k_q1_stats(const LT *__restrict__
     __shared__ unsigned long long bins[DEC ? NR : 1][64];
     // in-row indices are 32-bit (vocab <= 2^31 entries); with one row per block
     // (RW = 8) the row pointer is provably wave-uniform (SGPR-based loads)
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, w = BUF ? wave_in_block() : tid >> 6;   // BUF: SGPR rows
     const int g = NR == 1 ? 0 : w / RW, wg = NR == 1 ? w : w % RW, gt = tid - g * NT;
     if (DEC && wg == 0) bins[g][lane] = 0;
     q1_load_tab_rep(tabr, xsh);
@@ -1947,34 +1979,31 @@ __global__ __launch_bounds__(64 * NWB, 4) void k_q1_stats(const LT *__restrict__
     u32x4 x[R];
     if (PF) {                                                  // first tile of the block's first row
         const int64_t r0 = (int64_t)blockIdx.x * NR + g;
-        q1_load_tile<LT, R>(x, r0 < rows ? row_of(r0) : lg, r0 < rows, 0, gt, NT, nvec);
+        q1_load_tile<R>(x, Src(r0 < rows ? row_of(r0) : lg, r0 < rows, nvec), 0, gt, NT);
     }
-    // one 16-B vector of a tile (neutral -inf beyond the row), for the rolling prefetches
-    auto ld_vec = [&](const LT *rw, bool ok, int tile, int j) {
-        const int vi = tile * NT * R + gt + NT * j;
-        return ok && vi < nvec ? ld16(rw, vi, LAC_Q1_NT) : neg_inf16(sizeof(LT));
-    };
+    // one 16-B vector of a tile, for the rolling prefetches
+    auto ld_vec = [&](const Src &src, int tile, int j) { return src(tile * NT * R + gt + NT * j); };
     for (int64_t rb = (int64_t)blockIdx.x * NR; rb < rows; rb += stride) {
         const int64_t r = rb + g;
         const bool valid = r < rows;
-        const LT *row = valid ? row_of(r) : lg;
+        const Src row(valid ? row_of(r) : lg, valid, nvec);
         float mx = -INFINITY;
         if (MULTI) {
             // PF: tile k+1's vector j loads into x[j] as soon as tile k's max has used it
             for (int tile = 0; tile < ntiles; tile++) {
-                if (!PF) q1_load_tile<LT, R>(x, row, valid, tile * NT * R, gt, NT, nvec);
+                if (!PF) q1_load_tile<R>(x, row, tile * NT * R, gt, NT);
 #pragma unroll
                 for (int j = 0; j < R; j++) {
 #pragma unroll
                     for (int e = 0; e < N; e++) mx = fmaxf(mx, logit_at<LT>(x[j], e));
                     if (PF && tile + 1 < ntiles) {
-                        x[j] = ld_vec(row, valid, tile + 1, j);
+                        x[j] = ld_vec(row, tile + 1, j);
                         __builtin_amdgcn_sched_barrier(0);
                     }
                 }
             }
         } else {
-            if (!PF) q1_load_tile<LT, R>(x, row, valid, 0, gt, NT, nvec);   // PF: loaded during the last row
+            if (!PF) q1_load_tile<R>(x, row, 0, gt, NT);   // PF: loaded during the last row
             if constexpr (!IMAX) {
 #pragma unroll
                 for (int j = 0; j < R; j++)
@@ -2047,7 +2076,7 @@ __global__ __launch_bounds__(64 * NWB, 4) void k_q1_stats(const LT *__restrict__
             for (int j = 0; j < R; j++) asm volatile("" : "+v"(x[j]));
         }
         for (int tile = ntiles - 1; tile >= 0; tile--) {
-            if (MULTI && !PF && tile != ntiles - 1) q1_load_tile<LT, R>(x, row, valid, tile * NT * R, gt, NT, nvec);
+            if (MULTI && !PF && tile != ntiles - 1) q1_load_tile<R>(x, row, tile * NT * R, gt, NT);
             uint32_t sv[R];
             auto take = [&](int j, uint32_t sl) {
                 const int vi = tile * NT * R + gt + NT * j;
@@ -2074,10 +2103,12 @@ __global__ __launch_bounds__(64 * NWB, 4) void k_q1_stats(const LT *__restrict__
             // the block's next row, so those loads overlap the rest of this row's work
             const int64_t rn = r + stride;
             const bool nvalid = rn < rows;
-            const LT *nrow = nvalid ? row_of(rn) : lg;
+            const bool down = MULTI && tile > 0;              // uniform
+            const Src rroll = down ? row : Src(nvalid ? row_of(rn) : lg, nvalid, nvec);
+            const int troll = down ? tile - 1 : 0;
             auto roll = [&](int j) {
                 if (PF) {                                      // tiles walk down: tile - 1, then the next row's tile 0
-                    x[j] = (MULTI && tile > 0) ? ld_vec(row, valid, tile - 1, j) : ld_vec(nrow, nvalid, 0, j);
+                    x[j] = ld_vec(rroll, troll, j);
                     __builtin_amdgcn_sched_barrier(0);         // keep the load after vector j's use
                 }
             };
@@ -2663,6 +2694,7 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
     if (sh == 10) return q1_stats_launch<LT, 16, 16, DEC, true, false, 16>(c, a, st);   // tiles of 16384
     if (sh == 11 && nvec <= 64 * 16 * 8) return q1_stats_launch<LT, 16, 8, DEC, false, true, 16>(c, a, st);
     if (sh == 12 && nvec <= 64 * 16 * 8) return q1_stats_launch<LT, 16, 8, DEC, false, false, 16>(c, a, st);
+    if (sh == 15 && nvec <= 64 * 16 * 16) return q1_stats_launch<LT, 16, 16, DEC, false, true, 16>(c, a, st);
     if (sh == 13) return q1_stats_launch<LT, 8, 8, DEC, true, true>(c, a, st);         // tiles of (8,8,y)
     if (sh == 14) return q1_stats_launch<LT, 16, 8, DEC, true, true, 16>(c, a, st);    // tiles of (16,8,y)
     if (sh == 8) return q1_stats_launch<LT, 8, 8, DEC, true, false>(c, a, st);      // tiles of 4096 vectors
