@@ -1968,7 +1968,8 @@ __global__ __launch_bounds__(64 * NWB, 4) void k_q1_stats(const LT *__restrict__
     // in-row indices are 32-bit (vocab <= 2^31 entries); with one row per block
     // (RW = 8) the row pointer is provably wave-uniform (SGPR-based loads)
     const int tid = threadIdx.x, lane = tid & 63, w = BUF ? wave_in_block() : tid >> 6;   // BUF: SGPR rows
-    const int g = NR == 1 ? 0 : w / RW, wg = NR == 1 ? w : w % RW, gt = tid - g * NT;
+    const int g = NR == 1 ? 0 : w / RW, wg = NR == 1 ? w : w % RW;
+    int gt = tid - g * NT;
     if (DEC && wg == 0) bins[g][lane] = 0;
     q1_load_tab_rep(tabr, xsh);
     const uint32_t loff = (uint32_t)(lane & 31) << 2;
@@ -1984,6 +1985,10 @@ __global__ __launch_bounds__(64 * NWB, 4) void k_q1_stats(const LT *__restrict__
     // one 16-B vector of a tile, for the rolling prefetches
     auto ld_vec = [&](const Src &src, int tile, int j) { return src(tile * NT * R + gt + NT * j); };
     for (int64_t rb = (int64_t)blockIdx.x * NR; rb < rows; rb += stride) {
+        // gt opaque per row: the R per-vector lane offsets / indices derived from it are
+        // recomputed (one add each) instead of hoisted out of the row loop, where
+        // 2R loop-invariant VGPRs spilled the 16-vector shapes
+        if (R > 8 && !DEC) asm volatile("" : "+v"(gt));          // (decode: measured neutral, spills more)
         const int64_t r = rb + g;
         const bool valid = r < rows;
         const Src row(valid ? row_of(r) : lg, valid, nvec);
@@ -2694,7 +2699,6 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
     if (sh == 10) return q1_stats_launch<LT, 16, 16, DEC, true, false, 16>(c, a, st);   // tiles of 16384
     if (sh == 11 && nvec <= 64 * 16 * 8) return q1_stats_launch<LT, 16, 8, DEC, false, true, 16>(c, a, st);
     if (sh == 12 && nvec <= 64 * 16 * 8) return q1_stats_launch<LT, 16, 8, DEC, false, false, 16>(c, a, st);
-    if (sh == 15 && nvec <= 64 * 16 * 16) return q1_stats_launch<LT, 16, 16, DEC, false, true, 16>(c, a, st);
     if (sh == 13) return q1_stats_launch<LT, 8, 8, DEC, true, true>(c, a, st);         // tiles of (8,8,y)
     if (sh == 14) return q1_stats_launch<LT, 16, 8, DEC, true, true, 16>(c, a, st);    // tiles of (16,8,y)
     if (sh == 8) return q1_stats_launch<LT, 8, 8, DEC, true, false>(c, a, st);      // tiles of 4096 vectors
