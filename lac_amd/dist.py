@@ -6,6 +6,8 @@ collective at all.  The only exchange is collecting the variable-length
 bitstreams afterwards: RCCL has no gather-v, so ranks
 first agree on the widest stream (an all-reduce MAX of one int64) and then
 all-gather fixed-width slots of that width plus the per-stream bit counts.
+Decoding reverses it: ``scatter_bitstreams`` hands each rank its shard of a
+job's bitstreams from the rank that holds them.
 With the ``nccl`` backend (RCCL on ROCm) the tensors stay in HBM and move
 over xGMI; with ``gloo`` (tests) they are CPU tensors.
 """
@@ -48,6 +50,55 @@ def gather_bitstreams(bits, nbits, group=None):
     _all_gather(out_bits, slot, group, world)
     _all_gather(out_n, nbits.contiguous(), group, world)
     return out_bits, out_n
+
+
+def scatter_bitstreams(all_bits=None, all_nbits=None, total_streams=None, src=0, group=None, device=None):
+    """Decode side of the exchange: rank ``src`` holds every
+    stream's packed bits ``[total, width]`` (uint8, a gathered job or a stored
+    one) and bit counts ``[total]`` (int64); every rank receives its own
+    contiguous shard ``shard_range(total, rank, world)`` and decodes it
+    independently (``BatchCoder.decode_open(bits, nbits)``).  Non-source ranks
+    pass ``None`` for the tensors; shapes travel in one broadcast.  Shards are
+    padded to the largest one so the scatter moves equal-sized slots.
+    Returns ``(bits [hi - lo, width], nbits [hi - lo])`` on every rank.
+    """
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    gloo = dist.get_backend(group) == "gloo"
+    if rank == src:
+        device = all_bits.device
+    dev = torch.device("cpu") if gloo else torch.device(device if device is not None else "cuda")
+    hdr = torch.zeros(2, dtype=torch.int64, device=dev)
+    if rank == src:
+        hdr[0], hdr[1] = all_bits.shape[0], all_bits.shape[1]
+    dist.broadcast(hdr, src=src, group=group)
+    total, width = int(hdr[0]), int(hdr[1])
+    if total_streams is not None and total_streams != total:
+        raise ValueError(f"source holds {total} streams, caller expected {total_streams}")
+    S = max(hi - lo for lo, hi in (shard_range(total, r, world) for r in range(world)))
+    lo, hi = shard_range(total, rank, world)
+    out_b = torch.empty((S, width), dtype=torch.uint8, device=dev)
+    out_n = torch.empty((S,), dtype=torch.int64, device=dev)
+    sb = sn = None
+    if rank == src:
+        hb, hn = (all_bits.cpu(), all_nbits.cpu()) if gloo else (all_bits, all_nbits.to(torch.int64))
+        sb, sn = [], []
+        for r in range(world):
+            a, z = shard_range(total, r, world)
+            pb = torch.zeros((S, width), dtype=torch.uint8, device=hb.device)
+            pn = torch.zeros((S,), dtype=torch.int64, device=hn.device)
+            pb[:z - a] = hb[a:z]
+            pn[:z - a] = hn[a:z]
+            sb.append(pb)
+            sn.append(pn)
+    dist.scatter(out_b, sb, src=src, group=group)
+    dist.scatter(out_n, sn, src=src, group=group)
+    out_b, out_n = out_b[:hi - lo], out_n[:hi - lo]
+    if gloo and device is not None and torch.device(device).type != "cpu":
+        out_b, out_n = out_b.to(device), out_n.to(device)
+    return out_b.contiguous(), out_n.contiguous()
 
 
 def _all_gather(out, inp, group, world):

@@ -7,7 +7,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from lac_amd.dist import BitstreamGatherer, gather_bitstreams, shard_range
+from lac_amd.dist import BitstreamGatherer, gather_bitstreams, scatter_bitstreams, shard_range
 
 
 def _free_port():
@@ -118,3 +118,46 @@ def test_bitstream_gatherer_gloo_world2():
         b1, n1, ob1, on1 = res[1][j]
         assert ob0 == ob1 == b0 + b1                    # fixed-width slots: every byte travels
         assert on0 == on1 == n0 + n1
+
+
+def _scatter_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # a job of 7 streams (uneven shards 3 + 4) held by rank 0 is scattered ...
+    g = torch.Generator().manual_seed(7)
+    total, width = 7, 24
+    nbits = torch.randint(0, width * 8 + 1, (total,), generator=g, dtype=torch.int64)
+    bits = torch.randint(0, 256, (total, width), generator=g, dtype=torch.uint8)
+    mb, mn = scatter_bitstreams(bits if rank == 0 else None, nbits if rank == 0 else None, total_streams=total)
+    # ... and an even job's shards gathered back reproduce it (gather pads to the
+    # widest stream of the job, so compare the bytes every stream owns)
+    eb, en = scatter_bitstreams(bits[:6] if rank == 0 else None, nbits[:6] if rank == 0 else None)
+    ab, an = gather_bitstreams(eb, en)
+    q.put((rank, mb.tolist(), mn.tolist(), bits.tolist(), nbits.tolist(), ab.tolist(), an.tolist()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_scatter_bitstreams_gloo_world2():
+    """Decode-side exchange: uneven shards of a job held by rank 0, then the
+    gather of those shards round-trips to the source job."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_scatter_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict((r[0], r[1:]) for r in (q.get(timeout=120) for _ in range(2)))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    bits, nbits = res[0][2], res[0][3]
+    for rank in (0, 1):
+        lo, hi = shard_range(7, rank, 2)
+        mb, mn = res[rank][0], res[rank][1]
+        assert mn == nbits[lo:hi] and mb == bits[lo:hi]
+        ab, an = res[rank][4], res[rank][5]
+        assert an == nbits[:6]
+        for i, n in enumerate(nbits[:6]):
+            assert ab[i][:(n + 7) // 8] == bits[i][:(n + 7) // 8]
