@@ -1783,14 +1783,20 @@ __device__ inline uint32_t q1_val(float x, float c, const uint32_t *tab) { retur
 // banks (bank = dword mod 32); lane l reads copy l & 31, so every lookup of a
 // group hits 32 distinct banks whatever the indices -- no bank conflicts for the
 // random gather (a single shared copy measured 68 % conflict cycles).
-constexpr int kQ1Rep = 32;
+#ifndef LAC_Q1_REP
+#define LAC_Q1_REP 32            // table copies (power of two <= 32): lane l reads copy l % REP
+#endif
+#ifndef LAC_Q1_MINW
+#define LAC_Q1_MINW 4            // k_q1_stats launch bound: waves per SIMD
+#endif
+constexpr int kQ1Rep = LAC_Q1_REP;
 __device__ inline void q1_load_tab_rep(uint32_t *tabr, uint32_t xsh) {
     for (int i = threadIdx.x; i < LAC_Q1_TAB_SIZE * kQ1Rep; i += blockDim.x) tabr[i] = q1_entry(i / kQ1Rep, xsh);
     __syncthreads();
 }
 
 __device__ inline uint32_t q1_rep_at(const uint32_t *tabr, uint32_t j, uint32_t loff) {
-    return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(tabr) + ((j << 7) | loff));
+    return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(tabr) + ((j * (kQ1Rep * 4)) | loff));
 }
 
 // Sum of q1 over the N logits of one 16-B vector (replicated table, loff = byte
@@ -1948,7 +1954,7 @@ __device__ inline void q1_load_tile(u32x4 (&x)[R], const Src &src, int base, int
 }
 
 template <typename LT, int RW, int R, bool DEC, bool MULTI, bool PF, int NWB>
-__global__ __launch_bounds__(64 * NWB, 4) void k_q1_stats(const LT *__restrict__ lg, int64_t step_stride,
+__global__ __launch_bounds__(64 * NWB, LAC_Q1_MINW) void k_q1_stats(const LT *__restrict__ lg, int64_t step_stride,
                                                               int64_t stream_stride, const int32_t *__restrict__ sym,
                                                               int64_t B, int64_t rows, int64_t V, int64_t t0,
                                                               uint32_t xsh, int64_t G, RowStats *__restrict__ out,
@@ -1972,7 +1978,7 @@ __global__ __launch_bounds__(64 * NWB, 4) void k_q1_stats(const LT *__restrict__
     int gt = tid - g * NT;
     if (DEC && wg == 0) bins[g][lane] = 0;
     q1_load_tab_rep(tabr, xsh);
-    const uint32_t loff = (uint32_t)(lane & 31) << 2;
+    const uint32_t loff = (uint32_t)(lane & (kQ1Rep - 1)) << 2;
     const int nvec = (int)(V / N);
     const int ntiles = MULTI ? (nvec + NT * R - 1) / (NT * R) : 1;
     const int64_t stride = (int64_t)gridDim.x * NR;
@@ -2684,9 +2690,11 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
     if (sh == 0) {                     // decode: the prefetching (8,8) spills around the multi-sum
         static const int enc_order[] = {1, 2, 3, 6, 5}, dec_order[] = {1, 2, 3, 4, 5};
         for (int i : DEC ? dec_order : enc_order) {
-            // f32 encode rows of 4097..8192 vectors: one 16-wave block per CU with rolling
-            // prefetch, (16,8,y) = shape 11, before (8,16,n) (c3 f32: 1.33 vs 1.39 ms)
-            if (!DEC && sizeof(LT) == 4 && i == 5 && nvec <= 64 * 16 * 8) { sh = 11; break; }
+            // f32 rows of 4097..8192 vectors: one 16-wave block per CU with rolling
+            // prefetch, (16,8,y) = shape 11, before (8,16,n) (c3 f32: encode 1.33 vs
+            // 1.39 ms; decode, once the buffer-form loads removed its spills, 45.0 vs
+            // 40.9 M sym/s end to end, profiles/r02/q1_dec_shapes/)
+            if (sizeof(LT) == 4 && i == 5 && nvec <= 64 * 16 * 8) { sh = 11; break; }
             if (holds(i)) { sh = i; break; }
         }
         // measured at V = 128256 f32: encode tiles of (16,8) with the tile-rolling
