@@ -1790,13 +1790,15 @@ __device__ inline uint32_t q1_val(float x, float c, const uint32_t *tab) { retur
 #define LAC_Q1_MINW 4            // k_q1_stats launch bound: waves per SIMD
 #endif
 constexpr int kQ1Rep = LAC_Q1_REP;
+template <int REP = kQ1Rep>
 __device__ inline void q1_load_tab_rep(uint32_t *tabr, uint32_t xsh) {
-    for (int i = threadIdx.x; i < LAC_Q1_TAB_SIZE * kQ1Rep; i += blockDim.x) tabr[i] = q1_entry(i / kQ1Rep, xsh);
+    for (int i = threadIdx.x; i < LAC_Q1_TAB_SIZE * REP; i += blockDim.x) tabr[i] = q1_entry(i / REP, xsh);
     __syncthreads();
 }
 
+template <int REP = kQ1Rep>
 __device__ inline uint32_t q1_rep_at(const uint32_t *tabr, uint32_t j, uint32_t loff) {
-    return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(tabr) + ((j * (kQ1Rep * 4)) | loff));
+    return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(tabr) + ((j * (REP * 4)) | loff));
 }
 
 // Sum of q1 over the N logits of one 16-B vector (replicated table, loff = byte
@@ -1805,7 +1807,7 @@ __device__ inline uint32_t q1_rep_at(const uint32_t *tabr, uint32_t j, uint32_t 
 // a lane's sum of up to 128 entries fits 32 bits.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-template <typename LT>
+template <typename LT, int REP = kQ1Rep>
 __device__ inline uint32_t q1_vec_sum(const u32x4 &x, float c, bool fast, const uint32_t *tabr, uint32_t loff) {
     constexpr int N = LogitN<LT>::N;
     uint32_t s = 0;
@@ -1815,12 +1817,12 @@ __device__ inline uint32_t q1_vec_sum(const u32x4 &x, float c, bool fast, const 
         for (int j = 0; j < N; j += 2) {
             const f32x2 v = {logit_at<LT>(x, j), logit_at<LT>(x, j + 1)};
             const f32x2 y = __builtin_elementwise_fma(v, k, cc);
-            s += q1_rep_at(tabr, cvt_sat_u32(y.x), loff);
-            s += q1_rep_at(tabr, cvt_sat_u32(y.y), loff);
+            s += q1_rep_at<REP>(tabr, cvt_sat_u32(y.x), loff);
+            s += q1_rep_at<REP>(tabr, cvt_sat_u32(y.y), loff);
         }
     } else {
 #pragma unroll
-        for (int j = 0; j < N; j++) s += q1_rep_at(tabr, q1_j(logit_at<LT>(x, j), c), loff);
+        for (int j = 0; j < N; j++) s += q1_rep_at<REP>(tabr, q1_j(logit_at<LT>(x, j), c), loff);
     }
     return s;
 }
@@ -2163,6 +2165,244 @@ __global__ __launch_bounds__(64 * NWB, LAC_Q1_MINW) void k_q1_stats(const LT *__
             out[r] = st;
         }
     }
+}
+
+// k_q1_stats_rl: the q1 row statistics for rows of 8193..16384 16-B vectors (bf16
+// V <= 131072 -- the Llama-3 c4 vocab 128256 -- and f32 V <= 65536), whose one
+// row fills the register file of a CU.  One 16-wave block per CU; thread t holds
+// vectors j*1024 + t of its row: j < 8 in registers, j >= 8 in its own LDS slots
+// (slot k of wave w at [k*1024 + w*64, +64), written by global_load_lds, so
+// the in-flight data of the next row needs no VGPRs).  Pass 2 rolls both halves
+// to the block's next row as it consumes them -- an LDS slot right after its
+// read, a register vector right after its use -- so the next row streams in
+// while this one is quantised, instead of a CU alternating between loading a
+// whole row and computing it (shape 9, 65 % of peak at c4 bf16).  LDS: 8 table
+// copies (17 KB; 16 or 32 copies measured no faster at c3) + 128 KB of slots.
+// Same outputs as k_q1_stats (RowStats, or row max + 64 chunk totals).
+constexpr int kRLRep = 8;
+typedef __attribute__((address_space(3))) void lvoid_t;
+
+template <typename LT, bool DEC>
+__global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ lg, int64_t step_stride,
+                                                         int64_t stream_stride, const int32_t *__restrict__ sym,
+                                                         int64_t B, int64_t rows, int64_t V, int64_t t0, uint32_t xsh,
+                                                         int64_t G, RowStats *__restrict__ out,
+                                                         uint64_t *__restrict__ chunks, float *__restrict__ mrow) {
+    constexpr int N = LogitN<LT>::N, NT = 1024, R = 8, L = 8, NW = 16;
+    constexpr bool IMAX = LAC_Q1_IMAX && sizeof(LT) == 2;
+    static_assert((R + L) * N <= 128, "lane sums must fit 32 bits");
+    __shared__ uint32_t tabr[LAC_Q1_TAB_SIZE * kRLRep];
+    __shared__ u32x4 slots[L * NT];
+    __shared__ float smax[NW];
+    __shared__ int smaxi[NW];
+    __shared__ uint64_t ssum[NW][2];
+    __shared__ uint32_t sps;
+    __shared__ unsigned long long bins[DEC ? 64 : 1];
+    int tid = threadIdx.x;
+    const int lane = tid & 63, w = wave_in_block();
+    if (DEC && w == 0) bins[lane] = 0;
+    q1_load_tab_rep<kRLRep>(tabr, xsh);
+    const uint32_t loff = (uint32_t)(lane & (kRLRep - 1)) << 2;
+    const int nvec = (int)(V / N);
+    const int64_t stride = gridDim.x;
+    auto row_of = [&](int64_t r) { return lg + (t0 + r / B) * step_stride + (r % B) * stream_stride; };
+    // vector j of this thread (clamped into the row: a duplicate cannot change the
+    // maximum, and the sums mask out-of-row vectors)
+    auto vidx = [&](int j) { const int vi = j * NT + tid; return vi < nvec ? vi : nvec - 1; };
+    auto ld_reg = [&](const RowSrc<true, sizeof(LT)> &src, int j) { return src(j * NT + tid); };
+    // LDS-DMA as asm: the compiler's own global_load_lds makes every later LDS read
+    // wait vmcnt(0) (it cannot tell the slots apart), which serialised the refills.
+    // The asm is invisible to its wait counting, so this kernel waits explicitly:
+    // vmcnt(0) before pass 1 reads any slot, lgkmcnt(0) before a slot is refilled.
+    const uint32_t slot_base = (uint32_t)(uintptr_t)(lvoid_t *)&slots[w * 64];   // wave-uniform LDS address
+    auto ld_lds = [&](const LT *rw, int k) {
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(rw) + vidx(R + k);
+        uint32_t keep;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(src), "s"(slot_base + (uint32_t)(k * NT * 16))
+                     : "memory");
+    };
+    u32x4 x[R];
+    {                                                          // the block's first row
+        const int64_t r0 = blockIdx.x;
+        const LT *rw = r0 < rows ? row_of(r0) : lg;
+        const RowSrc<true, sizeof(LT)> src(rw, true, nvec);
+#pragma unroll
+        for (int k = 0; k < L; k++) ld_lds(rw, k);
+#pragma unroll
+        for (int j = 0; j < R; j++) x[j] = ld_reg(src, j);
+    }
+    for (int64_t r = blockIdx.x; r < rows; r += stride) {
+        // tid opaque per row: the per-load addresses derived from it are recomputed
+        // next to each load, not hoisted out of the loop and spilled (a spill reload
+        // is a VM load: its vmcnt(0) would drain the prefetches)
+        asm volatile("" : "+v"(tid));
+        const int64_t rn = r + stride;
+        const LT *nrow = rn < rows ? row_of(rn) : lg;
+        // pass 1: the row maximum over registers and slots (everything has landed)
+        __builtin_amdgcn_s_waitcnt(0);                         // this wave's LDS-DMA writes (asm: untracked)
+        asm volatile("" ::: "memory");
+        // slot vectors are read where used (not held across the barrier: registers)
+        auto slot = [&](int k) { return slots[k * NT + tid]; };
+        float m;
+        if constexpr (IMAX) {
+            s16x2 pm = {(short)-32768, (short)-32768};
+            auto pmax = [&](const u32x4 &v) {
+                pm = __builtin_elementwise_max(pm, as_s16x2(v.x));
+                pm = __builtin_elementwise_max(pm, as_s16x2(v.y));
+                pm = __builtin_elementwise_max(pm, as_s16x2(v.z));
+                pm = __builtin_elementwise_max(pm, as_s16x2(v.w));
+            };
+#pragma unroll
+            for (int j = 0; j < R; j++) pmax(x[j]);
+#pragma unroll
+            for (int k = 0; k < L; k++) pmax(slot(k));
+            const int li = pm.x > pm.y ? (int)pm.x : (int)pm.y;
+            const int wi = (int)wave_reduce((uint32_t)li, [](uint32_t a, uint32_t b) {
+                return (uint32_t)((int)a > (int)b ? (int)a : (int)b);
+            });
+            if (lane == 0) smaxi[w] = wi;
+            if (!DEC && tid == 0) sps = 0;
+            __syncthreads();
+            int bi = smaxi[0];
+#pragma unroll
+            for (int i = 1; i < NW; i++) bi = smaxi[i] > bi ? smaxi[i] : bi;
+            if (bi >= 0 && bi <= 0x7F80) {                    // block-uniform (see k_q1_stats)
+                m = __uint_as_float((uint32_t)bi << 16);
+            } else {
+                float mx = -INFINITY;
+#pragma unroll
+                for (int j = 0; j < R; j++)
+#pragma unroll
+                    for (int e = 0; e < N; e++) mx = fmaxf(mx, logit_at<LT>(x[j], e));
+#pragma unroll
+                for (int k = 0; k < L; k++) {
+                    const u32x4 v = slot(k);
+#pragma unroll
+                    for (int e = 0; e < N; e++) mx = fmaxf(mx, logit_at<LT>(v, e));
+                }
+                mx = wave_max_f32(mx);
+                if (lane == 0) smax[w] = mx;
+                __syncthreads();
+                m = smax[0];
+#pragma unroll
+                for (int i = 1; i < NW; i++) m = fmaxf(m, smax[i]);
+            }
+        } else {
+            float mx = -INFINITY;
+#pragma unroll
+            for (int j = 0; j < R; j++)
+#pragma unroll
+                for (int e = 0; e < N; e++) mx = fmaxf(mx, logit_at<LT>(x[j], e));
+#pragma unroll
+            for (int k = 0; k < L; k++) {
+                const u32x4 v = slot(k);
+#pragma unroll
+                for (int e = 0; e < N; e++) mx = fmaxf(mx, logit_at<LT>(v, e));
+            }
+            mx = wave_max_f32(mx);
+            if (lane == 0) smax[w] = mx;
+            if (!DEC && tid == 0) sps = 0;
+            __syncthreads();
+            m = smax[0];
+#pragma unroll
+            for (int i = 1; i < NW; i++) m = fmaxf(m, smax[i]);
+        }
+        const bool fast = q1_fast_row(m);
+        const float c = q1_c(m);
+        int sfull = -1, sr = 0;
+        if (!DEC) {
+            const int64_t s = sym[(t0 + r / B) * B + r % B];
+            const int sc = (int)(s < 0 ? 0 : (s > V ? V : s));
+            sfull = sc / N;
+            sr = sc - sfull * N;
+        }
+        uint32_t tot = 0, lo = 0, sv[8];                     // DEC: one half's vector sums
+        if (!DEC && sfull < nvec && (sfull & (NT - 1)) == tid) {
+            // the vector holding s, split once before pass 2 (both halves still hold
+            // this row): one copy of this code instead of one per vector in pass 2
+            const int js = sfull / NT;
+            u32x4 v = js >= R ? slot(js - R) : x[0];
+#pragma unroll
+            for (int jj = 1; jj < R; jj++) v = js == jj ? x[jj] : v;
+            uint32_t pl = 0, ps = 0;
+#pragma unroll
+            for (int e = 0; e < N; e++) {
+                const uint32_t q = q1_rep_at<kRLRep>(tabr, q1_j(logit_at<LT>(v, e), c), loff);
+                pl += e < sr ? q : 0;
+                ps += e == sr ? q : 0;
+            }
+            lo = pl;
+            sps = ps;
+        }
+        // pass 2 (slots first, so their refills are issued earliest)
+        auto take = [&](int j, const u32x4 &v, uint32_t sl) {
+            const int vi = j * NT + tid;
+            sl = vi < nvec ? sl : 0;
+            if (DEC) {
+                sv[j & 7] = sl;
+            } else {
+                tot += sl;
+                lo += vi < sfull ? sl : 0;
+            }
+            (void)v;
+        };
+        const RowSrc<true, sizeof(LT)> nsrc(nrow, true, nvec);
+        // DEC: the 64-vector group totals of one half (vectors j0 .. j0+7) into the bins
+        auto bin_half = [&](int j0) {
+            const uint64_t gsum = wave_multi_sum32<8>(sv);     // lane l < 8: index q_index<8>(l)
+            if (lane < 8) {
+                const int grp = w + NW * (j0 + q_index<8>(lane));   // vectors [grp*64, grp*64 + 64)
+                if (grp * 64 < nvec) atomicAdd(&bins[grp / (int)G], (unsigned long long)gsum);
+            }
+        };
+        auto pass2 = [&](bool fs) {
+#pragma unroll
+            for (int k = 0; k < L; k++) {
+                const u32x4 v = slot(k);
+                take(R + k, v, q1_vec_sum<LT, kRLRep>(v, c, fs, tabr, loff));
+                __builtin_amdgcn_s_waitcnt(0xc07f);           // lgkmcnt(0): this wave's reads of slot k are done
+                ld_lds(nrow, k);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            if (DEC) bin_half(R);
+#pragma unroll
+            for (int j = 0; j < R; j++) {
+                take(j, x[j], q1_vec_sum<LT, kRLRep>(x[j], c, fs, tabr, loff));
+                x[j] = ld_reg(nsrc, j);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            if (DEC) bin_half(0);
+        };
+        if (fast) pass2(true); else pass2(false);             // row-uniform
+        if (!DEC) {
+            const uint64_t t64 = wave_sum_u64(tot), l64 = wave_sum_u64(lo);
+            if (lane == 0) { ssum[w][0] = t64; ssum[w][1] = l64; }
+        }
+        __syncthreads();
+        if (DEC) {
+            if (w == 0) {
+                chunks[r * 64 + lane] = bins[lane];
+                bins[lane] = 0;
+                if (lane == 0) mrow[r] = m;
+            }
+        } else if (tid == 0) {
+            uint64_t T = 0, Ls = 0;
+#pragma unroll
+            for (int i = 0; i < NW; i++) { T += ssum[i][0]; Ls += ssum[i][1]; }
+            RowStats st;
+            st.lo = Ls;
+            st.hi = Ls + sps;
+            st.tot = T;
+            st.minp = 1;
+            st.inv_tot = 1.0 / (double)T;
+            st.pad = 0;
+            out[r] = st;
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0);                             // no LDS-DMA outlives the block
+    asm volatile("" ::: "memory");
 }
 
 // k_q1_decode: one wave per stream, sequential over a chunk of steps, from the
@@ -2671,6 +2911,18 @@ static int q1_stats_launch(lac_ctx *c, const Q1Args &a, hipStream_t st) {
     return LAC_OK;
 }
 
+template <typename LT, bool DEC>
+static int q1_stats_rl_launch(lac_ctx *c, const Q1Args &a, hipStream_t st) {
+    const int64_t need = a.rows, cap = (int64_t)c->cus;     // one 16-wave block per CU
+    const unsigned grid = (unsigned)(need < cap ? need : cap);
+    const int64_t nvec = c->V / LogitN<LT>::N;
+    ProfScope ps(c, KID_Q1_STATS, st);
+    k_q1_stats_rl<LT, DEC><<<grid, 1024, 0, st>>>((const LT *)a.lg, a.ss, a.bs, a.sym, c->B, a.rows, c->V, a.t0,
+                                                   a.xsh, q1_groups_per_chunk(nvec), c->stats, c->q1chunks, c->q1m);
+    CHECK_LAUNCH();
+    return LAC_OK;
+}
+
 // Row-group shapes (waves per row RW, 16-B vectors per thread R, rolling
 // prefetch) of k_q1_stats.  AUTO takes the first listed shape that holds the row
 // in registers (measured on MI355X, c3 shape: encode bf16 (8,8,y) 0.75 ms vs
@@ -2697,6 +2949,11 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
             if (sizeof(LT) == 4 && i == 5 && nvec <= 64 * 16 * 8) { sh = 11; break; }
             if (holds(i)) { sh = i; break; }
         }
+        // rows of 8193..16384 vectors: registers + LDS slots (shape 15; same-box, bf16
+        // V = 128256 encode 3.23 -> 2.49 ms = 84 % of peak, f32 V = 65536 encode 2.73 ->
+        // 2.43 ms, decode 21.5 -> 24.0 M sym/s; bf16 decode keeps shape 9 (17.9 vs 15.9 M
+        // sym/s: the decode form spills), profiles/r02/q1_rl/)
+        if (sh == 0 && nvec <= 16384 && !(DEC && sizeof(LT) == 2)) sh = 15;
         // measured at V = 128256 f32: encode tiles of (16,8) with the tile-rolling
         // prefetch 1.98 ms vs 2.18 for tiles of (8,8) (shape 13, its (8,8) form: 2.20)
         if (sh == 0) sh = nvec <= 64 * 16 * 16 ? 9 : (DEC ? 10 : (sizeof(LT) == 4 ? 14 : 8));
@@ -2707,10 +2964,14 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
     if (sh == 10) return q1_stats_launch<LT, 16, 16, DEC, true, false, 16>(c, a, st);   // tiles of 16384
     if (sh == 11 && nvec <= 64 * 16 * 8) return q1_stats_launch<LT, 16, 8, DEC, false, true, 16>(c, a, st);
     if (sh == 12 && nvec <= 64 * 16 * 8) return q1_stats_launch<LT, 16, 8, DEC, false, false, 16>(c, a, st);
+    if (sh == 15 && nvec <= 16384) return q1_stats_rl_launch<LT, DEC>(c, a, st);     // registers + LDS slots
     if (sh == 13) return q1_stats_launch<LT, 8, 8, DEC, true, true>(c, a, st);         // tiles of (8,8,y)
     if (sh == 14) return q1_stats_launch<LT, 16, 8, DEC, true, true, 16>(c, a, st);    // tiles of (16,8,y)
     if (sh == 8) return q1_stats_launch<LT, 8, 8, DEC, true, false>(c, a, st);      // tiles of 4096 vectors
-    if (!holds(sh)) return fail(LAC_E_ARG, "q1 shape %d does not hold a row of %lld vectors", sh, (long long)nvec);
+    // shapes 9, 11, 12, 15 with a row too long for them, and 1..7 likewise (kQ1Shapes
+    // describes 1..7 only: a forced 11 / 12 used to index past it)
+    if (sh > 7 || !holds(sh))
+        return fail(LAC_E_ARG, "q1 shape %d does not hold a row of %lld vectors", sh, (long long)nvec);
     switch (sh) {
     case 1: return q1_stats_launch<LT, 1, 4, DEC, false, false>(c, a, st);
     case 2: return q1_stats_launch<LT, 2, 8, DEC, false, false>(c, a, st);
@@ -2901,7 +3162,7 @@ int lac_set_option(lac_ctx *c, int option, int64_t value) {
         c->fine_decode = (int)value;
         return LAC_OK;
     case LAC_OPT_Q1_SHAPE:
-        if (value < 0 || value > 14) return fail(LAC_E_ARG, "bad q1 shape");
+        if (value < 0 || value > 15) return fail(LAC_E_ARG, "bad q1 shape");
         c->q1_shape = (int)value;
         return LAC_OK;
     case LAC_OPT_MAPPING:
