@@ -197,6 +197,7 @@ def main():
              7: "k_q1_decode"}
     decode_info = {"symbols_per_s": B * T / (d1 - d0), "kernel": "+".join(names[k] for k in dkids),
                    "kernel_ms_per_step": dstep_ms,
+                   "kernel_ms_per_step_each": {names[k]: dms[k] / max(T, 1) for k in dkids},
                    "achieved_GBps": B * (V * ebytes + 4) / (dstep_ms * 1e-3) / 1e9 if dkids else None}
     round_trip = bool(torch.equal(dec, sym)) and rc == 0
     if dist:

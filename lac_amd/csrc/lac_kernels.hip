@@ -1790,10 +1790,40 @@ __device__ inline uint32_t q1_val(float x, float c, const uint32_t *tab) { retur
 #define LAC_Q1_MINW 4            // k_q1_stats launch bound: waves per SIMD
 #endif
 constexpr int kQ1Rep = LAC_Q1_REP;
+#ifndef LAC_Q1_FASTFILL
+#define LAC_Q1_FASTFILL 1        // replicated-table fill: loads first, 16-B LDS writes
+#endif
 template <int REP = kQ1Rep>
 __device__ inline void q1_load_tab_rep(uint32_t *tabr, uint32_t xsh) {
     for (int i = threadIdx.x; i < LAC_Q1_TAB_SIZE * REP; i += blockDim.x) tabr[i] = q1_entry(i / REP, xsh);
     __syncthreads();
+}
+// The same table, filled by a block of NTHR threads: entry i's REP copies are REP/4
+// 16-B writes, and each thread issues all of its constant-table loads before its
+// first write (the strided loop above ran 34 dependent load -> write rounds per
+// thread for 32 copies at 512 threads, before any row load was issued).
+template <int REP, int NTHR>
+__device__ inline void q1_fill_tab_rep(uint32_t *tabr, uint32_t xsh) {
+    if constexpr (!LAC_Q1_FASTFILL) {
+        q1_load_tab_rep<REP>(tabr, xsh);
+    } else {
+        static_assert(REP % 4 == 0, "16-B writes of copies");
+        constexpr int Q = REP / 4, ITEMS = LAC_Q1_TAB_SIZE * Q, IT = (ITEMS + NTHR - 1) / NTHR;
+        uint32_t v[IT];
+#pragma unroll
+        for (int k = 0; k < IT; k++) {
+            const int item = (int)threadIdx.x + k * NTHR;         // entry item / Q, copies 4 (item % Q) ..
+            v[k] = item < ITEMS ? c_q1_tab[kQ1L - item / Q] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < IT; k++) {
+            const int item = (int)threadIdx.x + k * NTHR;
+            uint32_t e = v[k] >> xsh;
+            e = e ? e : 1u;
+            if (item < ITEMS) reinterpret_cast<u32x4 *>(tabr)[item] = u32x4{e, e, e, e};
+        }
+        __syncthreads();
+    }
 }
 
 template <int REP = kQ1Rep>
@@ -1979,17 +2009,20 @@ __global__ __launch_bounds__(64 * NWB, LAC_Q1_MINW) void k_q1_stats(const LT *__
     const int g = NR == 1 ? 0 : w / RW, wg = NR == 1 ? w : w % RW;
     int gt = tid - g * NT;
     if (DEC && wg == 0) bins[g][lane] = 0;
-    q1_load_tab_rep(tabr, xsh);
-    const uint32_t loff = (uint32_t)(lane & (kQ1Rep - 1)) << 2;
     const int nvec = (int)(V / N);
     const int ntiles = MULTI ? (nvec + NT * R - 1) / (NT * R) : 1;
     const int64_t stride = (int64_t)gridDim.x * NR;
     auto row_of = [&](int64_t r) { return lg + (t0 + r / B) * step_stride + (r % B) * stream_stride; };
     u32x4 x[R];
-    if (PF) {                                                  // first tile of the block's first row
-        const int64_t r0 = (int64_t)blockIdx.x * NR + g;
+    if (PF) {                                                  // first tile of the block's first row,
+        const int64_t r0 = (int64_t)blockIdx.x * NR + g;      // in flight while the table fills
         q1_load_tile<R>(x, Src(r0 < rows ? row_of(r0) : lg, r0 < rows, nvec), 0, gt, NT);
     }
+    // the 16-vector shapes sit at the 128-VGPR cap: the fast fill's live loads spill them
+    // (bf16 V = 128256 decode stats 220 -> 283 us per step)
+    if constexpr (R > 8) q1_load_tab_rep<kQ1Rep>(tabr, xsh);
+    else q1_fill_tab_rep<kQ1Rep, 64 * NWB>(tabr, xsh);
+    const uint32_t loff = (uint32_t)(lane & (kQ1Rep - 1)) << 2;
     // one 16-B vector of a tile, for the rolling prefetches
     auto ld_vec = [&](const Src &src, int tile, int j) { return src(tile * NT * R + gt + NT * j); };
     for (int64_t rb = (int64_t)blockIdx.x * NR; rb < rows; rb += stride) {
@@ -2201,6 +2234,8 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
     int tid = threadIdx.x;
     const int lane = tid & 63, w = wave_in_block();
     if (DEC && w == 0) bins[lane] = 0;
+    // (the fast fill below the first row's loads, as in k_q1_stats, spilled this
+    // kernel at its 128-VGPR cap: 2.52 -> 2.70 ms at bf16 V = 128256)
     q1_load_tab_rep<kRLRep>(tabr, xsh);
     const uint32_t loff = (uint32_t)(lane & (kRLRep - 1)) << 2;
     const int nvec = (int)(V / N);
@@ -2426,10 +2461,15 @@ __global__ LAC_DEC_BOUNDS void k_q1_decode(const LT *__restrict__ lg, int64_t st
     const uint64_t mynbits = nbits[b];
     const int64_t nvec = V / N;
     uint64_t next = nsteps > 0 ? chunks[b * 64 + lane] : 0;
+    float mnext = nsteps > 0 ? mrow[b] : 0.f;
     for (int64_t i = 0; i < nsteps; i++) {
         const int64_t t = t0 + i, r = i * B + b;
         const uint64_t mine = next;
-        if (i + 1 < nsteps) next = chunks[(r + B) * 64 + lane];     // prefetch: independent of the state
+        const float mcur = mnext;
+        if (i + 1 < nsteps) {                                  // prefetch: independent of the state
+            next = chunks[(r + B) * 64 + lane];
+            mnext = mrow[r + B];
+        }
         int32_t *out = sym_out + t * B + b;
         if (st.err) {
             if (lane == 0) *out = -1;
@@ -2437,7 +2477,7 @@ __global__ LAC_DEC_BOUNDS void k_q1_decode(const LT *__restrict__ lg, int64_t st
         }
         const LT *row = lg + t * step_stride + b * stream_stride;
         const BitWin win = bit_window(mybits, mynbits, st.pos);    // in flight during the search
-        const float c = q1_c(mrow[r]);
+        const float c = q1_c(mcur);
         const uint64_t T = wave_sum_u64(mine);
         const uint64_t incl = wave_incl_scan_u64(mine);
         int err = 0;
