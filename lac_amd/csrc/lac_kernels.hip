@@ -80,6 +80,14 @@ constexpr int kWavesPerBlock = 4;     // 256-thread workgroups
 
 // ------------------------------------------------------------------ wave helpers
 __device__ inline uint32_t lane_id() { return __lane_id(); }
+// The lane index recomputed by two VALU ops where it is used: an asm result the
+// compiler cannot hoist, CSE or spill (a lane index held across a long loop at the
+// 128-VGPR cap was spilled, and its reload's vmcnt(0) drained the loads in flight).
+__device__ inline int lane_fresh() {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
 // The wave's index in its workgroup as a wave-uniform (SGPR) value: the
 // compiler cannot tell threadIdx.x >> 6 is uniform, so everything derived from
 // it (stream index, row pointers, coder state) would otherwise occupy VGPRs.
@@ -1918,6 +1926,24 @@ __device__ inline uint64_t wave_multi_sum32(uint32_t (&v)[R]) {
     r64 += shfl_xor_u64(r64, 32);
     return r64;
 }
+// One halving step of multi_halve<R, BIT> for one pair (v[i], v[i + live/2]),
+// so callers can run it as soon as both values exist.
+template <int BIT>
+__device__ inline uint32_t halve_pair(uint32_t lo, uint32_t hi) {
+    const bool upper = (lane_id() >> BIT) & 1;
+    return (upper ? hi : lo) + xor_dpp<BIT>(upper ? lo : hi);
+}
+// The end of wave_multi_sum32<8> once the caller has run all three halving steps
+// itself (halve_pair<0/1/2>, see k_q1_stats_rl): r = its stage-2 value.
+__device__ inline uint64_t wave_multi_sum32_tail8(uint32_t r) {
+    r += xor_dpp<3>(r);
+    uint64_t r64 = r;
+    r64 += shfl_xor_u64(r64, 16);
+    r64 += shfl_xor_u64(r64, 32);
+    return r64;
+}
+constexpr int kHalveOrder[8] = {0, 4, 2, 6, 1, 5, 3, 7};   // butterfly pairs complete early
+
 template <int R>
 __device__ inline int q_index(int lane) {                   // lane bit b -> index bit log2(R)-1-b
     int idx = 0;
@@ -2230,10 +2256,9 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
     __shared__ int smaxi[NW];
     __shared__ uint64_t ssum[NW][2];
     __shared__ uint32_t sps;
-    __shared__ unsigned long long bins[DEC ? 64 : 1];
+    __shared__ unsigned long long gtot[DEC ? NW * (R + L) : 1];   // DEC: every 64-vector group's total
     int tid = threadIdx.x;
     const int lane = tid & 63, w = wave_in_block();
-    if (DEC && w == 0) bins[lane] = 0;
     // (the fast fill below the first row's loads, as in k_q1_stats, spilled this
     // kernel at its 128-VGPR cap: 2.52 -> 2.70 ms at bf16 V = 128256)
     q1_load_tab_rep<kRLRep>(tabr, xsh);
@@ -2344,6 +2369,7 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
 #pragma unroll
             for (int i = 1; i < NW; i++) m = fmaxf(m, smax[i]);
         }
+        if (DEC && tid == 0) mrow[r] = m;                     // now: m is not held over pass 2
         const bool fast = q1_fast_row(m);
         const float c = q1_c(m);
         int sfull = -1, sr = 0;
@@ -2384,27 +2410,49 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
             (void)v;
         };
         const RowSrc<true, sizeof(LT)> nsrc(nrow, true, nvec);
-        // DEC: the 64-vector group totals of one half (vectors j0 .. j0+7) into the bins
+        // DEC: the 64-vector group totals of one half (vectors j0 .. j0+7) into the bins,
+        // by wave_multi_sum32<8>'s butterfly run as the sums appear: vectors are taken in
+        // the order 0 4 2 6 1 5 3 7 and each halving step runs once both of its inputs
+        // exist, so at most 3 sums are live instead of 8 (the 8-live form spilled at the
+        // 128-VGPR cap).  Same totals, lane for lane.
         auto bin_half = [&](int j0) {
-            const uint64_t gsum = wave_multi_sum32<8>(sv);     // lane l < 8: index q_index<8>(l)
-            if (lane < 8) {
-                const int grp = w + NW * (j0 + q_index<8>(lane));   // vectors [grp*64, grp*64 + 64)
-                if (grp * 64 < nvec) atomicAdd(&bins[grp / (int)G], (unsigned long long)gsum);
+            const uint64_t gsum = wave_multi_sum32_tail8(sv[0]);   // lane l < 8: index q_index<8>(l)
+            // each group has one writer: a plain LDS store (no division by G, no atomics;
+            // the chunk totals are summed from these after the row's barrier)
+            // (lane_fresh: the lane and its bit-reversed index are recomputed here rather
+            // than held across the row loop -- held, they spilled, and the reload's
+            // vmcnt(0) waited for the next row's slot loads just issued)
+            const int ln = lane_fresh();
+            if (ln < 8) gtot[w + NW * (j0 + q_index<8>(ln))] = gsum;   // vectors [grp*64, +64)
+        };
+        auto pair_halve = [&](int k) {                         // k: the vector just taken (compile-time)
+            if (!DEC) return;
+            if (k == 4) sv[0] = halve_pair<0>(sv[0], sv[4]);
+            if (k == 6) { sv[2] = halve_pair<0>(sv[2], sv[6]); sv[0] = halve_pair<1>(sv[0], sv[2]); }
+            if (k == 5) sv[1] = halve_pair<0>(sv[1], sv[5]);
+            if (k == 7) {
+                sv[3] = halve_pair<0>(sv[3], sv[7]);
+                sv[1] = halve_pair<1>(sv[1], sv[3]);
+                sv[0] = halve_pair<2>(sv[0], sv[1]);
             }
         };
         auto pass2 = [&](bool fs) {
 #pragma unroll
-            for (int k = 0; k < L; k++) {
+            for (int q = 0; q < L; q++) {
+                const int k = DEC ? kHalveOrder[q] : q;
                 const u32x4 v = slot(k);
                 take(R + k, v, q1_vec_sum<LT, kRLRep>(v, c, fs, tabr, loff));
+                pair_halve(k);
                 __builtin_amdgcn_s_waitcnt(0xc07f);           // lgkmcnt(0): this wave's reads of slot k are done
                 ld_lds(nrow, k);
                 __builtin_amdgcn_sched_barrier(0);
             }
             if (DEC) bin_half(R);
 #pragma unroll
-            for (int j = 0; j < R; j++) {
+            for (int q = 0; q < R; q++) {
+                const int j = DEC ? kHalveOrder[q] : q;
                 take(j, x[j], q1_vec_sum<LT, kRLRep>(x[j], c, fs, tabr, loff));
+                pair_halve(j);
                 x[j] = ld_reg(nsrc, j);
                 __builtin_amdgcn_sched_barrier(0);
             }
@@ -2418,9 +2466,11 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
         __syncthreads();
         if (DEC) {
             if (w == 0) {
-                chunks[r * 64 + lane] = bins[lane];
-                bins[lane] = 0;
-                if (lane == 0) mrow[r] = m;
+                // chunk c = groups [c G, (c + 1) G) of the row's ngrp groups
+                const int ngrp = (nvec + 63) / 64, ln = lane_fresh(), g0 = ln * (int)G;
+                uint64_t ct = 0;
+                for (int gi = g0; gi < g0 + (int)G && gi < ngrp; gi++) ct += gtot[gi];
+                chunks[r * 64 + ln] = ct;
             }
         } else if (tid == 0) {
             uint64_t T = 0, Ls = 0;
@@ -2991,9 +3041,10 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
         }
         // rows of 8193..16384 vectors: registers + LDS slots (shape 15; same-box, bf16
         // V = 128256 encode 3.23 -> 2.49 ms = 84 % of peak, f32 V = 65536 encode 2.73 ->
-        // 2.43 ms, decode 21.5 -> 24.0 M sym/s; bf16 decode keeps shape 9 (17.9 vs 15.9 M
-        // sym/s: the decode form spills), profiles/r02/q1_rl/)
-        if (sh == 0 && nvec <= 16384 && !(DEC && sizeof(LT) == 2)) sh = 15;
+        // 2.43 ms, decode 21.5 -> 24.0 M sym/s, profiles/r02/q1_rl/; bf16 decode, once its
+        // spills were removed (streamed butterfly, per-group LDS totals, fresh lane index),
+        // 220 -> 210 us per step of 4096 rows vs shape 9, profiles/r02/q1_rl_dec/)
+        if (sh == 0 && nvec <= 16384) sh = 15;
         // measured at V = 128256 f32: encode tiles of (16,8) with the tile-rolling
         // prefetch 1.98 ms vs 2.18 for tiles of (8,8) (shape 13, its (8,8) form: 2.20)
         if (sh == 0) sh = nvec <= 64 * 16 * 16 ? 9 : (DEC ? 10 : (sizeof(LT) == 4 ? 14 : 8));
