@@ -413,6 +413,28 @@ class BatchCoder:
         return int(self.lib.lac_q1_k(self.prec, self.vocab))
 
 
+def logits_row_multiple(dtype) -> int:
+    """Entries per 16-B vector of a logits row (8 bf16, 4 f32): the logits path
+    (lac_encode_logits, include/lac.h) needs vocab and row strides to be multiples of it."""
+    torch = _torch()
+    if dtype not in (torch.bfloat16, torch.float32):
+        raise TypeError(f"logits must be bfloat16 or float32, got {dtype}")
+    return 8 if dtype == torch.bfloat16 else 4
+
+
+def pad_logits(logits):
+    """[..., V] logits -> contiguous [..., Vp] with Vp the next multiple of
+    logits_row_multiple, the new entries -inf (q1 gives each the minimum weight, 1).
+    Encode and decode must both code the padded rows."""
+    torch = _torch()
+    m = logits_row_multiple(logits.dtype)
+    V = logits.shape[-1]
+    Vp = (V + m - 1) // m * m
+    if Vp != V:
+        logits = torch.nn.functional.pad(logits, (0, Vp - V), value=float("-inf"))
+    return logits.contiguous()
+
+
 def digits_of(E: int, k: int):
     """Raw digits of one symbol from its trace entry (first digit 0..3)."""
     if k <= 0:

@@ -155,19 +155,29 @@ class LogitsCompressor:
 
     def __init__(self, module, vocab, prec=48, bos=1, logits_dtype=None, device="cuda"):
         import torch
+        from .batch import logits_row_multiple
         self.module = module.to(device).eval()
         self.vocab, self.prec, self.bos = int(vocab), int(prec), int(bos)
         self.dtype = logits_dtype or torch.bfloat16
         self.device = torch.device(device)
+        # the logits kernels read rows as 16-B vectors: a vocab that is not a multiple
+        # of 8 (bf16) / 4 (f32) -- GPT-2's 50257, say -- is coded over rows padded
+        # with -inf (pad entries get the q1 minimum weight, 1 unit; compress and
+        # decompress pad alike, so the code stays lossless)
+        m = logits_row_multiple(self.dtype)
+        self.vcode = (self.vocab + m - 1) // m * m
 
     def _logits(self, ctx):
         import torch
         with torch.no_grad():
-            return self.module(ctx).to(self.dtype).contiguous()
+            lg = self.module(ctx).to(self.dtype)
+            if self.vcode != lg.shape[-1]:
+                lg = torch.nn.functional.pad(lg, (0, self.vcode - lg.shape[-1]), value=float("-inf"))
+            return lg.contiguous()
 
     def _coder(self, B, T):
         from .batch import BatchCoder
-        return BatchCoder(self.vocab, B, prec=self.prec, pmf_bits=32, capacity_bits=T * (self.prec + 2) + 256,
+        return BatchCoder(self.vcode, B, prec=self.prec, pmf_bits=32, capacity_bits=T * (self.prec + 2) + 256,
                           device=self.device)
 
     def compress(self, tokens):

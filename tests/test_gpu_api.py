@@ -230,6 +230,41 @@ def test_logits_compressor_roundtrip_and_oracle():
     assert torch.equal(back, toks)
 
 
+def test_logits_compressor_vocab_not_a_multiple_of_8():
+    """A vocab the 16-B row vectors do not divide (1001, bf16 and f32): rows padded
+    with -inf, bytes == oracle on the padded logits, tokens round trip, and the
+    library itself refuses the unpadded rows (LAC_E_ARG)."""
+    from lac_amd._lib import LacError
+    from lac_amd.batch import BatchCoder, pad_logits
+    from lac_amd.llm import LogitsCompressor, TinyCausalLM
+    from oracle import oracle as coracle
+    V, B, T, prec = 1001, 3, 12, 48
+    model = TinyCausalLM(vocab=V, d=32, layers=1, heads=2, max_len=64, seed=4)
+    toks = torch.from_numpy(np.random.default_rng(6).integers(0, V, (B, T))).to("cuda:0")
+    for dt in (torch.bfloat16, torch.float32):
+        lc = LogitsCompressor(model, V, prec=prec, logits_dtype=dt, device="cuda:0")
+        assert lc.vcode == (1008 if dt == torch.bfloat16 else 1004)
+        data, nbits = lc.compress(toks)
+        ctx = torch.cat([torch.ones((B, 1), dtype=torch.long, device="cuda:0"), toks[:, :-1]], 1)
+        lg = lc._logits(ctx)
+        assert lg.shape[-1] == lc.vcode and torch.isinf(lg[..., V:]).all()
+        h = lg.transpose(0, 1).contiguous()
+        host = h.view(torch.int16).cpu().numpy().view(np.uint16) if dt == torch.bfloat16 else h.cpu().numpy()
+        pmf = coracle.q1_quantize(host, prec)
+        assert (pmf[..., V:] == 1).all()
+        out, nb, status, rc = coracle.encode_batch(pmf, toks.t().contiguous().cpu().numpy().astype(np.int32), prec)
+        assert rc == 0
+        for b in range(B):
+            assert int(nbits[b]) == int(nb[b]) and data[b] == out[b, :(int(nb[b]) + 7) // 8].tobytes()
+        assert torch.equal(lc.decompress(data, nbits, T), toks)
+        raw = torch.randn((T, B, V), device="cuda:0").to(dt)
+        c = BatchCoder(V, B, prec=prec, device="cuda:0")
+        with pytest.raises(LacError):
+            c.encode_logits_job(raw, toks.t().contiguous().to(torch.int32))
+        c.close()
+        assert pad_logits(raw).shape[-1] == lc.vcode
+
+
 def test_quantiser_matches_reference_numpy_ops():
     """quantise_logits is the reference's float64 numpy quantiser (llama_compress.py:24-30)."""
     from lac_amd.llm import quantise_logits
