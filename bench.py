@@ -255,12 +255,15 @@ def main():
         alg_bytes = units * (V * ebytes + 4)
         achieved = alg_bytes / (rs_launch_ms * 1e-3) / 1e9 if cnt[kid] else None
         rows = (f"{args.input[7:]} logit rows, q1 tables in-kernel" if logits_in else f"uint{args.pmf_bits} pmf rows")
-        cfg = {"workload": f"c3: vocab={V}, {B} streams/GPU, {T} symbols/stream per job, prec={P}, {rows}",
+        cname = {32000: "c3", 128256: "c4"}.get(V, "custom")      # BASELINE.json configs
+        cfg = {"workload": f"{cname}: vocab={V}, {B} streams/GPU, {T} symbols/stream per job, prec={P}, {rows}",
                "vocab": V, "streams": B, "tokens": T, "prec": P, "pmf_bits": args.pmf_bits, "input": args.input,
                "parallelism": f"streams sharded over {world} GPU(s)" + (f", {'RCCL' if backend == 'nccl' else backend} bitstream all-gather" if world > 1 else "")}
         value = world * B * T * args.steps / dt
         line = {
-            "metric": METRIC, "value": value, "unit": "symbols/s", "n_gpus": world, "steps": args.steps,
+            "metric": METRIC if (V, B) == (32000, 4096) else
+                      f"encoded symbols/sec at vocab={V}, batch={B} streams; bit-exact round-trip",
+            "value": value, "unit": "symbols/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None,
             "dtype": ("u32" if logits_in else f"u{args.pmf_bits}"),

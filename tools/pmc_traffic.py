@@ -23,6 +23,8 @@ STREAMING = ("k_encode_fused", "k_row_stats", "k_decode_step", "k_decode_wave_fi
 
 
 def short(name):
+    if "::k_q1_stats_rl<" in name:                      # the register + LDS-slot row-stats kernel
+        return "k_q1_stats"
     for k in STREAMING + ("k_encode", "k_finish", "k_q1_decode"):
         if f"::{k}<" in name or f"::{k}(" in name:
             return k
