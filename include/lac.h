@@ -78,8 +78,10 @@ enum {                       /* lac_set_option */
                                       9 = 16-wave (16,16,n), 10 = tiles of 9, 11 = (16,8,y),
                                       12 = (16,8,n), 13 / 14 = tiles of (8,8) / (16,8) with a
                                       tile-walking prefetch, 15 = 16-wave, 8 vectors/thread in
-                                      registers + 8 in LDS (rows <= 16384 vectors); identical
-                                      results, only speed differs */
+                                      registers + 8 in LDS (rows <= 16384 vectors; 16 table copies
+                                      when the row fits a trimmed last slot, <= 16064 vectors),
+                                      16 = 15 with 8 table copies always; identical results,
+                                      only speed differs */
     LAC_OPT_DECODE_FINE = 7,       /* one-wave decode (FUSED path): 1 = one total per 64 vectors of
                                       the row, so only 1 KB is re-read after the search (default,
                                       rows <= 131072 u32 / 65536 u64 entries); 0 = <= 64 chunk totals */

@@ -2235,13 +2235,19 @@ __global__ __launch_bounds__(64 * NWB, LAC_Q1_MINW) void k_q1_stats(const LT *__
 // to the block's next row as it consumes them -- an LDS slot right after its
 // read, a register vector right after its use -- so the next row streams in
 // while this one is quantised, instead of a CU alternating between loading a
-// whole row and computing it (shape 9, 65 % of peak at c4 bf16).  LDS: 8 table
-// copies (17 KB; 16 or 32 copies measured no faster at c3) + 128 KB of slots.
+// whole row and computing it (shape 9, 65 % of peak at c4 bf16).  LDS: REP table
+// copies + the slots.  With all 8 slots (128 KB: rows up to 16384 vectors) only 8
+// copies fit, and four lanes of a 32-lane LDS group share a copy: 57 % of the
+// lookups' LDS cycles were bank conflicts (PMC, bf16 c4).  Rows of <= 16064
+// vectors (bf16 V <= 128512: Llama-3's 128256) need only LASTN = 704 threads' worth
+// of the last slot, which leaves room for 16 copies (two lanes per copy).
 // Same outputs as k_q1_stats (RowStats, or row max + 64 chunk totals).
 constexpr int kRLRep = 8;
+constexpr int kRLLastTrim = 704;                 // last-slot threads of the 16-copy form
+constexpr int kRLTrimMaxVec = 15 * 1024 + kRLLastTrim;   // rows it holds: 16064 vectors
 typedef __attribute__((address_space(3))) void lvoid_t;
 
-template <typename LT, bool DEC>
+template <typename LT, bool DEC, int REP = kRLRep, int LASTN = 1024>
 __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ lg, int64_t step_stride,
                                                          int64_t stream_stride, const int32_t *__restrict__ sym,
                                                          int64_t B, int64_t rows, int64_t V, int64_t t0, uint32_t xsh,
@@ -2250,8 +2256,10 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
     constexpr int N = LogitN<LT>::N, NT = 1024, R = 8, L = 8, NW = 16;
     constexpr bool IMAX = LAC_Q1_IMAX && sizeof(LT) == 2;
     static_assert((R + L) * N <= 128, "lane sums must fit 32 bits");
-    __shared__ uint32_t tabr[LAC_Q1_TAB_SIZE * kRLRep];
-    __shared__ u32x4 slots[L * NT];
+    static_assert(LASTN % 64 == 0 && LASTN <= NT, "the last slot is trimmed by whole waves");
+    constexpr bool TRIM = LASTN < NT;
+    __shared__ uint32_t tabr[LAC_Q1_TAB_SIZE * REP];
+    __shared__ u32x4 slots[(L - 1) * NT + LASTN];
     __shared__ float smax[NW];
     __shared__ int smaxi[NW];
     __shared__ uint64_t ssum[NW][2];
@@ -2261,9 +2269,11 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
     const int lane = tid & 63, w = wave_in_block();
     // (the fast fill below the first row's loads, as in k_q1_stats, spilled this
     // kernel at its 128-VGPR cap: 2.52 -> 2.70 ms at bf16 V = 128256)
-    q1_load_tab_rep<kRLRep>(tabr, xsh);
-    const uint32_t loff = (uint32_t)(lane & (kRLRep - 1)) << 2;
+    q1_load_tab_rep<REP>(tabr, xsh);
+    const uint32_t loff = (uint32_t)(lane & (REP - 1)) << 2;
     const int nvec = (int)(V / N);
+    // TRIM: waves past LASTN have no last slot (their vectors there lie beyond the row)
+    const bool noslot = TRIM && w * 64 >= LASTN;
     const int64_t stride = gridDim.x;
     auto row_of = [&](int64_t r) { return lg + (t0 + r / B) * step_stride + (r % B) * stream_stride; };
     // vector j of this thread (clamped into the row: a duplicate cannot change the
@@ -2276,6 +2286,7 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
     // vmcnt(0) before pass 1 reads any slot, lgkmcnt(0) before a slot is refilled.
     const uint32_t slot_base = (uint32_t)(uintptr_t)(lvoid_t *)&slots[w * 64];   // wave-uniform LDS address
     auto ld_lds = [&](const LT *rw, int k) {
+        if (k == L - 1 && noslot) return;                      // wave-uniform
         const u32x4 *src = reinterpret_cast<const u32x4 *>(rw) + vidx(R + k);
         uint32_t keep;
         asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
@@ -2304,7 +2315,11 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
         __builtin_amdgcn_s_waitcnt(0);                         // this wave's LDS-DMA writes (asm: untracked)
         asm volatile("" ::: "memory");
         // slot vectors are read where used (not held across the barrier: registers)
-        auto slot = [&](int k) { return slots[k * NT + tid]; };
+        // (a wave without a last slot reads the neutral -inf: no other wave's DMA
+        // writes are waited for here, and those vectors are masked from the sums)
+        auto slot = [&](int k) {
+            return (k == L - 1 && noslot) ? neg_inf16(sizeof(LT)) : slots[k * NT + tid];
+        };
         float m;
         if constexpr (IMAX) {
             s16x2 pm = {(short)-32768, (short)-32768};
@@ -2390,7 +2405,7 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
             uint32_t pl = 0, ps = 0;
 #pragma unroll
             for (int e = 0; e < N; e++) {
-                const uint32_t q = q1_rep_at<kRLRep>(tabr, q1_j(logit_at<LT>(v, e), c), loff);
+                const uint32_t q = q1_rep_at<REP>(tabr, q1_j(logit_at<LT>(v, e), c), loff);
                 pl += e < sr ? q : 0;
                 ps += e == sr ? q : 0;
             }
@@ -2441,7 +2456,7 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
             for (int q = 0; q < L; q++) {
                 const int k = DEC ? kHalveOrder[q] : q;
                 const u32x4 v = slot(k);
-                take(R + k, v, q1_vec_sum<LT, kRLRep>(v, c, fs, tabr, loff));
+                take(R + k, v, q1_vec_sum<LT, REP>(v, c, fs, tabr, loff));
                 pair_halve(k);
                 __builtin_amdgcn_s_waitcnt(0xc07f);           // lgkmcnt(0): this wave's reads of slot k are done
                 ld_lds(nrow, k);
@@ -2451,7 +2466,7 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
 #pragma unroll
             for (int q = 0; q < R; q++) {
                 const int j = DEC ? kHalveOrder[q] : q;
-                take(j, x[j], q1_vec_sum<LT, kRLRep>(x[j], c, fs, tabr, loff));
+                take(j, x[j], q1_vec_sum<LT, REP>(x[j], c, fs, tabr, loff));
                 pair_halve(j);
                 x[j] = ld_reg(nsrc, j);
                 __builtin_amdgcn_sched_barrier(0);
@@ -3001,14 +3016,21 @@ static int q1_stats_launch(lac_ctx *c, const Q1Args &a, hipStream_t st) {
     return LAC_OK;
 }
 
+// trim: the 16-copy form with a trimmed last slot, for rows of <= kRLTrimMaxVec vectors
 template <typename LT, bool DEC>
-static int q1_stats_rl_launch(lac_ctx *c, const Q1Args &a, hipStream_t st) {
+static int q1_stats_rl_launch(lac_ctx *c, const Q1Args &a, hipStream_t st, bool trim) {
     const int64_t need = a.rows, cap = (int64_t)c->cus;     // one 16-wave block per CU
     const unsigned grid = (unsigned)(need < cap ? need : cap);
     const int64_t nvec = c->V / LogitN<LT>::N;
     ProfScope ps(c, KID_Q1_STATS, st);
-    k_q1_stats_rl<LT, DEC><<<grid, 1024, 0, st>>>((const LT *)a.lg, a.ss, a.bs, a.sym, c->B, a.rows, c->V, a.t0,
-                                                   a.xsh, q1_groups_per_chunk(nvec), c->stats, c->q1chunks, c->q1m);
+    if (trim && nvec <= kRLTrimMaxVec)
+        k_q1_stats_rl<LT, DEC, 16, kRLLastTrim><<<grid, 1024, 0, st>>>(
+            (const LT *)a.lg, a.ss, a.bs, a.sym, c->B, a.rows, c->V, a.t0, a.xsh, q1_groups_per_chunk(nvec),
+            c->stats, c->q1chunks, c->q1m);
+    else
+        k_q1_stats_rl<LT, DEC><<<grid, 1024, 0, st>>>((const LT *)a.lg, a.ss, a.bs, a.sym, c->B, a.rows, c->V,
+                                                       a.t0, a.xsh, q1_groups_per_chunk(nvec), c->stats,
+                                                       c->q1chunks, c->q1m);
     CHECK_LAUNCH();
     return LAC_OK;
 }
@@ -3055,11 +3077,13 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
     if (sh == 10) return q1_stats_launch<LT, 16, 16, DEC, true, false, 16>(c, a, st);   // tiles of 16384
     if (sh == 11 && nvec <= 64 * 16 * 8) return q1_stats_launch<LT, 16, 8, DEC, false, true, 16>(c, a, st);
     if (sh == 12 && nvec <= 64 * 16 * 8) return q1_stats_launch<LT, 16, 8, DEC, false, false, 16>(c, a, st);
-    if (sh == 15 && nvec <= 16384) return q1_stats_rl_launch<LT, DEC>(c, a, st);     // registers + LDS slots
+    // registers + LDS slots: 15 = 16 table copies where the trimmed slots hold the row, else
+    // 8; 16 = always 8 copies (tuning)
+    if ((sh == 15 || sh == 16) && nvec <= 16384) return q1_stats_rl_launch<LT, DEC>(c, a, st, sh == 15);
     if (sh == 13) return q1_stats_launch<LT, 8, 8, DEC, true, true>(c, a, st);         // tiles of (8,8,y)
     if (sh == 14) return q1_stats_launch<LT, 16, 8, DEC, true, true, 16>(c, a, st);    // tiles of (16,8,y)
     if (sh == 8) return q1_stats_launch<LT, 8, 8, DEC, true, false>(c, a, st);      // tiles of 4096 vectors
-    // shapes 9, 11, 12, 15 with a row too long for them, and 1..7 likewise (kQ1Shapes
+    // shapes 9, 11, 12, 15, 16 with a row too long for them, and 1..7 likewise (kQ1Shapes
     // describes 1..7 only: a forced 11 / 12 used to index past it)
     if (sh > 7 || !holds(sh))
         return fail(LAC_E_ARG, "q1 shape %d does not hold a row of %lld vectors", sh, (long long)nvec);
@@ -3253,7 +3277,7 @@ int lac_set_option(lac_ctx *c, int option, int64_t value) {
         c->fine_decode = (int)value;
         return LAC_OK;
     case LAC_OPT_Q1_SHAPE:
-        if (value < 0 || value > 15) return fail(LAC_E_ARG, "bad q1 shape");
+        if (value < 0 || value > 16) return fail(LAC_E_ARG, "bad q1 shape");
         c->q1_shape = (int)value;
         return LAC_OK;
     case LAC_OPT_MAPPING:

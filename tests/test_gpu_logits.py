@@ -231,12 +231,14 @@ def test_incremental_logits_encode_mixes_with_pmf_steps():
     assert (n1 == n2).all() and one == two
 
 
-@pytest.mark.parametrize("dtype,V", [("bf16", 32000), ("f32", 32000), ("bf16", 128256), ("f32", 65536)])
+@pytest.mark.parametrize("dtype,V", [("bf16", 32000), ("f32", 32000), ("bf16", 128256), ("f32", 65536),
+                                     ("bf16", 128512), ("bf16", 128520)])
 def test_every_q1_shape_gives_the_same_bits(dtype, V):
     """Every forced row-stats shape (8/16-wave blocks, tiles, rolling prefetch,
     registers + LDS slots) yields the AUTO shape's bytes and decodes; shapes that
     cannot hold the row are refused with LAC_E_ARG.  V = 128256 bf16 and 65536
-    f32 fill the register + LDS shape (15) exactly up to its 16384 vectors."""
+    f32 fill the register + LDS shape (15) exactly up to its 16384 vectors; bf16
+    128512 / 128520 sit on either side of its 16-copy form's 16064-vector limit."""
     from lac_amd._lib import LacError
     B, steps, prec = 12, 3, 48
     x = _logits(777, steps, B, V, specials=True)
@@ -247,7 +249,7 @@ def test_every_q1_shape_gives_the_same_bits(dtype, V):
     c.encode_logits_job(dl, sym)
     want, wn = c.to_bytes()
     ran = 0
-    for sh in range(1, 16):
+    for sh in range(1, 17):
         c.set_q1_shape(sh)
         try:
             c.encode_logits_job(dl, sym)
