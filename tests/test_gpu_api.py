@@ -362,6 +362,42 @@ def test_batch_decode_rejects_bad_shapes():
     coder.close()
 
 
+def test_persistent_fused_decode_with_failed_streams():
+    """More streams than resident decode waves (k_decode_wave_fine walks several
+    streams per wave, prefetching the next stream's first row group over the last
+    step): every stream decodes, also when the stream before it on the same wave
+    failed at open (sticky LAC_E_ARG from nbits beyond its row), on u32 and u64
+    rows; the fused path equals the stats path stream for stream."""
+    from lac_amd.batch import BatchCoder
+    dev = "cuda:0"
+    for bits_w, V in ((32, 2048), (64, 1024)):
+        B, T, prec = 6000, 5, 40
+        g = torch.Generator(device=dev).manual_seed(bits_w)
+        pmf = (torch.randint(1, 1 << 20, (T, B, V), generator=g, device=dev, dtype=torch.int64))
+        pmf = pmf.to(torch.int32) if bits_w == 32 else pmf
+        sym = torch.randint(0, V, (T, B), generator=g, device=dev, dtype=torch.int32)
+        coder = BatchCoder(V, B, prec=prec, pmf_bits=bits_w, capacity_bits=T * (prec + 2) + 256, device=dev)
+        coder.encode_job(pmf, sym)
+        coder.raise_on_error()
+        bits = coder.bits_tensor()
+        nb = coder.nbits_tensor()
+        bad = torch.arange(0, B, 997, device=dev)                # a few streams on different waves
+        nb_bad = nb.clone()
+        nb_bad[bad] = bits.shape[1] * 8 + 1
+        coder.set_decode_path("fused")
+        coder.decode_open(bits, nb_bad)
+        out = coder.decode(pmf)
+        rc, err, _ = coder.status()
+        ok = torch.ones(B, dtype=torch.bool, device=dev)
+        ok[bad] = False
+        assert (torch.from_numpy(err).to(dev)[bad] == -1).all() and (torch.from_numpy(err).to(dev)[ok] == 0).all()
+        assert (out[:, bad] == -1).all() and torch.equal(out[:, ok], sym[:, ok])
+        coder.set_decode_path("stats")
+        coder.decode_open(bits, nb)
+        assert torch.equal(coder.decode(pmf), sym)
+        coder.close()
+
+
 def test_acsampler_per_token_pdfs_bits_and_entropy():
     """ACSampler with a new float pdf per token: GPU bits and bits_per_token ==
     the reference's (tests/golden/acsampler_cb.json); the host Region mirror
