@@ -362,12 +362,11 @@ def test_batch_decode_rejects_bad_shapes():
     coder.close()
 
 
-def test_persistent_fused_decode_with_failed_streams():
-    """More streams than resident decode waves (k_decode_wave_fine walks several
-    streams per wave, prefetching the next stream's first row group over the last
-    step): every stream decodes, also when the stream before it on the same wave
-    failed at open (sticky LAC_E_ARG from nbits beyond its row), on u32 and u64
-    rows; the fused path equals the stats path stream for stream."""
+def test_fused_decode_many_streams_with_failed_streams():
+    """6000 streams through the one-wave-per-stream decoder (more streams than
+    resident waves: two dispatch rounds and a partial third), a few of them failed
+    at open (sticky LAC_E_ARG from nbits beyond the row): those report -1, every
+    other stream decodes, on u32 and u64 rows; the stats path agrees."""
     from lac_amd.batch import BatchCoder
     dev = "cuda:0"
     for bits_w, V in ((32, 2048), (64, 1024)):

@@ -254,6 +254,48 @@ def test_c4_shape_softmax_tables():
     c.close()
 
 
+def test_c5_stream_count_on_one_gpu():
+    """SURVEY c5's whole job -- V=128256, 32768 streams (8 x 4096) -- on one MI355X
+    (2 steps: 33.6 GB of u32 rows, and the same shape as bf16 logits): sampled
+    streams bit-exact against the C oracle, every stream round-trips, and the bits
+    of stream b do not depend on the batch it is coded in (the first 4096 streams
+    coded alone give the same bytes -- what lets c5 shard over 8 GPUs)."""
+    from oracle import oracle as coracle
+    V, B, steps, prec = 128256, 32768, 2, 48
+    pmf, sym = synth.softmax_tables(steps, B, V, seed=55, device=DEV)
+    c = _coder(V, B, prec, cap=steps * (prec + 2) + 256)
+    c.encode_job(pmf, sym)
+    data, n = c.to_bytes()
+    sample = list(range(0, B, 2999)) + [B - 1]
+    sub = pmf[:, sample, :].cpu().numpy().view(np.uint32)
+    out, nb, status, rc = coracle.encode_batch(sub, sym[:, sample].cpu().numpy(), prec, nthreads=16)
+    assert rc == 0
+    for i, b in enumerate(sample):
+        assert int(n[b]) == int(nb[i]) and data[b] == out[i, :(int(nb[i]) + 7) // 8].tobytes(), b
+    c.decode_open()
+    assert torch.equal(c.decode(pmf), sym)
+    c.close()
+    shard = _coder(V, 4096, prec, cap=steps * (prec + 2) + 256)
+    shard.encode_job(pmf[:, 4096:8192], sym[:, 4096:8192].contiguous())
+    assert shard.to_bytes()[0] == data[4096:8192]
+    shard.close()
+    del pmf
+    c = _coder(V, B, prec, cap=steps * (prec + 2) + 256)
+    lg, sym2 = synth.logits_batch(steps, B, V, seed=56, device=DEV, dtype=torch.bfloat16,
+                                  quantise=c.quantize_logits)
+    c.encode_logits_job(lg, sym2)
+    data2, n2 = c.to_bytes()
+    host = lg[:, sample, :].contiguous().view(torch.int16).cpu().numpy().view(np.uint16)
+    out, nb, status, rc = coracle.encode_batch(coracle.q1_quantize(host, prec), sym2[:, sample].cpu().numpy(), prec,
+                                               nthreads=16)
+    assert rc == 0
+    for i, b in enumerate(sample):
+        assert int(n2[b]) == int(nb[i]) and data2[b] == out[i, :(int(nb[i]) + 7) // 8].tobytes(), b
+    c.decode_open()
+    assert torch.equal(c.decode_logits(lg), sym2)
+    c.close()
+
+
 # ---------------------------------------------------------------- errors
 @pytest.mark.parametrize("path", ["split", "fused"])
 def test_error_symbol_range(path):
