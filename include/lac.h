@@ -253,6 +253,26 @@ int lac_quantize_logits(lac_ctx *ctx, const void *logits_dev, int logit_type, in
  * A_from_bin.run(bits, stop=0) emits (arith_code.py:268-299, :322-326). */
 int lac_decode_determined(lac_ctx *ctx, int64_t *ndet_host, void *stream);
 
+/* Decoder registers of one stream, A_from_bin's state (arith_code.py:248-256) in
+ * the value form: l, h, the prec-bit value window x (bits at or past the stream's
+ * nbits read as 0), pos = index of the next bit to read, symbols decoded, the
+ * sticky error, and the determined flag / count of lac_decode_determined. */
+typedef struct lac_dec_state {
+    int64_t l, h, x;
+    uint64_t pos;
+    int64_t nsym;
+    int32_t err, det;
+    int64_t err_step, ndet;
+} lac_dec_state;
+
+/* Copy every stream's decoder registers to / from the host (synchronise).  With
+ * lac_decode_open (which binds a longer bit buffer) and a host-side update of x
+ * for the bits that arrived since, this resumes a decoder: the bit-serial
+ * A_from_bin.step(bit) of the reference (arith_code.py:291-298) is built on it
+ * (lac_amd.coder).  Not thread-safe with launches on the same context. */
+int lac_decode_get_state(lac_ctx *ctx, lac_dec_state *host_out, void *stream);
+int lac_decode_set_state(lac_ctx *ctx, const lac_dec_state *host_in, void *stream);
+
 /* Live kernel timing: with profiling on, every kernel launch is bracketed by
  * hipEvents recorded on its own stream.  lac_profile_read synchronises and
  * returns, per kernel id (0 row_stats, 1 encode, 2 finish, 3 decode_step,

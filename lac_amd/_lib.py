@@ -56,6 +56,8 @@ PROTOTYPES = [
     ("lac_decode_step", _i, [_vp, _vp, _i64, _vp, _vp]),
     ("lac_decode_steps", _i, [_vp, _vp, _i64, _i64, _i64, _vp, _vp]),
     ("lac_decode_determined", _i, [_vp, _vp, _vp]),
+    ("lac_decode_get_state", _i, [_vp, _vp, _vp]),
+    ("lac_decode_set_state", _i, [_vp, _vp, _vp]),
     ("lac_profile_enable", _i, [_vp, _i]),
     ("lac_profile_read", _i, [_vp, _vp, _vp, _i]),
     ("lac_q1_k", _i, [_i, _i64]),

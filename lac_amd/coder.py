@@ -30,9 +30,12 @@ import bisect
 import itertools
 import math
 
+import ctypes as C
+
 import numpy as np
 
 from . import _lib
+from ._lib import check
 from .batch import BatchCoder, digits_of
 
 
@@ -401,8 +404,85 @@ class A_from_bin:
         data = bytes(group_bits(iter(bl)))
         return iter(self._decode_bytes(data, len(bl), n, max_symbols))
 
+    # ---- bit-serial decoding: step(bit) / __call__(bit) (arith_code.py:291-298, 318-321)
+    _DEC_STATE = np.dtype([("l", "<i8"), ("h", "<i8"), ("x", "<i8"), ("pos", "<u8"), ("nsym", "<i8"),
+                           ("err", "<i4"), ("det", "<i4"), ("err_step", "<i8"), ("ndet", "<i8")])   # lac_dec_state
+
     def step(self, bit):
-        raise NotImplementedError("bit-at-a-time decoding is not provided; decode whole streams with run()")
+        """receive_bit + the decide_symbol / emit_symbol loop (arith_code.py:291-298):
+        yields, once each, the symbols that the bits received so far determine --
+        the same symbols after the same bits as the reference.
+
+        The GPU decodes; between calls the decoder's registers wait on the host
+        (include/lac.h lac_decode_get_state / set_state).  Each call tries the next
+        symbol against the bits so far, zero-padded: when both the 0- and 1-padded
+        ends of the available bits map to one symbol (the reference's ls == hs)
+        it is committed, the predictor accepts it and the next is tried; otherwise
+        the registers stay as they were.  A new bit inside the value window of
+        the committed registers is added to x where it sits (it was read as 0)."""
+        return iter(self._step_bit(int(bit)))
+
+    def __call__(self, bit):
+        if bit is None:
+            raise NotImplementedError("A_from_bin.flush (arith_code.py:300-317) is not provided: its heuristic "
+                                      "raises on about a fifth of valid streams (SURVEY.md finding 5)")
+        return tuple(self.step(bit))
+
+    def _step_bit(self, bit):
+        import torch
+        if bit not in (0, 1):
+            raise ValueError("bits are 0 or 1")
+        if not hasattr(self, "_sbits"):
+            self._sbits = []
+            self._stab = _Tables(self.predictor)
+            self._scoder = None
+            self._sstate = np.zeros(1, dtype=self._DEC_STATE)
+            self._sstate["h"] = self.denom - 1
+            self._sstate["pos"] = self.precision
+            self._sstate["det"] = 1
+            self._sstate["err_step"] = -1
+        n = len(self._sbits)
+        self._sbits.append(bit)
+        st = self._sstate
+        pos = int(st["pos"][0])
+        if bit and pos - self.precision <= n < pos:          # was read as a padding 0
+            st["x"] += 1 << (pos - 1 - n)
+        out = []
+        while True:
+            row = self._stab.row()
+            V = len(row)
+            if self._scoder is None or self._scoder.vocab != V:
+                if self._scoder is not None:
+                    self._scoder.close()
+                self._scoder = BatchCoder(V, 1, prec=self.precision, pmf_bits=64, capacity_bits=64)
+                self._scoder.set_mapping(self._stab.mapping)
+            c = self._scoder
+            nb = len(self._sbits)
+            stride = ((nb + 7) // 8 + 8) // 8 * 8
+            buf = np.zeros((1, stride), dtype=np.uint8)
+            packed = np.packbits(np.asarray(self._sbits, dtype=np.uint8))
+            buf[0, :len(packed)] = packed
+            bits_dev = torch.from_numpy(buf).to(c.device)
+            nbits_dev = torch.tensor([nb], dtype=torch.int64, device=c.device)
+            c.decode_open(bits_dev, nbits_dev)
+            trial = st.copy()
+            trial["det"] = 1
+            trial["ndet"] = 0
+            check(c.lib.lac_decode_set_state(c.ctx, trial.ctypes.data_as(C.c_void_p), c._stream))
+            pmf = torch.from_numpy(row.view(np.int64).reshape(1, 1, V)).to(c.device)
+            s = int(c.decode(pmf).cpu()[0, 0])
+            new = np.zeros(1, dtype=self._DEC_STATE)
+            check(c.lib.lac_decode_get_state(c.ctx, new.ctypes.data_as(C.c_void_p), c._stream))
+            # not determined by the bits so far -- or not decodable from them yet: the
+            # 0-padded window can fall below l (the reference's lb - l < 0 then maps
+            # the two ends to different symbols and it emits nothing either)
+            if int(new["err"][0]) or int(new["ndet"][0]) != 1:
+                break
+            st = new
+            out.append(s)
+            self.predictor.accept(s)
+        self._sstate = st
+        return out
 
     def decode(self, bits, length, stop=1, n=None):
         """A_from_bin.decode(int, length) -- arith_code.py:327-334."""

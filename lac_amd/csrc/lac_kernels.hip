@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <stdarg.h>
+#include <stddef.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
@@ -3418,6 +3419,29 @@ int lac_decode_open(lac_ctx *c, const uint8_t *bits_dev, uint64_t stride_bytes, 
     k_dec_init<<<(unsigned)((c->B + 255) / 256), 256, 0, S(stream)>>>(c->dec, c->B, c->prec, bits_dev, stride_bytes,
                                                                       nbits_dev);
     CHECK_LAUNCH();
+    return LAC_OK;
+}
+
+static_assert(sizeof(lac_dec_state) == sizeof(DecState) && offsetof(lac_dec_state, ndet) == offsetof(DecState, ndet) &&
+                  offsetof(lac_dec_state, det) == offsetof(DecState, det) &&
+                  offsetof(lac_dec_state, pos) == offsetof(DecState, pos),
+              "lac_dec_state mirrors DecState");
+
+int lac_decode_get_state(lac_ctx *c, lac_dec_state *host_out, void *stream) {
+    if (!c || !host_out) return fail(LAC_E_ARG, "NULL argument");
+    if (c->mode != 1) return fail(LAC_E_STATE, "call lac_decode_open first");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemcpyAsync(host_out, c->dec, sizeof(DecState) * c->B, hipMemcpyDeviceToHost, S(stream)));
+    HIPCHK(hipStreamSynchronize(S(stream)));
+    return LAC_OK;
+}
+
+int lac_decode_set_state(lac_ctx *c, const lac_dec_state *host_in, void *stream) {
+    if (!c || !host_in) return fail(LAC_E_ARG, "NULL argument");
+    if (c->mode != 1) return fail(LAC_E_STATE, "call lac_decode_open first");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemcpyAsync(c->dec, host_in, sizeof(DecState) * c->B, hipMemcpyHostToDevice, S(stream)));
+    HIPCHK(hipStreamSynchronize(S(stream)));
     return LAC_OK;
 }
 

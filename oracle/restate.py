@@ -167,16 +167,18 @@ def encode_bytes(rows, symbols, prec):
 
 
 # ------------------------------------------------------------------ decoders
-def decode_bitserial(rows, bits, prec):
+def decode_bitserial(rows, bits, prec, counts=None):
     """A_from_bin.run(bits, stop=0) restated -- arith_code.py:248-299.
 
-    Returns every symbol the reference decoder determines from ``bits``.
+    Returns every symbol the reference decoder determines from ``bits``; with a
+    list ``counts``, appends how many symbols each bit's step(bit) yields (:291-298).
     """
     R = _Rows(rows)
     denom, decision = 1 << prec, 1 << (prec - 1)
     l, h, lb, hb = 0, denom - 1, 0, denom - 1
     out = []
     for bit in bits:
+        before = len(out)
         wb = (hb - lb + 1) // 2                      # receive_bit :264-267
         lb += wb * bit
         hb = lb + wb - 1
@@ -199,6 +201,8 @@ def decode_bitserial(rows, bits, prec):
                 h = h * 2 + 1 - d * denom
                 lb = lb * 2 - d * denom
                 hb = hb * 2 + 1 - d * denom
+        if counts is not None:
+            counts.append(len(out) - before)
     return out
 
 

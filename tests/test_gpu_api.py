@@ -75,6 +75,49 @@ def test_cdfpredictor_against_golden(kind):
         assert list(ac.from_bin.run(bits, stop=0)) == c["syms"] + c["decoded_extra"]
 
 
+def test_bit_serial_step_matches_reference():
+    """A_from_bin.step(bit) / __call__(bit) (arith_code.py:291-298, 318-321): after
+    every bit, exactly the symbols the reference's step(bit) yields -- per-bit counts
+    recorded by running the reference over 77 golden streams (tests/golden/
+    step_cases.json, tools/gen_golden_step.py): static and per-step tables, V up to
+    1000, prec 10..61, fudged rows included."""
+    from lac_amd import synth
+    from lac_amd.coder import AC, CDFPredictor
+
+    class Replay(CDFPredictor):
+        def __init__(self, rows):
+            self.rows, self.i = rows, 0
+            self._load()
+
+        def _load(self):
+            r = self.rows[min(self.i, len(self.rows) - 1)]
+            self.dist = np.cumsum(np.asarray(r, dtype=object)).tolist()
+            self.minp = min(int(x) for x in r if x > 0)
+
+        def accept(self, s):
+            self.i += 1
+            self._load()
+
+    gen = {c["name"]: c for c in load_golden("gen_cases.json")}
+    for case in load_golden("step_cases.json")["cases"]:
+        if "rows" in case:
+            rows = case["rows"]
+        else:
+            g = gen[case["gen"]]
+            rows = [synth.pmf_row(g["seed"], t, 0, g["V"], g["kind"], g["exp_range"]).tolist()
+                    for t in range(g["steps"])]
+        data = bytes.fromhex(case["bytes"])
+        bits = [(data[i >> 3] >> (7 - (i & 7))) & 1 for i in range(case["L"])]
+        dec = AC(Replay(rows), case["prec"]).from_bin
+        counts, syms = [], []
+        for i, b in enumerate(bits):
+            out = dec(b) if i % 2 else tuple(dec.step(b))
+            counts.append(len(out))
+            syms.extend(out)
+        assert counts == case["counts"], case["src"]
+        assert syms == case["syms"], case["src"]
+
+
 def test_probpredictor_subclass_adaptive():
     """An adaptive ProbPredictor (counts of past symbols) round-trips and matches the oracle."""
     from lac_amd.coder import AC, ProbPredictor

@@ -141,3 +141,22 @@ def test_kat2_acsampler_c_oracle():
     bits = coracle.acsampler_encode(cdf, data.tolist(), 48)
     out = bytes(restate.group_bits(bits))
     assert len(out) == kat["out_len"] and hashlib.sha256(out).hexdigest() == kat["out_sha256"]
+
+
+def test_bitserial_restatement_per_bit_counts():
+    """The restated bit-serial decoder yields, bit for bit, what the reference's
+    A_from_bin.step did (tests/golden/step_cases.json, tools/gen_golden_step.py)."""
+    from lac_amd import synth
+    gen = {c["name"]: c for c in load_golden("gen_cases.json")}
+    for case in load_golden("step_cases.json")["cases"]:
+        if "rows" in case:
+            rows = case["rows"]
+        else:
+            g = gen[case["gen"]]
+            rows = [[int(v) for v in synth.pmf_row(g["seed"], t, 0, g["V"], g["kind"], g["exp_range"])]
+                    for t in range(g["steps"])]
+        data = bytes.fromhex(case["bytes"])
+        bits = [(data[i >> 3] >> (7 - (i & 7))) & 1 for i in range(case["L"])]
+        counts = []
+        assert restate.decode_bitserial(rows, bits, case["prec"], counts) == case["syms"], case["src"]
+        assert counts == case["counts"], case["src"]
