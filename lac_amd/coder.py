@@ -441,8 +441,15 @@ class A_from_bin:
             self._sstate["pos"] = self.precision
             self._sstate["det"] = 1
             self._sstate["err_step"] = -1
+            self._sbuf = np.zeros(64, dtype=np.uint8)        # packed bits, MSB first (host copy)
+            self._sdev = None                                # its device copy, re-sent when it grows
+        if (len(self._sbits) >> 3) + 8 >= len(self._sbuf):
+            self._sbuf = np.concatenate([self._sbuf, np.zeros(len(self._sbuf), dtype=np.uint8)])
+            self._sdev = None
         n = len(self._sbits)
         self._sbits.append(bit)
+        if bit:
+            self._sbuf[n >> 3] |= 0x80 >> (n & 7)
         st = self._sstate
         pos = int(st["pos"][0])
         if bit and pos - self.precision <= n < pos:          # was read as a padding 0
@@ -458,13 +465,13 @@ class A_from_bin:
                 self._scoder.set_mapping(self._stab.mapping)
             c = self._scoder
             nb = len(self._sbits)
-            stride = ((nb + 7) // 8 + 8) // 8 * 8
-            buf = np.zeros((1, stride), dtype=np.uint8)
-            packed = np.packbits(np.asarray(self._sbits, dtype=np.uint8))
-            buf[0, :len(packed)] = packed
-            bits_dev = torch.from_numpy(buf).to(c.device)
-            nbits_dev = torch.tensor([nb], dtype=torch.int64, device=c.device)
-            c.decode_open(bits_dev, nbits_dev)
+            if self._sdev is None or self._sdev.device != c.device:
+                self._sdev = torch.from_numpy(self._sbuf.reshape(1, -1)).to(c.device)
+                self._snb = torch.zeros(1, dtype=torch.int64, device=c.device)
+            else:                                        # only the byte the new bit went into
+                self._sdev[0, n >> 3] = int(self._sbuf[n >> 3])
+            self._snb.fill_(nb)
+            c.decode_open(self._sdev, self._snb)
             trial = st.copy()
             trial["det"] = 1
             trial["ndet"] = 0

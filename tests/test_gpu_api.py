@@ -116,6 +116,13 @@ def test_bit_serial_step_matches_reference():
             syms.extend(out)
         assert counts == case["counts"], case["src"]
         assert syms == case["syms"], case["src"]
+    # a longer stream (the bit buffer grows several times): step() == run(bits, stop=0)
+    data = bytes(np.random.default_rng(9).integers(0, 256, 400, dtype=np.uint8))
+    ac = AC(CDFPredictor(list(range(1, 257))), 48)
+    bits = list(ac.to_bin.bits(iter(data)))
+    dec = AC(CDFPredictor(list(range(1, 257))), 48).from_bin
+    stepped = [s for b in bits for s in dec.step(b)]
+    assert stepped == list(ac.from_bin.run(bits, stop=0)) and bytes(stepped[:len(data)]) == data
 
 
 def test_probpredictor_subclass_adaptive():
