@@ -400,6 +400,10 @@ class A_from_bin:
         ``stop=1`` does not run the reference's heuristic flush (:300-317),
         which raises on about a fifth of valid streams (SURVEY.md finding 5).
         """
+        if hasattr(self, "_sbits") and n is None:
+            # bits already fed through step(): the reference's run is step() over each
+            # bit (arith_code.py:322-326), continuing from where those left off
+            return iter([s for b in bits for s in self._step_bit(int(b))])
         bl = [int(b) for b in bits]
         data = bytes(group_bits(iter(bl)))
         return iter(self._decode_bytes(data, len(bl), n, max_symbols))

@@ -123,6 +123,10 @@ def test_bit_serial_step_matches_reference():
     dec = AC(CDFPredictor(list(range(1, 257))), 48).from_bin
     stepped = [s for b in bits for s in dec.step(b)]
     assert stepped == list(ac.from_bin.run(bits, stop=0)) and bytes(stepped[:len(data)]) == data
+    # run() on a decoder that step() has fed continues it, as the reference's run does
+    dec = AC(CDFPredictor(list(range(1, 257))), 48).from_bin
+    head = [s for b in bits[:1000] for s in dec.step(b)]
+    assert head + list(dec.run(bits[1000:], stop=0)) == stepped
 
 
 def test_probpredictor_subclass_adaptive():
