@@ -408,6 +408,38 @@ class A_from_bin:
         data = bytes(group_bits(iter(bl)))
         return iter(self._decode_bytes(data, len(bl), n, max_symbols))
 
+    # ---- registers (arith_code.py:249-263): l, h and the received-bit interval [lb, hb]
+    # in the same frame; bit-serial decoding keeps them on the host between bits
+    @property
+    def l(self):
+        return int(self._sstate["l"][0]) if hasattr(self, "_sstate") else 0
+
+    @property
+    def h(self):
+        return int(self._sstate["h"][0]) if hasattr(self, "_sstate") else self.denom - 1
+
+    def _pad(self):
+        if not hasattr(self, "_sstate"):
+            return self.precision
+        past = int(self._sstate["pos"][0]) - len(self._sbits)
+        return min(max(past, 0), self.precision)
+
+    @property
+    def lb(self):
+        return int(self._sstate["x"][0]) if hasattr(self, "_sstate") else 0
+
+    @property
+    def hb(self):
+        return self.lb + (1 << self._pad()) - 1
+
+    def __repr__(self):
+        sl = bin(self.l + (self.denom << 1))[3:]
+        sh = bin(self.h + (self.denom << 1))[3:]
+        slb = bin(self.lb + (self.denom << 1))[3:]
+        shb = bin(self.hb + (self.denom << 1))[3:]
+        slb = "".join(slb[i] for i in range(len(slb)) if slb[i] == shb[i])
+        return f"A_from_bin([{sl[0]}.{sl[1:]},{sh[0]}.{sh[1:]}],{slb[0]}.{slb[1:]})"
+
     # ---- bit-serial decoding: step(bit) / __call__(bit) (arith_code.py:291-298, 318-321)
     _DEC_STATE = np.dtype([("l", "<i8"), ("h", "<i8"), ("x", "<i8"), ("pos", "<u8"), ("nsym", "<i8"),
                            ("err", "<i4"), ("det", "<i4"), ("err_step", "<i8"), ("ndet", "<i8")])   # lac_dec_state

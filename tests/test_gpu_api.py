@@ -123,6 +123,18 @@ def test_bit_serial_step_matches_reference():
     dec = AC(CDFPredictor(list(range(1, 257))), 48).from_bin
     stepped = [s for b in bits for s in dec.step(b)]
     assert stepped == list(ac.from_bin.run(bits, stop=0)) and bytes(stepped[:len(data)]) == data
+    # the registers after each bit: l <= lb <= hb <= h once a symbol is out, and the
+    # [lb, hb] interval halves per received bit as receive_bit does (:264-267)
+    dec = AC(CDFPredictor(list(range(1, 257))), 48).from_bin
+    assert (dec.l, dec.h, dec.lb, dec.hb) == (0, (1 << 48) - 1, 0, (1 << 48) - 1)
+    for i, b in enumerate(bits[:300]):
+        w = dec.hb - dec.lb + 1
+        before = (dec.lb, dec.h - dec.l)
+        out = list(dec.step(b))
+        if not out:
+            assert dec.hb - dec.lb + 1 == w // 2 and dec.lb == before[0] + b * (w // 2)
+        assert dec.l <= dec.lb <= dec.hb <= dec.h or not out
+    assert repr(dec).startswith("A_from_bin([")
     # run() on a decoder that step() has fed continues it, as the reference's run does
     dec = AC(CDFPredictor(list(range(1, 257))), 48).from_bin
     head = [s for b in bits[:1000] for s in dec.step(b)]
