@@ -269,7 +269,10 @@ typedef struct lac_dec_state {
  * lac_decode_open (which binds a longer bit buffer) and a host-side update of x
  * for the bits that arrived since, this resumes a decoder: the bit-serial
  * A_from_bin.step(bit) of the reference (arith_code.py:291-298) is built on it
- * (lac_amd.coder).  Not thread-safe with launches on the same context. */
+ * (lac_amd.coder).  set_state refuses (LAC_E_ARG, nothing copied) register sets
+ * no decoder reaches: l outside [0, 2^prec), h < l, h - l >= 2^prec, pos < prec
+ * (streams with err set are copied as they are).  Not thread-safe with launches
+ * on the same context. */
 int lac_decode_get_state(lac_ctx *ctx, lac_dec_state *host_out, void *stream);
 int lac_decode_set_state(lac_ctx *ctx, const lac_dec_state *host_in, void *stream);
 

@@ -3439,6 +3439,16 @@ int lac_decode_get_state(lac_ctx *c, lac_dec_state *host_out, void *stream) {
 int lac_decode_set_state(lac_ctx *c, const lac_dec_state *host_in, void *stream) {
     if (!c || !host_in) return fail(LAC_E_ARG, "NULL argument");
     if (c->mode != 1) return fail(LAC_E_STATE, "call lac_decode_open first");
+    // only register sets a decoder can reach: 0 <= l < 2^prec, l <= h, h - l < 2^prec,
+    // pos >= prec (the kernels check x against [l, h] themselves)
+    const int64_t D = (int64_t)1 << c->prec;
+    for (int64_t b = 0; b < c->B; b++) {
+        const lac_dec_state &q = host_in[b];
+        if (q.err) continue;
+        if (q.l < 0 || q.l >= D || q.h < q.l || q.h - q.l >= D || q.pos < (uint64_t)c->prec ||
+            q.pos > ((uint64_t)1 << 60) || q.nsym < 0 || q.ndet < 0 || (q.det != 0 && q.det != 1))
+            return fail(LAC_E_ARG, "stream %lld: decoder registers out of range", (long long)b);
+    }
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipMemcpyAsync(c->dec, host_in, sizeof(DecState) * c->B, hipMemcpyHostToDevice, S(stream)));
     HIPCHK(hipStreamSynchronize(S(stream)));

@@ -135,6 +135,20 @@ def test_bit_serial_step_matches_reference():
             assert dec.hb - dec.lb + 1 == w // 2 and dec.lb == before[0] + b * (w // 2)
         assert dec.l <= dec.lb <= dec.hb <= dec.h or not out
     assert repr(dec).startswith("A_from_bin([")
+    # lac_decode_set_state refuses registers no decoder reaches (nothing is copied)
+    import ctypes as C
+    from lac_amd._lib import LacError, check
+    c = dec._scoder
+    st = dec._sstate.copy()
+    for field, bad in (("l", -1), ("h", -5), ("pos", 3)):
+        b = st.copy()
+        b[field] = bad
+        with pytest.raises(LacError):
+            check(c.lib.lac_decode_set_state(c.ctx, b.ctypes.data_as(C.c_void_p), c._stream))
+    b = st.copy()
+    b["h"] = int(b["l"][0]) + (1 << 48)
+    with pytest.raises(LacError):
+        check(c.lib.lac_decode_set_state(c.ctx, b.ctypes.data_as(C.c_void_p), c._stream))
     # run() on a decoder that step() has fed continues it, as the reference's run does
     dec = AC(CDFPredictor(list(range(1, 257))), 48).from_bin
     head = [s for b in bits[:1000] for s in dec.step(b)]
