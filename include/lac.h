@@ -80,7 +80,9 @@ enum {                       /* lac_set_option */
                                       tile-walking prefetch, 15 = 16-wave, 8 vectors/thread in
                                       registers + 8 in LDS (rows <= 16384 vectors; 16 table copies
                                       when the row fits a trimmed last slot, <= 16064 vectors),
-                                      16 = 15 with 8 table copies always; identical results,
+                                      16 = 15 with 8 table copies always, 17 / 18 = the same
+                                      register + LDS form with 4 rows of <= 4096 / 2 rows of
+                                      <= 8192 vectors per 16-wave block; identical results,
                                       only speed differs */
     LAC_OPT_DECODE_FINE = 7,       /* one-wave decode (FUSED path): 1 = one total per 64 vectors of
                                       the row, so only 1 KB is re-read after the search (default,

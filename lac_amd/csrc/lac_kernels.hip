@@ -2248,44 +2248,55 @@ constexpr int kRLLastTrim = 704;                 // last-slot threads of the 16-
 constexpr int kRLTrimMaxVec = 15 * 1024 + kRLLastTrim;   // rows it holds: 16064 vectors
 typedef __attribute__((address_space(3))) void lvoid_t;
 
-template <typename LT, bool DEC, int REP = kRLRep, int LASTN = 1024>
+// NT < 1024: 1024 / NT rows per block, NT threads (NT / 64 waves) each, for
+// shorter rows (c3: bf16 V = 32000 with NT = 256, f32 with NT = 512): each wave
+// holds twice the vectors of the 8-wave register shapes, so the per-row
+// reductions and barriers are spread over twice the bytes, and the CU keeps 4 (2)
+// rows in registers + slots rolling instead of 2.  The max is taken per row; the
+// IMAX fallback (float max, with its own barrier) is taken by the whole block if
+// any of its rows needs it.
+template <typename LT, bool DEC, int REP = kRLRep, int LASTN = 1024, int NT = 1024>
 __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ lg, int64_t step_stride,
                                                          int64_t stream_stride, const int32_t *__restrict__ sym,
                                                          int64_t B, int64_t rows, int64_t V, int64_t t0, uint32_t xsh,
                                                          int64_t G, RowStats *__restrict__ out,
                                                          uint64_t *__restrict__ chunks, float *__restrict__ mrow) {
-    constexpr int N = LogitN<LT>::N, NT = 1024, R = 8, L = 8, NW = 16;
+    constexpr int N = LogitN<LT>::N, R = 8, L = 8, NW = 16, NRB = 1024 / NT, NWR = NT / 64;
+    constexpr int SL = (L - 1) * NT + LASTN;                   // slot vectors per row
     constexpr bool IMAX = LAC_Q1_IMAX && sizeof(LT) == 2;
     static_assert((R + L) * N <= 128, "lane sums must fit 32 bits");
+    static_assert(NT == 256 || NT == 512 || NT == 1024, "rows of 4, 8 or 16 waves");
     static_assert(LASTN % 64 == 0 && LASTN <= NT, "the last slot is trimmed by whole waves");
     constexpr bool TRIM = LASTN < NT;
     __shared__ uint32_t tabr[LAC_Q1_TAB_SIZE * REP];
-    __shared__ u32x4 slots[(L - 1) * NT + LASTN];
+    __shared__ u32x4 slots[NRB * SL];
     __shared__ float smax[NW];
     __shared__ int smaxi[NW];
     __shared__ uint64_t ssum[NW][2];
-    __shared__ uint32_t sps;
-    __shared__ unsigned long long gtot[DEC ? NW * (R + L) : 1];   // DEC: every 64-vector group's total
+    __shared__ uint32_t sps[NRB];
+    __shared__ unsigned long long gtot[DEC ? NRB * NWR * (R + L) : 1];   // DEC: every 64-vector group's total
     int tid = threadIdx.x;
     const int lane = tid & 63, w = wave_in_block();
+    const int g = w / NWR, wg = w % NWR;                      // this wave's row of the block, wave in that row
     // (the fast fill below the first row's loads, as in k_q1_stats, spilled this
     // kernel at its 128-VGPR cap: 2.52 -> 2.70 ms at bf16 V = 128256)
     q1_load_tab_rep<REP>(tabr, xsh);
     const uint32_t loff = (uint32_t)(lane & (REP - 1)) << 2;
     const int nvec = (int)(V / N);
     // TRIM: waves past LASTN have no last slot (their vectors there lie beyond the row)
-    const bool noslot = TRIM && w * 64 >= LASTN;
-    const int64_t stride = gridDim.x;
+    const bool noslot = TRIM && wg * 64 >= LASTN;
+    const int64_t stride = (int64_t)gridDim.x * NRB;
     auto row_of = [&](int64_t r) { return lg + (t0 + r / B) * step_stride + (r % B) * stream_stride; };
+    auto gti = [&]() { return tid - g * NT; };                 // thread index in the row
     // vector j of this thread (clamped into the row: a duplicate cannot change the
     // maximum, and the sums mask out-of-row vectors)
-    auto vidx = [&](int j) { const int vi = j * NT + tid; return vi < nvec ? vi : nvec - 1; };
-    auto ld_reg = [&](const RowSrc<true, sizeof(LT)> &src, int j) { return src(j * NT + tid); };
+    auto vidx = [&](int j) { const int vi = j * NT + gti(); return vi < nvec ? vi : nvec - 1; };
+    auto ld_reg = [&](const RowSrc<true, sizeof(LT)> &src, int j) { return src(j * NT + gti()); };
     // LDS-DMA as asm: the compiler's own global_load_lds makes every later LDS read
     // wait vmcnt(0) (it cannot tell the slots apart), which serialised the refills.
     // The asm is invisible to its wait counting, so this kernel waits explicitly:
     // vmcnt(0) before pass 1 reads any slot, lgkmcnt(0) before a slot is refilled.
-    const uint32_t slot_base = (uint32_t)(uintptr_t)(lvoid_t *)&slots[w * 64];   // wave-uniform LDS address
+    const uint32_t slot_base = (uint32_t)(uintptr_t)(lvoid_t *)&slots[g * SL + wg * 64];   // wave-uniform
     auto ld_lds = [&](const LT *rw, int k) {
         if (k == L - 1 && noslot) return;                      // wave-uniform
         const u32x4 *src = reinterpret_cast<const u32x4 *>(rw) + vidx(R + k);
@@ -2296,8 +2307,8 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
                      : "memory");
     };
     u32x4 x[R];
-    {                                                          // the block's first row
-        const int64_t r0 = blockIdx.x;
+    {                                                          // the block's first rows
+        const int64_t r0 = (int64_t)blockIdx.x * NRB + g;
         const LT *rw = r0 < rows ? row_of(r0) : lg;
         const RowSrc<true, sizeof(LT)> src(rw, true, nvec);
 #pragma unroll
@@ -2305,11 +2316,13 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
 #pragma unroll
         for (int j = 0; j < R; j++) x[j] = ld_reg(src, j);
     }
-    for (int64_t r = blockIdx.x; r < rows; r += stride) {
+    for (int64_t rb = (int64_t)blockIdx.x * NRB; rb < rows; rb += stride) {
         // tid opaque per row: the per-load addresses derived from it are recomputed
         // next to each load, not hoisted out of the loop and spilled (a spill reload
         // is a VM load: its vmcnt(0) would drain the prefetches)
         asm volatile("" : "+v"(tid));
+        const int64_t r = rb + g;
+        const bool valid = r < rows;
         const int64_t rn = r + stride;
         const LT *nrow = rn < rows ? row_of(rn) : lg;
         // pass 1: the row maximum over registers and slots (everything has landed)
@@ -2319,7 +2332,7 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
         // (a wave without a last slot reads the neutral -inf: no other wave's DMA
         // writes are waited for here, and those vectors are masked from the sums)
         auto slot = [&](int k) {
-            return (k == L - 1 && noslot) ? neg_inf16(sizeof(LT)) : slots[k * NT + tid];
+            return (k == L - 1 && noslot) ? neg_inf16(sizeof(LT)) : slots[g * SL + k * NT + gti()];
         };
         float m;
         if constexpr (IMAX) {
@@ -2339,12 +2352,19 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
                 return (uint32_t)((int)a > (int)b ? (int)a : (int)b);
             });
             if (lane == 0) smaxi[w] = wi;
-            if (!DEC && tid == 0) sps = 0;
+            if (!DEC && gti() == 0) sps[g] = 0;
             __syncthreads();
-            int bi = smaxi[0];
+            int bi = 0;
+            bool all_ok = true;                                // block-uniform: every row's int max usable
 #pragma unroll
-            for (int i = 1; i < NW; i++) bi = smaxi[i] > bi ? smaxi[i] : bi;
-            if (bi >= 0 && bi <= 0x7F80) {                    // block-uniform (see k_q1_stats)
+            for (int gg = 0; gg < NRB; gg++) {
+                int bm = smaxi[gg * NWR];
+#pragma unroll
+                for (int i = 1; i < NWR; i++) bm = smaxi[gg * NWR + i] > bm ? smaxi[gg * NWR + i] : bm;
+                all_ok = all_ok && bm >= 0 && bm <= 0x7F80;
+                bi = gg == g ? bm : bi;
+            }
+            if (all_ok) {                                      // (see k_q1_stats)
                 m = __uint_as_float((uint32_t)bi << 16);
             } else {
                 float mx = -INFINITY;
@@ -2361,9 +2381,9 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
                 mx = wave_max_f32(mx);
                 if (lane == 0) smax[w] = mx;
                 __syncthreads();
-                m = smax[0];
+                m = smax[g * NWR];
 #pragma unroll
-                for (int i = 1; i < NW; i++) m = fmaxf(m, smax[i]);
+                for (int i = 1; i < NWR; i++) m = fmaxf(m, smax[g * NWR + i]);
             }
         } else {
             float mx = -INFINITY;
@@ -2379,24 +2399,24 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
             }
             mx = wave_max_f32(mx);
             if (lane == 0) smax[w] = mx;
-            if (!DEC && tid == 0) sps = 0;
+            if (!DEC && gti() == 0) sps[g] = 0;
             __syncthreads();
-            m = smax[0];
+            m = smax[g * NWR];
 #pragma unroll
-            for (int i = 1; i < NW; i++) m = fmaxf(m, smax[i]);
+            for (int i = 1; i < NWR; i++) m = fmaxf(m, smax[g * NWR + i]);
         }
-        if (DEC && tid == 0) mrow[r] = m;                     // now: m is not held over pass 2
+        if (DEC && valid && gti() == 0) mrow[r] = m;          // now: m is not held over pass 2
         const bool fast = q1_fast_row(m);
         const float c = q1_c(m);
         int sfull = -1, sr = 0;
-        if (!DEC) {
+        if (!DEC && valid) {
             const int64_t s = sym[(t0 + r / B) * B + r % B];
             const int sc = (int)(s < 0 ? 0 : (s > V ? V : s));
             sfull = sc / N;
             sr = sc - sfull * N;
         }
         uint32_t tot = 0, lo = 0, sv[8];                     // DEC: one half's vector sums
-        if (!DEC && sfull < nvec && (sfull & (NT - 1)) == tid) {
+        if (!DEC && sfull >= 0 && sfull < nvec && (sfull & (NT - 1)) == gti()) {
             // the vector holding s, split once before pass 2 (both halves still hold
             // this row): one copy of this code instead of one per vector in pass 2
             const int js = sfull / NT;
@@ -2411,11 +2431,11 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
                 ps += e == sr ? q : 0;
             }
             lo = pl;
-            sps = ps;
+            sps[g] = ps;
         }
         // pass 2 (slots first, so their refills are issued earliest)
         auto take = [&](int j, const u32x4 &v, uint32_t sl) {
-            const int vi = j * NT + tid;
+            const int vi = j * NT + gti();
             sl = vi < nvec ? sl : 0;
             if (DEC) {
                 sv[j & 7] = sl;
@@ -2439,7 +2459,7 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
             // than held across the row loop -- held, they spilled, and the reload's
             // vmcnt(0) waited for the next row's slot loads just issued)
             const int ln = lane_fresh();
-            if (ln < 8) gtot[w + NW * (j0 + q_index<8>(ln))] = gsum;   // vectors [grp*64, +64)
+            if (ln < 8) gtot[g * NWR * (R + L) + wg + NWR * (j0 + q_index<8>(ln))] = gsum;   // [grp*64, +64)
         };
         auto pair_halve = [&](int k) {                         // k: the vector just taken (compile-time)
             if (!DEC) return;
@@ -2474,27 +2494,27 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
             }
             if (DEC) bin_half(0);
         };
-        if (fast) pass2(true); else pass2(false);             // row-uniform
+        if (fast) pass2(true); else pass2(false);             // row-uniform (a wave is in one row)
         if (!DEC) {
             const uint64_t t64 = wave_sum_u64(tot), l64 = wave_sum_u64(lo);
             if (lane == 0) { ssum[w][0] = t64; ssum[w][1] = l64; }
         }
         __syncthreads();
         if (DEC) {
-            if (w == 0) {
+            if (wg == 0 && valid) {
                 // chunk c = groups [c G, (c + 1) G) of the row's ngrp groups
                 const int ngrp = (nvec + 63) / 64, ln = lane_fresh(), g0 = ln * (int)G;
                 uint64_t ct = 0;
-                for (int gi = g0; gi < g0 + (int)G && gi < ngrp; gi++) ct += gtot[gi];
+                for (int gi = g0; gi < g0 + (int)G && gi < ngrp; gi++) ct += gtot[g * NWR * (R + L) + gi];
                 chunks[r * 64 + ln] = ct;
             }
-        } else if (tid == 0) {
+        } else if (gti() == 0 && valid) {
             uint64_t T = 0, Ls = 0;
 #pragma unroll
-            for (int i = 0; i < NW; i++) { T += ssum[i][0]; Ls += ssum[i][1]; }
+            for (int i = 0; i < NWR; i++) { T += ssum[g * NWR + i][0]; Ls += ssum[g * NWR + i][1]; }
             RowStats st;
             st.lo = Ls;
-            st.hi = Ls + sps;
+            st.hi = Ls + sps[g];
             st.tot = T;
             st.minp = 1;
             st.inv_tot = 1.0 / (double)T;
@@ -3017,23 +3037,40 @@ static int q1_stats_launch(lac_ctx *c, const Q1Args &a, hipStream_t st) {
     return LAC_OK;
 }
 
-// trim: the 16-copy form with a trimmed last slot, for rows of <= kRLTrimMaxVec vectors
-template <typename LT, bool DEC>
-static int q1_stats_rl_launch(lac_ctx *c, const Q1Args &a, hipStream_t st, bool trim) {
-    const int64_t need = a.rows, cap = (int64_t)c->cus;     // one 16-wave block per CU
+template <typename LT, bool DEC, int REP, int LASTN, int NT>
+static int q1_rl_kernel(lac_ctx *c, const Q1Args &a, hipStream_t st) {
+    constexpr int NRB = 1024 / NT;
+    const int64_t need = (a.rows + NRB - 1) / NRB, cap = (int64_t)c->cus;   // one 16-wave block per CU
     const unsigned grid = (unsigned)(need < cap ? need : cap);
     const int64_t nvec = c->V / LogitN<LT>::N;
     ProfScope ps(c, KID_Q1_STATS, st);
-    if (trim && nvec <= kRLTrimMaxVec)
-        k_q1_stats_rl<LT, DEC, 16, kRLLastTrim><<<grid, 1024, 0, st>>>(
-            (const LT *)a.lg, a.ss, a.bs, a.sym, c->B, a.rows, c->V, a.t0, a.xsh, q1_groups_per_chunk(nvec),
-            c->stats, c->q1chunks, c->q1m);
-    else
-        k_q1_stats_rl<LT, DEC><<<grid, 1024, 0, st>>>((const LT *)a.lg, a.ss, a.bs, a.sym, c->B, a.rows, c->V,
-                                                       a.t0, a.xsh, q1_groups_per_chunk(nvec), c->stats,
-                                                       c->q1chunks, c->q1m);
+    k_q1_stats_rl<LT, DEC, REP, LASTN, NT><<<grid, 1024, 0, st>>>(
+        (const LT *)a.lg, a.ss, a.bs, a.sym, c->B, a.rows, c->V, a.t0, a.xsh, q1_groups_per_chunk(nvec), c->stats,
+        c->q1chunks, c->q1m);
     CHECK_LAUNCH();
     return LAC_OK;
+}
+
+// The register + LDS-slot shapes (k_q1_stats_rl), by rows per block:
+//   15 = one row of <= 16384 vectors (16 table copies when <= 16064: trimmed last slot), 16 = the same with 8
+//   copies always, 17 = four rows of <= 4096 vectors (4 waves each), 18 = two rows of <= 8192 (8 waves each).
+// A trimmed last slot (whole waves only) makes room for 16 table copies where the LDS allows it.
+template <typename LT, bool DEC>
+static int q1_stats_rl_launch(lac_ctx *c, const Q1Args &a, hipStream_t st, int shape) {
+    const int64_t nvec = c->V / LogitN<LT>::N;
+    switch (shape) {
+    case 15:
+        if (nvec <= kRLTrimMaxVec) return q1_rl_kernel<LT, DEC, 16, kRLLastTrim, 1024>(c, a, st);
+        return q1_rl_kernel<LT, DEC, kRLRep, 1024, 1024>(c, a, st);
+    case 16:
+        return q1_rl_kernel<LT, DEC, kRLRep, 1024, 1024>(c, a, st);
+    case 17:                                       // LDS: 4 x 31 KB of slots + 16 copies (encode) / 8 (decode)
+        if (nvec <= 15 * 256 + 192) return q1_rl_kernel<LT, DEC, DEC ? 8 : 16, 192, 256>(c, a, st);
+        return q1_rl_kernel<LT, DEC, kRLRep, 256, 256>(c, a, st);
+    default:                                       // 18 -- LDS: 2 x 61 KB of slots + 16 copies
+        if (nvec <= 15 * 512 + 320) return q1_rl_kernel<LT, DEC, 16, 320, 512>(c, a, st);
+        return q1_rl_kernel<LT, DEC, kRLRep, 512, 512>(c, a, st);
+    }
 }
 
 // Row-group shapes (waves per row RW, 16-B vectors per thread R, rolling
@@ -3054,7 +3091,15 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
     auto holds = [&](int i) { return nvec <= 64 * kQ1Shapes[i - 1][0] * kQ1Shapes[i - 1][1]; };
     if (sh == 0) {                     // decode: the prefetching (8,8) spills around the multi-sum
         static const int enc_order[] = {1, 2, 3, 6, 5}, dec_order[] = {1, 2, 3, 4, 5};
+        // several rows per 16-wave block in registers + LDS slots (shapes 17 / 18; same-box,
+        // profiles/r02/q1_rl_rows/): rows of 4097..8192 vectors in both directions (bf16
+        // V = 65536 encode 1.48 -> 1.31 ms, f32 c3 1.241 -> 1.200 ms = 87 % of peak, decode
+        // stats 2-3 % faster), f32 rows of 2049..4096 vectors in encode (V = 16384: 0.678 ->
+        // 0.621 ms).  bf16 c3 keeps shape 6 to encode (0.651 vs 0.660 ms) and 4 to decode.
+        if (nvec > 4096 && nvec <= 8192) sh = 18;
+        else if (!DEC && sizeof(LT) == 4 && nvec > 2048 && nvec <= 4096) sh = 17;
         for (int i : DEC ? dec_order : enc_order) {
+            if (sh) break;
             // f32 rows of 4097..8192 vectors: one 16-wave block per CU with rolling
             // prefetch, (16,8,y) = shape 11, before (8,16,n) (c3 f32: encode 1.33 vs
             // 1.39 ms; decode, once the buffer-form loads removed its spills, 45.0 vs
@@ -3078,13 +3123,15 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
     if (sh == 10) return q1_stats_launch<LT, 16, 16, DEC, true, false, 16>(c, a, st);   // tiles of 16384
     if (sh == 11 && nvec <= 64 * 16 * 8) return q1_stats_launch<LT, 16, 8, DEC, false, true, 16>(c, a, st);
     if (sh == 12 && nvec <= 64 * 16 * 8) return q1_stats_launch<LT, 16, 8, DEC, false, false, 16>(c, a, st);
-    // registers + LDS slots: 15 = 16 table copies where the trimmed slots hold the row, else
-    // 8; 16 = always 8 copies (tuning)
-    if ((sh == 15 || sh == 16) && nvec <= 16384) return q1_stats_rl_launch<LT, DEC>(c, a, st, sh == 15);
+    // registers + LDS slots (q1_stats_rl_launch): 15 / 16 one row of <= 16384 vectors per
+    // block, 17 four rows of <= 4096, 18 two rows of <= 8192
+    if ((sh == 15 || sh == 16) && nvec <= 16384) return q1_stats_rl_launch<LT, DEC>(c, a, st, sh);
+    if (sh == 17 && nvec <= 4096) return q1_stats_rl_launch<LT, DEC>(c, a, st, 17);
+    if (sh == 18 && nvec <= 8192) return q1_stats_rl_launch<LT, DEC>(c, a, st, 18);
     if (sh == 13) return q1_stats_launch<LT, 8, 8, DEC, true, true>(c, a, st);         // tiles of (8,8,y)
     if (sh == 14) return q1_stats_launch<LT, 16, 8, DEC, true, true, 16>(c, a, st);    // tiles of (16,8,y)
     if (sh == 8) return q1_stats_launch<LT, 8, 8, DEC, true, false>(c, a, st);      // tiles of 4096 vectors
-    // shapes 9, 11, 12, 15, 16 with a row too long for them, and 1..7 likewise (kQ1Shapes
+    // shapes 9, 11, 12, 15..18 with a row too long for them, and 1..7 likewise (kQ1Shapes
     // describes 1..7 only: a forced 11 / 12 used to index past it)
     if (sh > 7 || !holds(sh))
         return fail(LAC_E_ARG, "q1 shape %d does not hold a row of %lld vectors", sh, (long long)nvec);
@@ -3278,7 +3325,7 @@ int lac_set_option(lac_ctx *c, int option, int64_t value) {
         c->fine_decode = (int)value;
         return LAC_OK;
     case LAC_OPT_Q1_SHAPE:
-        if (value < 0 || value > 16) return fail(LAC_E_ARG, "bad q1 shape");
+        if (value < 0 || value > 18) return fail(LAC_E_ARG, "bad q1 shape");
         c->q1_shape = (int)value;
         return LAC_OK;
     case LAC_OPT_MAPPING:

@@ -249,7 +249,7 @@ def test_every_q1_shape_gives_the_same_bits(dtype, V):
     c.encode_logits_job(dl, sym)
     want, wn = c.to_bytes()
     ran = 0
-    for sh in range(1, 17):
+    for sh in range(1, 19):
         c.set_q1_shape(sh)
         try:
             c.encode_logits_job(dl, sym)
