@@ -2255,16 +2255,59 @@ typedef __attribute__((address_space(3))) void lvoid_t;
 // rows in registers + slots rolling instead of 2.  The max is taken per row; the
 // IMAX fallback (float max, with its own barrier) is taken by the whole block if
 // any of its rows needs it.
-template <typename LT, bool DEC, int REP = kRLRep, int LASTN = 1024, int NT = 1024>
+//
+// PAIR: rows of up to 2 x 16064 vectors (f32 V <= 128512: Llama-3's 128256 in f32,
+// which no CU's registers + LDS hold) split over a pair of blocks, each holding one
+// half exactly as above.  The halves meet twice per row: the row maximum (each
+// block posts its half's maximum with the row's sequence number into one of two
+// alternating words and waits for its partner's: the only wait), and the sums
+// (each half adds its partials -- total, lo, hi, or its 64 chunk partials -- into
+// the row's zeroed outputs with relaxed device-scope atomics: no wait, and no
+// fence -- a release/acquire fence here writes back / invalidates the whole L2 and
+// cost ~35 us per row).  A pair shares an XCD (blocks b and b ^ 8; dispatch is
+// round-robin over the 8 XCDs), the grid never exceeds the CU count (one block per
+// CU: both halves are resident), and the wait is bounded: a partner that never
+// posts poisons the row's total (+2^62: LAC_E_TABLE at the coder) instead of
+// hanging the GPU.
+constexpr uint32_t kPairSpinMax = 1u << 24;                 // ~1 s of s_sleep 2
+
+__device__ inline uint64_t pair_ld(const uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// post this half's row maximum (sequence number seq >= 1) and return the partner's;
+// *ok = false when it never came
+__device__ inline float pair_exchange_max(uint64_t *xch, uint32_t seq, float m, bool *ok) {
+    const unsigned b = blockIdx.x, slot = seq & 1;
+    __hip_atomic_store(&xch[2 * b + slot], ((uint64_t)seq << 32) | __float_as_uint(m), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t *px = &xch[2 * (b ^ 8u) + slot];
+    uint64_t v = pair_ld(px);
+    for (uint32_t n = 0; (uint32_t)(v >> 32) != seq && n < kPairSpinMax; n++) {
+        __builtin_amdgcn_s_sleep(2);
+        v = pair_ld(px);
+    }
+    *ok = (uint32_t)(v >> 32) == seq;
+    return __uint_as_float((uint32_t)v);
+}
+
+__device__ inline void pair_add(uint64_t *p, uint64_t v) {
+    (void)__hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+constexpr uint64_t kPairPoison = 1ull << 62;                 // a failed exchange: the row's total is >= 2^62
+
+template <typename LT, bool DEC, int REP = kRLRep, int LASTN = 1024, int NT = 1024, bool PAIR = false>
 __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ lg, int64_t step_stride,
                                                          int64_t stream_stride, const int32_t *__restrict__ sym,
                                                          int64_t B, int64_t rows, int64_t V, int64_t t0, uint32_t xsh,
                                                          int64_t G, RowStats *__restrict__ out,
-                                                         uint64_t *__restrict__ chunks, float *__restrict__ mrow) {
+                                                         uint64_t *__restrict__ chunks, float *__restrict__ mrow,
+                                                         uint64_t *__restrict__ xch, int split) {
     constexpr int N = LogitN<LT>::N, R = 8, L = 8, NW = 16, NRB = 1024 / NT, NWR = NT / 64;
     constexpr int SL = (L - 1) * NT + LASTN;                   // slot vectors per row
-    constexpr bool IMAX = LAC_Q1_IMAX && sizeof(LT) == 2;
+    constexpr bool IMAX = LAC_Q1_IMAX && sizeof(LT) == 2 && !PAIR;
     static_assert((R + L) * N <= 128, "lane sums must fit 32 bits");
+    static_assert(!PAIR || NT == 1024, "pairs: one row half per block");
     static_assert(NT == 256 || NT == 512 || NT == 1024, "rows of 4, 8 or 16 waves");
     static_assert(LASTN % 64 == 0 && LASTN <= NT, "the last slot is trimmed by whole waves");
     constexpr bool TRIM = LASTN < NT;
@@ -2282,11 +2325,20 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
     // kernel at its 128-VGPR cap: 2.52 -> 2.70 ms at bf16 V = 128256)
     q1_load_tab_rep<REP>(tabr, xsh);
     const uint32_t loff = (uint32_t)(lane & (REP - 1)) << 2;
-    const int nvec = (int)(V / N);
+    // PAIR: block b holds half hh = (b >> 3) & 1 of the rows of pair (b >> 4) * 8 + (b & 7)
+    const int hh = PAIR ? (int)((blockIdx.x >> 3) & 1) : 0;
+    const int64_t bix = PAIR ? (int64_t)((blockIdx.x >> 4) * 8 + (blockIdx.x & 7)) : (int64_t)blockIdx.x;
+    const int vofs = hh * split;                                // vectors of the row before this half
+    const int nvec = (int)(V / N) - (PAIR ? (hh ? split : (int)(V / N) - split) : 0);
     // TRIM: waves past LASTN have no last slot (their vectors there lie beyond the row)
     const bool noslot = TRIM && wg * 64 >= LASTN;
-    const int64_t stride = (int64_t)gridDim.x * NRB;
-    auto row_of = [&](int64_t r) { return lg + (t0 + r / B) * step_stride + (r % B) * stream_stride; };
+    const int64_t stride = (int64_t)(PAIR ? gridDim.x / 2 : gridDim.x) * NRB;
+    auto row_of = [&](int64_t r) {
+        return lg + (t0 + r / B) * step_stride + (r % B) * stream_stride + (int64_t)vofs * N;
+    };
+    __shared__ float sxm;
+    __shared__ int sxok;
+    uint32_t seq = 0;                                           // PAIR: rows done + 1
     auto gti = [&]() { return tid - g * NT; };                 // thread index in the row
     // vector j of this thread (clamped into the row: a duplicate cannot change the
     // maximum, and the sums mask out-of-row vectors)
@@ -2308,7 +2360,7 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
     };
     u32x4 x[R];
     {                                                          // the block's first rows
-        const int64_t r0 = (int64_t)blockIdx.x * NRB + g;
+        const int64_t r0 = bix * NRB + g;
         const LT *rw = r0 < rows ? row_of(r0) : lg;
         const RowSrc<true, sizeof(LT)> src(rw, true, nvec);
 #pragma unroll
@@ -2316,7 +2368,7 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
 #pragma unroll
         for (int j = 0; j < R; j++) x[j] = ld_reg(src, j);
     }
-    for (int64_t rb = (int64_t)blockIdx.x * NRB; rb < rows; rb += stride) {
+    for (int64_t rb = bix * NRB; rb < rows; rb += stride) {
         // tid opaque per row: the per-load addresses derived from it are recomputed
         // next to each load, not hoisted out of the loop and spilled (a spill reload
         // is a VM load: its vmcnt(0) would drain the prefetches)
@@ -2405,7 +2457,19 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
 #pragma unroll
             for (int i = 1; i < NWR; i++) m = fmaxf(m, smax[g * NWR + i]);
         }
-        if (DEC && valid && gti() == 0) mrow[r] = m;          // now: m is not held over pass 2
+        bool pok = true;
+        if constexpr (PAIR) {                                  // the row maximum of both halves
+            seq++;
+            if (tid == 0) {
+                bool ok;
+                sxm = pair_exchange_max(xch, seq, m, &ok);
+                sxok = ok;
+            }
+            __syncthreads();
+            m = fmaxf(m, sxm);                                 // = fmaxf over the whole row
+            pok = sxok != 0;
+        }
+        if (DEC && valid && gti() == 0 && hh == 0) mrow[r] = m;   // now: m is not held over pass 2
         const bool fast = q1_fast_row(m);
         const float c = q1_c(m);
         int sfull = -1, sr = 0;
@@ -2414,6 +2478,7 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
             const int sc = (int)(s < 0 ? 0 : (s > V ? V : s));
             sfull = sc / N;
             sr = sc - sfull * N;
+            sfull -= vofs;                                     // PAIR: < 0 in the second half when s is in the first
         }
         uint32_t tot = 0, lo = 0, sv[8];                     // DEC: one half's vector sums
         if (!DEC && sfull >= 0 && sfull < nvec && (sfull & (NT - 1)) == gti()) {
@@ -2503,18 +2568,34 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
         if (DEC) {
             if (wg == 0 && valid) {
                 // chunk c = groups [c G, (c + 1) G) of the row's ngrp groups
-                const int ngrp = (nvec + 63) / 64, ln = lane_fresh(), g0 = ln * (int)G;
+                // PAIR: this half's groups are the row's [gofs, gofs + ngrp) (split is a multiple of 64)
+                const int ngrp = (nvec + 63) / 64, ln = lane_fresh(), gofs = vofs / 64;
+                const int g0 = ln * (int)G, ga = g0 > gofs ? g0 : gofs;
+                const int gb = g0 + (int)G < gofs + ngrp ? g0 + (int)G : gofs + ngrp;
                 uint64_t ct = 0;
-                for (int gi = g0; gi < g0 + (int)G && gi < ngrp; gi++) ct += gtot[g * NWR * (R + L) + gi];
-                chunks[r * 64 + ln] = ct;
+                for (int gi = ga; gi < gb; gi++) ct += gtot[g * NWR * (R + L) + gi - gofs];
+                if constexpr (PAIR) {                          // into the zeroed chunk totals
+                    const uint64_t v = ct + (pok ? 0 : kPairPoison);
+                    if (v) pair_add(&chunks[r * 64 + ln], v);
+                } else {
+                    chunks[r * 64 + ln] = ct;
+                }
             }
         } else if (gti() == 0 && valid) {
-            uint64_t T = 0, Ls = 0;
+            uint64_t T = 0, Ls = 0, ps = sps[g];
 #pragma unroll
             for (int i = 0; i < NWR; i++) { T += ssum[g * NWR + i][0]; Ls += ssum[g * NWR + i][1]; }
+            if constexpr (PAIR) {                              // the halves' partials add up
+                RowStats *o = out + r;                         // (zeroed; inv_tot 0: the coder divides)
+                pair_add(&o->tot, T + (pok ? 0 : kPairPoison));
+                pair_add(&o->lo, Ls);
+                pair_add(&o->hi, Ls + ps);
+                if (hh == 0) __hip_atomic_store(&o->minp, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                continue;
+            }
             RowStats st;
             st.lo = Ls;
-            st.hi = Ls + sps[g];
+            st.hi = Ls + ps;
             st.tot = T;
             st.minp = 1;
             st.inv_tot = 1.0 / (double)T;
@@ -2711,6 +2792,7 @@ struct lac_ctx {
     uint64_t *q1chunks = nullptr;       // logits / stats-path decode: [chunk_steps * B][64] chunk totals
     void *dmeta = nullptr;              // stats-path decode: [chunk_steps * B] DecRowMeta
     float *q1m = nullptr;               //                [chunk_steps * B] row maxima
+    uint64_t *pxch = nullptr;           // paired row stats (shape 19): [2 * cus] maximum words
     // live kernel timing (lac_profile_enable): hipEvent pairs around launches
     bool prof = false;
     std::vector<hipEvent_t> ev_pool;
@@ -3046,9 +3128,43 @@ static int q1_rl_kernel(lac_ctx *c, const Q1Args &a, hipStream_t st) {
     ProfScope ps(c, KID_Q1_STATS, st);
     k_q1_stats_rl<LT, DEC, REP, LASTN, NT><<<grid, 1024, 0, st>>>(
         (const LT *)a.lg, a.ss, a.bs, a.sym, c->B, a.rows, c->V, a.t0, a.xsh, q1_groups_per_chunk(nvec), c->stats,
-        c->q1chunks, c->q1m);
+        c->q1chunks, c->q1m, nullptr, 0);
     CHECK_LAUNCH();
     return LAC_OK;
+}
+
+// Paired row stats (shape 19): the first half of a row holds 64 * floor(groups / 2)
+// vectors, the second the rest; both halves must fit one block's registers + slots.
+static int q1_pair_split(int64_t nvec) { return (int)(64 * (((nvec + 63) / 64) / 2)); }
+static bool q1_pair_holds(lac_ctx *c, int64_t nvec) {
+    return c->cus >= 16 && nvec > 16384 && nvec - q1_pair_split(nvec) <= 16384;
+}
+
+template <typename LT, bool DEC, int REP, int LASTN>
+static int q1_pair_kernel(lac_ctx *c, const Q1Args &a, hipStream_t st) {
+    const int64_t nvec = c->V / LogitN<LT>::N;
+    if (!c->pxch) HIPCHK(hipMalloc(&c->pxch, sizeof(uint64_t) * 2 * c->cus));
+    // pairs (b, b ^ 8) in groups of 16 blocks; never more blocks than CUs (one per CU:
+    // both halves of every pair resident at once)
+    const int64_t need = 16 * ((a.rows + 7) / 8), cap = (int64_t)(c->cus / 16) * 16;
+    const unsigned grid = (unsigned)(need < cap ? need : cap);
+    HIPCHK(hipMemsetAsync(c->pxch, 0, sizeof(uint64_t) * 2 * grid, st));   // no stale sequence numbers
+    // the halves add into zeroed outputs
+    if (DEC) HIPCHK(hipMemsetAsync(c->q1chunks, 0, sizeof(uint64_t) * 64 * a.rows, st));
+    else HIPCHK(hipMemsetAsync(c->stats, 0, sizeof(RowStats) * a.rows, st));
+    ProfScope ps(c, KID_Q1_STATS, st);
+    k_q1_stats_rl<LT, DEC, REP, LASTN, 1024, true><<<grid, 1024, 0, st>>>(
+        (const LT *)a.lg, a.ss, a.bs, a.sym, c->B, a.rows, c->V, a.t0, a.xsh, q1_groups_per_chunk(nvec), c->stats,
+        c->q1chunks, c->q1m, c->pxch, q1_pair_split(nvec));
+    CHECK_LAUNCH();
+    return LAC_OK;
+}
+
+template <typename LT, bool DEC>
+static int q1_stats_pair_launch(lac_ctx *c, const Q1Args &a, hipStream_t st) {
+    const int64_t nvec = c->V / LogitN<LT>::N, sp = q1_pair_split(nvec);
+    if (sp <= kRLTrimMaxVec && nvec - sp <= kRLTrimMaxVec) return q1_pair_kernel<LT, DEC, 16, kRLLastTrim>(c, a, st);
+    return q1_pair_kernel<LT, DEC, kRLRep, 1024>(c, a, st);
 }
 
 // The register + LDS-slot shapes (k_q1_stats_rl), by rows per block:
@@ -3113,6 +3229,8 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
         // spills were removed (streamed butterfly, per-group LDS totals, fresh lane index),
         // 220 -> 210 us per step of 4096 rows vs shape 9, profiles/r02/q1_rl_dec/)
         if (sh == 0 && nvec <= 16384) sh = 15;
+        // longer rows that two blocks' registers + slots hold: one half per block (shape 19)
+        if (sh == 0 && sizeof(LT) == 4 && q1_pair_holds(c, nvec)) sh = 19;   // (bf16 pairs spill)
         // measured at V = 128256 f32: encode tiles of (16,8) with the tile-rolling
         // prefetch 1.98 ms vs 2.18 for tiles of (8,8) (shape 13, its (8,8) form: 2.20)
         if (sh == 0) sh = nvec <= 64 * 16 * 16 ? 9 : (DEC ? 10 : (sizeof(LT) == 4 ? 14 : 8));
@@ -3128,10 +3246,11 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
     if ((sh == 15 || sh == 16) && nvec <= 16384) return q1_stats_rl_launch<LT, DEC>(c, a, st, sh);
     if (sh == 17 && nvec <= 4096) return q1_stats_rl_launch<LT, DEC>(c, a, st, 17);
     if (sh == 18 && nvec <= 8192) return q1_stats_rl_launch<LT, DEC>(c, a, st, 18);
+    if (sh == 19 && q1_pair_holds(c, nvec)) return q1_stats_pair_launch<LT, DEC>(c, a, st);
     if (sh == 13) return q1_stats_launch<LT, 8, 8, DEC, true, true>(c, a, st);         // tiles of (8,8,y)
     if (sh == 14) return q1_stats_launch<LT, 16, 8, DEC, true, true, 16>(c, a, st);    // tiles of (16,8,y)
     if (sh == 8) return q1_stats_launch<LT, 8, 8, DEC, true, false>(c, a, st);      // tiles of 4096 vectors
-    // shapes 9, 11, 12, 15..18 with a row too long for them, and 1..7 likewise (kQ1Shapes
+    // shapes 9, 11, 12, 15..19 with a row too long for them, and 1..7 likewise (kQ1Shapes
     // describes 1..7 only: a forced 11 / 12 used to index past it)
     if (sh > 7 || !holds(sh))
         return fail(LAC_E_ARG, "q1 shape %d does not hold a row of %lld vectors", sh, (long long)nvec);
@@ -3266,6 +3385,7 @@ int lac_close(lac_ctx *c) {
     (void)hipFree(c->q1chunks);
     (void)hipFree(c->dmeta);
     (void)hipFree(c->q1m);
+    (void)hipFree(c->pxch);
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
     delete c;
     return LAC_OK;
@@ -3325,7 +3445,7 @@ int lac_set_option(lac_ctx *c, int option, int64_t value) {
         c->fine_decode = (int)value;
         return LAC_OK;
     case LAC_OPT_Q1_SHAPE:
-        if (value < 0 || value > 18) return fail(LAC_E_ARG, "bad q1 shape");
+        if (value < 0 || value > 19) return fail(LAC_E_ARG, "bad q1 shape");
         c->q1_shape = (int)value;
         return LAC_OK;
     case LAC_OPT_MAPPING:

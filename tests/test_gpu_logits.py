@@ -232,13 +232,16 @@ def test_incremental_logits_encode_mixes_with_pmf_steps():
 
 
 @pytest.mark.parametrize("dtype,V", [("bf16", 32000), ("f32", 32000), ("bf16", 128256), ("f32", 65536),
-                                     ("bf16", 128512), ("bf16", 128520)])
+                                     ("bf16", 128512), ("bf16", 128520), ("f32", 65540), ("f32", 128256),
+                                     ("f32", 128512), ("f32", 128520), ("bf16", 131080)])
 def test_every_q1_shape_gives_the_same_bits(dtype, V):
     """Every forced row-stats shape (8/16-wave blocks, tiles, rolling prefetch,
     registers + LDS slots) yields the AUTO shape's bytes and decodes; shapes that
     cannot hold the row are refused with LAC_E_ARG.  V = 128256 bf16 and 65536
     f32 fill the register + LDS shape (15) exactly up to its 16384 vectors; bf16
-    128512 / 128520 sit on either side of its 16-copy form's 16064-vector limit."""
+    128512 / 128520 sit on either side of its 16-copy form's 16064-vector limit.
+    Rows past 16384 vectors (f32 65540 .. 128520, bf16 131080) take the paired
+    blocks (19), whose halves sit on either side of the same limit."""
     from lac_amd._lib import LacError
     B, steps, prec = 12, 3, 48
     x = _logits(777, steps, B, V, specials=True)
@@ -249,7 +252,7 @@ def test_every_q1_shape_gives_the_same_bits(dtype, V):
     c.encode_logits_job(dl, sym)
     want, wn = c.to_bytes()
     ran = 0
-    for sh in range(1, 19):
+    for sh in range(1, 20):
         c.set_q1_shape(sh)
         try:
             c.encode_logits_job(dl, sym)
@@ -262,3 +265,33 @@ def test_every_q1_shape_gives_the_same_bits(dtype, V):
         ran += 1
     assert ran >= (6 if V == 32000 else 3)
     c.close()
+
+
+@pytest.mark.parametrize("dtype,V,B,steps", [("f32", 65540, 300, 70), ("f32", 128256, 520, 3)])
+def test_paired_row_stats_many_rows(dtype, V, B, steps):
+    """Rows split over a pair of blocks (shape 19) with many rows per pair and, at
+    70 steps, two launches per job (the per-row arrival counts rearm, the maximum
+    words are cleared): logits path bytes == quantise + pmf path, decode round trip,
+    and == the tiled shape's bytes."""
+    g = torch.Generator(device=DEV).manual_seed(V + B)
+    dl = torch.randn((steps, B, V), device=DEV, generator=g) * 3
+    if dtype == "bf16":
+        dl = dl.to(torch.bfloat16)
+    prec = 48
+    c = _coder(V, B, prec, cap=steps * (prec + 2) + 256)
+    sym = torch.randint(0, V, (steps, B), device=DEV, generator=g, dtype=torch.int32)
+    c.encode_logits_job(dl, sym)
+    a, na = c.to_bytes()
+    c.set_q1_shape(14)
+    c.encode_logits_job(dl, sym)
+    assert c.to_bytes()[0] == a
+    c.set_q1_shape(0)
+    pmf = c.quantize_logits(dl)
+    c2 = _coder(V, B, prec, cap=steps * (prec + 2) + 256)
+    c2.encode_job(pmf, sym)
+    b, nb = c2.to_bytes()
+    assert (na == nb).all() and a == b
+    del pmf, c2
+    c.decode_open()
+    assert torch.equal(c.decode_logits(dl), sym)
+    c.raise_on_error()
