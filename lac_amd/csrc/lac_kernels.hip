@@ -2283,11 +2283,13 @@ __device__ inline uint64_t pair_ld(const uint64_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// post this half's row maximum (sequence number seq >= 1) and return the partner's;
+// post this half's 32-bit value (a row maximum; sequence number seq >= 1, one per
+// exchange: a block posts seq + 1 only after reading its partner's seq, so the
+// partner's word for seq is never overwritten unread) and return the partner's;
 // *ok = false when it never came
-__device__ inline float pair_exchange_max(uint64_t *xch, uint32_t seq, float m, bool *ok) {
+__device__ inline uint32_t pair_exchange(uint64_t *xch, uint32_t seq, uint32_t m, bool *ok) {
     const unsigned b = blockIdx.x, slot = seq & 1;
-    __hip_atomic_store(&xch[2 * b + slot], ((uint64_t)seq << 32) | __float_as_uint(m), __ATOMIC_RELAXED,
+    __hip_atomic_store(&xch[2 * b + slot], ((uint64_t)seq << 32) | m, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t *px = &xch[2 * (b ^ 8u) + slot];
     uint64_t v = pair_ld(px);
@@ -2296,7 +2298,12 @@ __device__ inline float pair_exchange_max(uint64_t *xch, uint32_t seq, float m, 
         v = pair_ld(px);
     }
     *ok = (uint32_t)(v >> 32) == seq;
-    return __uint_as_float((uint32_t)v);
+    return (uint32_t)v;
+}
+
+// fmaxf of two halves' maxima (as bits): = fmaxf over the whole row
+__device__ inline uint32_t f32_max_bits(uint32_t a, uint32_t b) {
+    return __float_as_uint(fmaxf(__uint_as_float(a), __uint_as_float(b)));
 }
 
 __device__ inline void pair_add(uint64_t *p, uint64_t v) {
@@ -2313,7 +2320,7 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
                                                          uint64_t *__restrict__ xch, int split) {
     constexpr int N = LogitN<LT>::N, R = 8, L = 8, NW = 16, NRB = 1024 / NT, NWR = NT / 64;
     constexpr int SL = (L - 1) * NT + LASTN;                   // slot vectors per row
-    constexpr bool IMAX = LAC_Q1_IMAX && sizeof(LT) == 2 && !PAIR;
+    constexpr bool IMAX = LAC_Q1_IMAX && sizeof(LT) == 2;
     static_assert((R + L) * N <= 128, "lane sums must fit 32 bits");
     static_assert(!PAIR || NT == 1024, "pairs: one row half per block");
     // (not the bf16 8-copy decode forms, which sit at the 128-VGPR cap: two more live
@@ -2347,9 +2354,22 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
     auto row_of = [&](int64_t r) {
         return lg + (t0 + r / B) * step_stride + (r % B) * stream_stride + (int64_t)vofs * N;
     };
-    __shared__ float sxm;
+    __shared__ uint32_t sxv;
     __shared__ int sxok;
-    uint32_t seq = 0;                                           // PAIR: rows done + 1
+    uint32_t seq = 0;                                           // PAIR: exchanges done
+    bool pok = true;                                            // PAIR: every exchange of this row came
+    // PAIR: this half's value for the row, combined with the partner's (block-wide)
+    auto pair_combine = [&](uint32_t v, auto op) {
+        seq++;
+        if (tid == 0) {
+            bool ok;
+            sxv = op(v, pair_exchange(xch, seq, v, &ok));
+            sxok = ok;
+        }
+        __syncthreads();
+        pok = pok && sxok != 0;
+        return sxv;
+    };
     int64_t pend_r = -1;                                        // DEC, LAC_Q1_DEFER: a row's chunk totals
     uint64_t pend = 0;                                          //   (lane ln: chunk ln) not yet stored
     auto flush_chunks = [&]() {
@@ -2410,6 +2430,7 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
             return (k == L - 1 && noslot) ? neg_inf16(sizeof(LT)) : slots[g * SL + k * NT + gti()];
         };
         float m;
+        pok = true;
         if constexpr (IMAX) {
             s16x2 pm = {(short)-32768, (short)-32768};
             auto pmax = [&](const u32x4 &v) {
@@ -2439,6 +2460,12 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
                 all_ok = all_ok && bm >= 0 && bm <= 0x7F80;
                 bi = gg == g ? bm : bi;
             }
+            if constexpr (PAIR) {                              // one row: the int max of both halves
+                bi = (int)pair_combine((uint32_t)bi, [](uint32_t a, uint32_t b) {
+                    return (int)a > (int)b ? a : b;
+                });
+                all_ok = bi >= 0 && bi <= 0x7F80;              // (both halves: the same branch)
+            }
             if (all_ok) {                                      // (see k_q1_stats)
                 m = __uint_as_float((uint32_t)bi << 16);
             } else {
@@ -2459,6 +2486,7 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
                 m = smax[g * NWR];
 #pragma unroll
                 for (int i = 1; i < NWR; i++) m = fmaxf(m, smax[g * NWR + i]);
+                if constexpr (PAIR) m = __uint_as_float(pair_combine(__float_as_uint(m), f32_max_bits));
             }
         } else {
             float mx = -INFINITY;
@@ -2479,18 +2507,7 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
             m = smax[g * NWR];
 #pragma unroll
             for (int i = 1; i < NWR; i++) m = fmaxf(m, smax[g * NWR + i]);
-        }
-        bool pok = true;
-        if constexpr (PAIR) {                                  // the row maximum of both halves
-            seq++;
-            if (tid == 0) {
-                bool ok;
-                sxm = pair_exchange_max(xch, seq, m, &ok);
-                sxok = ok;
-            }
-            __syncthreads();
-            m = fmaxf(m, sxm);                                 // = fmaxf over the whole row
-            pok = sxok != 0;
+            if constexpr (PAIR) m = __uint_as_float(pair_combine(__float_as_uint(m), f32_max_bits));
         }
         if (DEC && valid && gti() == 0 && hh == 0) mrow[r] = m;   // now: m is not held over pass 2
         if constexpr (DEC) flush_chunks();                    // the previous row's (LAC_Q1_DEFER)
@@ -2632,7 +2649,10 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
 // k_q1_decode: one wave per stream, sequential over a chunk of steps, from the
 // chunk totals of k_q1_stats: per step it finds the chunk holding
 // floor((x-l)*T/w), re-quantises only that chunk's logits and scans them to the
-// symbol, then renormalises as A_from_bin does (decode_advance).
+// symbol, then renormalises as A_from_bin does (decode_advance).  (Loading all of
+// a chunk's groups at once instead of one per search round measured no faster at
+// c4, 4 / 8 groups per chunk: with 16 stream-waves per CU the step is bound by
+// their VALU issue, not by the re-read's latency -- profiles/r02/q1_pair_bf16/.)
 template <typename LT>
 __global__ LAC_DEC_BOUNDS void k_q1_decode(const LT *__restrict__ lg, int64_t step_stride, int64_t stream_stride,
                                            int64_t t0, int64_t nsteps, int64_t V, int prec, uint32_t xsh,
@@ -2667,8 +2687,8 @@ __global__ LAC_DEC_BOUNDS void k_q1_decode(const LT *__restrict__ lg, int64_t st
         const LT *row = lg + t * step_stride + b * stream_stride;
         const BitWin win = bit_window(mybits, mynbits, st.pos);    // in flight during the search
         const float c = q1_c(mcur);
-        const uint64_t T = wave_sum_u64(mine);
         const uint64_t incl = wave_incl_scan_u64(mine);
+        const uint64_t T = readlane_u64(incl, 63);
         int err = 0;
         int64_t s = -1;
         const int64_t l = st.l, h = st.h, x = st.x;
@@ -3252,7 +3272,9 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
         // 220 -> 210 us per step of 4096 rows vs shape 9, profiles/r02/q1_rl_dec/)
         if (sh == 0 && nvec <= 16384) sh = 15;
         // longer rows that two blocks' registers + slots hold: one half per block (shape 19)
-        if (sh == 0 && sizeof(LT) == 4 && q1_pair_holds(c, nvec)) sh = 19;   // (bf16 pairs spill)
+        // (bf16: V = 256000 encode 4.36 -> 2.68 ms, 48 -> 78 % of peak; 262144, whose
+        // 16384-vector halves need the 8-copy form, 48 -> 59 %; profiles/r02/q1_pair_bf16/)
+        if (sh == 0 && q1_pair_holds(c, nvec)) sh = 19;
         // measured at V = 128256 f32: encode tiles of (16,8) with the tile-rolling
         // prefetch 1.98 ms vs 2.18 for tiles of (8,8) (shape 13, its (8,8) form: 2.20)
         if (sh == 0) sh = nvec <= 64 * 16 * 16 ? 9 : (DEC ? 10 : (sizeof(LT) == 4 ? 14 : 8));

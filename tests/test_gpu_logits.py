@@ -79,7 +79,8 @@ CASES = [
     (1000, 40, 30, 40, "f32"),
     (1000, 40, 30, 40, "bf16"),
     (128256, 8, 4, 48, "bf16"),            # 16-wave single-pass row stats
-    (128256, 4, 3, 48, "f32"),             # tiled row stats (encode 8-wave, decode 16-wave tiles)
+    (128256, 4, 5, 48, "f32"),             # rows split over a pair of blocks (shape 19)
+    (131080, 6, 5, 48, "bf16"),            # bf16 pairs: the int16 max exchanged, float fallback rows
     (65536, 6, 3, 48, "bf16"),             # (8,16) shape
     (24, 5, 50, 24, "f32"),
     (4096, 2048, 3, 48, "bf16"),
@@ -267,7 +268,8 @@ def test_every_q1_shape_gives_the_same_bits(dtype, V):
     c.close()
 
 
-@pytest.mark.parametrize("dtype,V,B,steps", [("f32", 65540, 300, 70), ("f32", 128256, 520, 3)])
+@pytest.mark.parametrize("dtype,V,B,steps", [("f32", 65540, 300, 70), ("f32", 128256, 520, 3),
+                                             ("bf16", 256000, 300, 3), ("bf16", 262144, 64, 3)])
 def test_paired_row_stats_many_rows(dtype, V, B, steps):
     """Rows split over a pair of blocks (shape 19) with many rows per pair and, at
     70 steps, two launches per job (the per-row arrival counts rearm, the maximum
