@@ -2720,7 +2720,11 @@ __global__ LAC_DEC_BOUNDS void k_q1_decode(const LT *__restrict__ lg, int64_t st
                     uint64_t loc[N], ls = 0;
 #pragma unroll
                     for (int j = 0; j < N; j++) {
-                        ls += valid ? q1_val(logit_at<LT>(xv, j), c, tab) : 0u;
+                        // looked up unconditionally (xv is a clamped in-row vector), masked
+                        // after: a conditional lookup compiled to one exec-masked branch
+                        // with its own LDS wait per entry
+                        const uint32_t q = q1_val(logit_at<LT>(xv, j), c, tab);
+                        ls += valid ? q : 0u;
                         loc[j] = ls;
                     }
                     const uint64_t in = wave_incl_scan_u64(ls);
