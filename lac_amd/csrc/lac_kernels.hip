@@ -64,9 +64,9 @@ using namespace lac;
 #define LAC_DECF_MINW 2
 #endif
 #if LAC_ENC_MINW > 0
-#define LAC_ENC_BOUNDS __launch_bounds__(256, LAC_ENC_MINW)
+#define LAC_ENC_BOUNDS __launch_bounds__(64 * LAC_STREAM_WG, LAC_ENC_MINW)
 #else
-#define LAC_ENC_BOUNDS __launch_bounds__(256)
+#define LAC_ENC_BOUNDS __launch_bounds__(64 * LAC_STREAM_WG)
 #endif
 #if LAC_DEC_MINW > 0
 #define LAC_DEC_BOUNDS __launch_bounds__(256, LAC_DEC_MINW)
@@ -78,6 +78,14 @@ namespace {
 
 constexpr int kChunkSteps = 64;       // split path: steps per row-stats launch at >= 512 streams
 constexpr int kWavesPerBlock = 4;     // 256-thread workgroups
+// one-wave-per-stream kernels (k_encode_fused, k_decode_wave(_fine)): waves per workgroup.
+// 1 or 2 (a finished wave's slot refilled without waiting for its workgroup's
+// slowest wave) measured no faster: c3 / c4 / u64 encode and decode within noise,
+// u64 decode 13 % slower at 2 (profiles/r02/stream_wg_rejected/)
+#ifndef LAC_STREAM_WG
+#define LAC_STREAM_WG 4
+#endif
+constexpr int kStreamWaves = LAC_STREAM_WG;
 
 // ------------------------------------------------------------------ wave helpers
 __device__ inline uint32_t lane_id() { return __lane_id(); }
@@ -684,7 +692,7 @@ __global__ LAC_ENC_BOUNDS void k_encode_fused(const E *__restrict__ pmf, int64_t
                                                       uint64_t cap_words, uint64_t *trace, uint64_t *nbits, int flags,
                                                       int mapping, int term) {
     const int lane = (int)lane_id();
-    const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    const int64_t b = (int64_t)blockIdx.x * kStreamWaves + (threadIdx.x >> 6);
     if (b >= B) return;
     EncState st = (flags & kReset) ? fresh_state(prec) : states[b];
     uint64_t *pa = planeA + (uint64_t)b * cap_words, *pc = planeC + (uint64_t)b * cap_words;
@@ -1113,7 +1121,7 @@ __global__ LAC_DEC_BOUNDS void k_decode_wave(const E *__restrict__ pmf, int64_t 
                                                      const uint64_t *nbits, int32_t *sym_out, int64_t B,
                                                      int mapping) {
     const int lane = (int)lane_id();
-    const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + wave_in_block();
+    const int64_t b = (int64_t)blockIdx.x * kStreamWaves + wave_in_block();
     if (b >= B) return;
     DecState st = states[b];
     const uint8_t *mybits = bits + b * stride;
@@ -1309,13 +1317,13 @@ __device__ inline uint64_t wave_sum8_u64(const uint64_t (&s)[8], uint32_t &ovf) 
 // load per lane (1 KB, 0.8 % of a 32000-entry u32 row) instead of a chunk of
 // eight (6.3 %), which also shortens the dependent tail of every step.
 template <typename E, int VEC, int NR>
-__global__ __launch_bounds__(256, LAC_DECF_MINW) void k_decode_wave_fine(const E *__restrict__ pmf, int64_t step_stride,
+__global__ __launch_bounds__(64 * LAC_STREAM_WG, LAC_DECF_MINW) void k_decode_wave_fine(const E *__restrict__ pmf, int64_t step_stride,
                                                   int64_t stream_stride, int64_t nsteps, int64_t V, int prec,
                                                   DecState *states, const uint8_t *bits, uint64_t stride,
                                                   const uint64_t *nbits, int32_t *sym_out, int64_t B, int mapping) {
     constexpr bool W = sizeof(E) == 8;
     const int lane = (int)lane_id();
-    const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + wave_in_block();
+    const int64_t b = (int64_t)blockIdx.x * kStreamWaves + wave_in_block();
     if (b >= B) return;
     DecState st = states[b];
     const uint8_t *mybits = bits + b * stride;
@@ -2910,7 +2918,7 @@ static int encode_impl(lac_ctx *c, const E *pmf, int64_t step_stride, int64_t st
     const bool fused = c->path == LAC_PATH_FUSED || (c->path == LAC_PATH_AUTO && c->B >= c->fused_min_streams);
     if (fused) {
         ProfScope ps(c, KID_FUSED, st);
-        k_encode_fused<E, VEC><<<blocks, 64 * kWavesPerBlock, 0, st>>>(
+        k_encode_fused<E, VEC><<<(unsigned)((c->B + kStreamWaves - 1) / kStreamWaves), 64 * kStreamWaves, 0, st>>>(
             pmf, step_stride, stream_stride, sym, c->B, 0, steps, c->V, c->prec, c->enc, c->planeA, c->planeC,
             c->cap_words, trace, c->nbits, flags, c->mapping, c->term);
         CHECK_LAUNCH();
@@ -2993,10 +3001,10 @@ template <typename E, int VEC>
 static int decode_wave_launch(lac_ctx *c, const E *pmf, int64_t step_stride, int64_t stream_stride, int64_t steps,
                               int32_t *out, hipStream_t st) {
     ProfScope ps(c, KID_DECODE_WAVE, st);
-    const unsigned blocks = (unsigned)((c->B + kWavesPerBlock - 1) / kWavesPerBlock);
+    const unsigned blocks = (unsigned)((c->B + kStreamWaves - 1) / kStreamWaves);
     const int64_t nit = (c->V / VEC + 63) / 64;               // 64-vector iterations per row
 #define LAC_FINE(NR)                                                                                              \
-    k_decode_wave_fine<E, VEC, NR><<<blocks, 64 * kWavesPerBlock, 0, st>>>(                                      \
+    k_decode_wave_fine<E, VEC, NR><<<blocks, 64 * kStreamWaves, 0, st>>>(                                        \
         pmf, step_stride, stream_stride, steps, c->V, c->prec, c->dec, c->dbits, c->dstride, c->dnbits, out, c->B, \
         c->mapping)
     bool fine = false;
@@ -3007,7 +3015,7 @@ static int decode_wave_launch(lac_ctx *c, const E *pmf, int64_t step_stride, int
         else if (fine) LAC_FINE(8);
     }
     if (!fine)
-        k_decode_wave<E, VEC><<<blocks, 64 * kWavesPerBlock, 0, st>>>(
+        k_decode_wave<E, VEC><<<blocks, 64 * kStreamWaves, 0, st>>>(
             pmf, step_stride, stream_stride, steps, c->V, c->prec, c->dec, c->dbits, c->dstride, c->dnbits, out, c->B,
             c->mapping);
 #undef LAC_FINE
