@@ -2277,7 +2277,7 @@ typedef __attribute__((address_space(3))) void lvoid_t;
 // CU: both halves are resident), and the wait is bounded: a partner that never
 // posts poisons the row's total (+2^62: LAC_E_TABLE at the coder) instead of
 // hanging the GPU.
-constexpr uint32_t kPairSpinMax = 1u << 24;                 // ~1 s of s_sleep 2
+constexpr uint32_t kPairSpinMax = 1u << 21;                 // polls: a few seconds (s_sleep 2 + a device-scope load each)
 
 // DEC: a row's 64 chunk totals are stored after the NEXT row's maximum, not at the
 // row's end, where the store's completion sat in front of the next row's vmcnt(0)
