@@ -2264,19 +2264,20 @@ typedef __attribute__((address_space(3))) void lvoid_t;
 // IMAX fallback (float max, with its own barrier) is taken by the whole block if
 // any of its rows needs it.
 //
-// PAIR: rows of up to 2 x 16064 vectors (f32 V <= 128512: Llama-3's 128256 in f32,
-// which no CU's registers + LDS hold) split over a pair of blocks, each holding one
-// half exactly as above.  The halves meet twice per row: the row maximum (each
-// block posts its half's maximum with the row's sequence number into one of two
-// alternating words and waits for its partner's: the only wait), and the sums
-// (each half adds its partials -- total, lo, hi, or its 64 chunk partials -- into
-// the row's zeroed outputs with relaxed device-scope atomics: no wait, and no
+// KG > 1 ("pairs", groups): rows longer than one CU's registers + LDS hold (f32 V =
+// 128256: Llama-3's vocab in f32; bf16 / f32 V = 151936 (Qwen2), 256000 (Gemma))
+// split over a group of KG = 2..4 blocks, each holding one segment of <= 16384
+// vectors exactly as above.  The segments meet twice per row: the row maximum
+// (each block posts its segment's maximum with the row's sequence number into one
+// of two alternating words and polls its partners': the only wait), and the sums
+// (each segment adds its partials -- total, lo, hi, or its 64 chunk partials --
+// into the row's zeroed outputs with relaxed device-scope atomics: no wait, and no
 // fence -- a release/acquire fence here writes back / invalidates the whole L2 and
-// cost ~35 us per row).  A pair shares an XCD (blocks b and b ^ 8; dispatch is
-// round-robin over the 8 XCDs), the grid never exceeds the CU count (one block per
-// CU: both halves are resident), and the wait is bounded: a partner that never
-// posts poisons the row's total (+2^62: LAC_E_TABLE at the coder) instead of
-// hanging the GPU.
+// cost ~35 us per row).  A group shares an XCD (blocks slot * 8 + xcd of KG
+// consecutive slots; dispatch is round-robin over the 8 XCDs), the grid never
+// exceeds the CU count (one block per CU: every member is resident), and the wait
+// is bounded: a partner that never posts poisons the row's total (+2^62:
+// LAC_E_TABLE at the coder) instead of hanging the GPU.
 constexpr uint32_t kPairSpinMax = 1u << 21;                 // polls: a few seconds (s_sleep 2 + a device-scope load each)
 
 // DEC: a row's 64 chunk totals are stored after the NEXT row's maximum, not at the
@@ -2291,22 +2292,31 @@ __device__ inline uint64_t pair_ld(const uint64_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// post this half's 32-bit value (a row maximum; sequence number seq >= 1, one per
-// exchange: a block posts seq + 1 only after reading its partner's seq, so the
-// partner's word for seq is never overwritten unread) and return the partner's;
-// *ok = false when it never came
-__device__ inline uint32_t pair_exchange(uint64_t *xch, uint32_t seq, uint32_t m, bool *ok) {
-    const unsigned b = blockIdx.x, slot = seq & 1;
-    __hip_atomic_store(&xch[2 * b + slot], ((uint64_t)seq << 32) | m, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t *px = &xch[2 * (b ^ 8u) + slot];
-    uint64_t v = pair_ld(px);
-    for (uint32_t n = 0; (uint32_t)(v >> 32) != seq && n < kPairSpinMax; n++) {
-        __builtin_amdgcn_s_sleep(2);
-        v = pair_ld(px);
+// post this block's 32-bit value (a row maximum; sequence number seq >= 1, one per
+// exchange: a block posts seq + 1 only after reading all its partners' seq, so no
+// partner's word for seq is overwritten unread) and fold in the K - 1 partners'
+// (blocks ((slot / K) * K + k) * 8 + xcd) with op; *ok = false when one never came
+template <int K, typename Op>
+__device__ inline uint32_t group_exchange(uint64_t *xch, uint32_t seq, uint32_t m, Op op, bool *ok) {
+    const unsigned b = blockIdx.x, sl = seq & 1, xcd = b & 7, g0 = ((b >> 3) / K) * K;
+    __hip_atomic_store(&xch[2 * b + sl], ((uint64_t)seq << 32) | m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t acc = m;
+    bool all = true;
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const unsigned pb = (g0 + k) * 8 + xcd;
+        if (pb == b) continue;
+        const uint64_t *px = &xch[2 * pb + sl];
+        uint64_t v = pair_ld(px);
+        for (uint32_t n = 0; (uint32_t)(v >> 32) != seq && n < kPairSpinMax; n++) {
+            __builtin_amdgcn_s_sleep(2);
+            v = pair_ld(px);
+        }
+        all = all && (uint32_t)(v >> 32) == seq;
+        acc = op(acc, (uint32_t)v);
     }
-    *ok = (uint32_t)(v >> 32) == seq;
-    return (uint32_t)v;
+    *ok = all;
+    return acc;
 }
 
 // fmaxf of two halves' maxima (as bits): = fmaxf over the whole row
@@ -2319,7 +2329,7 @@ __device__ inline void pair_add(uint64_t *p, uint64_t v) {
 }
 constexpr uint64_t kPairPoison = 1ull << 62;                 // a failed exchange: the row's total is >= 2^62
 
-template <typename LT, bool DEC, int REP = kRLRep, int LASTN = 1024, int NT = 1024, bool PAIR = false>
+template <typename LT, bool DEC, int REP = kRLRep, int LASTN = 1024, int NT = 1024, int KG = 1>
 __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ lg, int64_t step_stride,
                                                          int64_t stream_stride, const int32_t *__restrict__ sym,
                                                          int64_t B, int64_t rows, int64_t V, int64_t t0, uint32_t xsh,
@@ -2330,7 +2340,8 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
     constexpr int SL = (L - 1) * NT + LASTN;                   // slot vectors per row
     constexpr bool IMAX = LAC_Q1_IMAX && sizeof(LT) == 2;
     static_assert((R + L) * N <= 128, "lane sums must fit 32 bits");
-    static_assert(!PAIR || NT == 1024, "pairs: one row half per block");
+    constexpr bool PAIR = KG > 1;                              // a row over a group of KG blocks
+    static_assert(!PAIR || NT == 1024, "groups: one row segment per block");
     // (not the bf16 8-copy decode forms, which sit at the 128-VGPR cap: two more live
     // registers there add spills)
     constexpr bool DEFER = LAC_Q1_DEFER && !(sizeof(LT) == 2 && REP == kRLRep);
@@ -2351,14 +2362,16 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
     // kernel at its 128-VGPR cap: 2.52 -> 2.70 ms at bf16 V = 128256)
     q1_load_tab_rep<REP>(tabr, xsh);
     const uint32_t loff = (uint32_t)(lane & (REP - 1)) << 2;
-    // PAIR: block b holds half hh = (b >> 3) & 1 of the rows of pair (b >> 4) * 8 + (b & 7)
-    const int hh = PAIR ? (int)((blockIdx.x >> 3) & 1) : 0;
-    const int64_t bix = PAIR ? (int64_t)((blockIdx.x >> 4) * 8 + (blockIdx.x & 7)) : (int64_t)blockIdx.x;
-    const int vofs = hh * split;                                // vectors of the row before this half
-    const int nvec = (int)(V / N) - (PAIR ? (hh ? split : (int)(V / N) - split) : 0);
+    // PAIR: block b = slot * 8 + xcd holds segment hh = slot % KG of the rows of group
+    // (slot / KG) * 8 + xcd; segments are split vectors long, the last one the rest
+    const int slotb = (int)(blockIdx.x >> 3);
+    const int hh = PAIR ? slotb % KG : 0;
+    const int64_t bix = PAIR ? (int64_t)((slotb / KG) * 8 + (blockIdx.x & 7)) : (int64_t)blockIdx.x;
+    const int vofs = hh * split;                                // vectors of the row before this segment
+    const int nvec = PAIR ? (hh < KG - 1 ? split : (int)(V / N) - (KG - 1) * split) : (int)(V / N);
     // TRIM: waves past LASTN have no last slot (their vectors there lie beyond the row)
     const bool noslot = TRIM && wg * 64 >= LASTN;
-    const int64_t stride = (int64_t)(PAIR ? gridDim.x / 2 : gridDim.x) * NRB;
+    const int64_t stride = (int64_t)(gridDim.x / KG) * NRB;
     auto row_of = [&](int64_t r) {
         return lg + (t0 + r / B) * step_stride + (r % B) * stream_stride + (int64_t)vofs * N;
     };
@@ -2371,7 +2384,7 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
         seq++;
         if (tid == 0) {
             bool ok;
-            sxv = op(v, pair_exchange(xch, seq, v, &ok));
+            sxv = group_exchange<KG>(xch, seq, v, op, &ok);
             sxok = ok;
         }
         __syncthreads();
@@ -2494,7 +2507,7 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
                 m = smax[g * NWR];
 #pragma unroll
                 for (int i = 1; i < NWR; i++) m = fmaxf(m, smax[g * NWR + i]);
-                if constexpr (PAIR) m = __uint_as_float(pair_combine(__float_as_uint(m), f32_max_bits));
+                if constexpr (PAIR) m = __uint_as_float(pair_combine(__float_as_uint(m), [](uint32_t a, uint32_t b) { return f32_max_bits(a, b); }));
             }
         } else {
             float mx = -INFINITY;
@@ -2515,7 +2528,7 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
             m = smax[g * NWR];
 #pragma unroll
             for (int i = 1; i < NWR; i++) m = fmaxf(m, smax[g * NWR + i]);
-            if constexpr (PAIR) m = __uint_as_float(pair_combine(__float_as_uint(m), f32_max_bits));
+            if constexpr (PAIR) m = __uint_as_float(pair_combine(__float_as_uint(m), [](uint32_t a, uint32_t b) { return f32_max_bits(a, b); }));
         }
         if (DEC && valid && gti() == 0 && hh == 0) mrow[r] = m;   // now: m is not held over pass 2
         if constexpr (DEC) flush_chunks();                    // the previous row's (LAC_Q1_DEFER)
@@ -3187,38 +3200,63 @@ static int q1_rl_kernel(lac_ctx *c, const Q1Args &a, hipStream_t st) {
     return LAC_OK;
 }
 
-// Paired row stats (shape 19): the first half of a row holds 64 * floor(groups / 2)
-// vectors, the second the rest; both halves must fit one block's registers + slots.
-static int q1_pair_split(int64_t nvec) { return (int)(64 * (((nvec + 63) / 64) / 2)); }
-static bool q1_pair_holds(lac_ctx *c, int64_t nvec) {
-    return c->cus >= 16 && nvec > 16384 && nvec - q1_pair_split(nvec) <= 16384;
+// Grouped row stats (shape 19): a row over K = 2..4 blocks, segments of `split`
+// vectors (a multiple of 64), the last one the rest; every segment must fit one
+// block's registers + slots -- the 16-copy form (<= 16064 vectors) with the fewest
+// blocks if any K allows it, else the 8-copy form (<= 16384).
+struct Q1Group {
+    int k = 0, split = 0;
+    bool rep16 = false;
+};
+static bool q1_group(lac_ctx *c, int64_t nvec, Q1Group *g) {
+    if (nvec <= 16384) return false;
+    const int64_t ngrp = (nvec + 63) / 64;
+    for (int pass = 0; pass < 2; pass++) {
+        const int64_t lim = pass ? 16384 : kRLTrimMaxVec;
+        for (int k = 2; k <= 4 && 8 * k <= c->cus; k++) {
+            const int64_t sp = 64 * ((ngrp + k - 1) / k), last = nvec - (k - 1) * sp;
+            if (last > 0 && sp <= lim && last <= lim) {
+                g->k = k;
+                g->split = (int)sp;
+                g->rep16 = pass == 0;
+                return true;
+            }
+        }
+    }
+    return false;
 }
 
-template <typename LT, bool DEC, int REP, int LASTN>
-static int q1_pair_kernel(lac_ctx *c, const Q1Args &a, hipStream_t st) {
+template <typename LT, bool DEC, int REP, int LASTN, int K>
+static int q1_group_kernel(lac_ctx *c, const Q1Args &a, hipStream_t st, int split) {
     const int64_t nvec = c->V / LogitN<LT>::N;
     if (!c->pxch) HIPCHK(hipMalloc(&c->pxch, sizeof(uint64_t) * 2 * c->cus));
-    // pairs (b, b ^ 8) in groups of 16 blocks; never more blocks than CUs (one per CU:
-    // both halves of every pair resident at once)
-    const int64_t need = 16 * ((a.rows + 7) / 8), cap = (int64_t)(c->cus / 16) * 16;
+    // groups of K blocks in runs of 8 K (one per XCD each); never more blocks than CUs
+    // (one per CU: every member of every group resident at once)
+    const int64_t need = 8 * K * ((a.rows + 7) / 8), cap = (int64_t)(c->cus / (8 * K)) * (8 * K);
     const unsigned grid = (unsigned)(need < cap ? need : cap);
     HIPCHK(hipMemsetAsync(c->pxch, 0, sizeof(uint64_t) * 2 * grid, st));   // no stale sequence numbers
     // the halves add into zeroed outputs
     if (DEC) HIPCHK(hipMemsetAsync(c->q1chunks, 0, sizeof(uint64_t) * 64 * a.rows, st));
     else HIPCHK(hipMemsetAsync(c->stats, 0, sizeof(RowStats) * a.rows, st));
     ProfScope ps(c, KID_Q1_STATS, st);
-    k_q1_stats_rl<LT, DEC, REP, LASTN, 1024, true><<<grid, 1024, 0, st>>>(
+    k_q1_stats_rl<LT, DEC, REP, LASTN, 1024, K><<<grid, 1024, 0, st>>>(
         (const LT *)a.lg, a.ss, a.bs, a.sym, c->B, a.rows, c->V, a.t0, a.xsh, q1_groups_per_chunk(nvec), c->stats,
-        c->q1chunks, c->q1m, c->pxch, q1_pair_split(nvec));
+        c->q1chunks, c->q1m, c->pxch, split);
     CHECK_LAUNCH();
     return LAC_OK;
 }
 
+template <typename LT, bool DEC, int REP, int LASTN>
+static int q1_group_k(lac_ctx *c, const Q1Args &a, hipStream_t st, const Q1Group &g) {
+    if (g.k == 2) return q1_group_kernel<LT, DEC, REP, LASTN, 2>(c, a, st, g.split);
+    if (g.k == 3) return q1_group_kernel<LT, DEC, REP, LASTN, 3>(c, a, st, g.split);
+    return q1_group_kernel<LT, DEC, REP, LASTN, 4>(c, a, st, g.split);
+}
+
 template <typename LT, bool DEC>
-static int q1_stats_pair_launch(lac_ctx *c, const Q1Args &a, hipStream_t st) {
-    const int64_t nvec = c->V / LogitN<LT>::N, sp = q1_pair_split(nvec);
-    if (sp <= kRLTrimMaxVec && nvec - sp <= kRLTrimMaxVec) return q1_pair_kernel<LT, DEC, 16, kRLLastTrim>(c, a, st);
-    return q1_pair_kernel<LT, DEC, kRLRep, 1024>(c, a, st);
+static int q1_stats_group_launch(lac_ctx *c, const Q1Args &a, hipStream_t st, const Q1Group &g) {
+    if (g.rep16) return q1_group_k<LT, DEC, 16, kRLLastTrim>(c, a, st, g);
+    return q1_group_k<LT, DEC, kRLRep, 1024>(c, a, st, g);
 }
 
 // The register + LDS-slot shapes (k_q1_stats_rl), by rows per block:
@@ -3284,9 +3322,9 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
         // 220 -> 210 us per step of 4096 rows vs shape 9, profiles/r02/q1_rl_dec/)
         if (sh == 0 && nvec <= 16384) sh = 15;
         // longer rows that two blocks' registers + slots hold: one half per block (shape 19)
-        // (bf16: V = 256000 encode 4.36 -> 2.68 ms, 48 -> 78 % of peak; 262144, whose
-        // 16384-vector halves need the 8-copy form, 48 -> 59 %; profiles/r02/q1_pair_bf16/)
-        if (sh == 0 && q1_pair_holds(c, nvec)) sh = 19;
+        // (bf16: V = 256000 encode 4.36 -> 2.68 ms, 48 -> 78 % of peak; profiles/r02/q1_pair_bf16/)
+        Q1Group g0;
+        if (sh == 0 && q1_group(c, nvec, &g0)) sh = 19;
         // measured at V = 128256 f32: encode tiles of (16,8) with the tile-rolling
         // prefetch 1.98 ms vs 2.18 for tiles of (8,8) (shape 13, its (8,8) form: 2.20)
         if (sh == 0) sh = nvec <= 64 * 16 * 16 ? 9 : (DEC ? 10 : (sizeof(LT) == 4 ? 14 : 8));
@@ -3302,7 +3340,8 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
     if ((sh == 15 || sh == 16) && nvec <= 16384) return q1_stats_rl_launch<LT, DEC>(c, a, st, sh);
     if (sh == 17 && nvec <= 4096) return q1_stats_rl_launch<LT, DEC>(c, a, st, 17);
     if (sh == 18 && nvec <= 8192) return q1_stats_rl_launch<LT, DEC>(c, a, st, 18);
-    if (sh == 19 && q1_pair_holds(c, nvec)) return q1_stats_pair_launch<LT, DEC>(c, a, st);
+    Q1Group grp;
+    if (sh == 19 && q1_group(c, nvec, &grp)) return q1_stats_group_launch<LT, DEC>(c, a, st, grp);
     if (sh == 13) return q1_stats_launch<LT, 8, 8, DEC, true, true>(c, a, st);         // tiles of (8,8,y)
     if (sh == 14) return q1_stats_launch<LT, 16, 8, DEC, true, true, 16>(c, a, st);    // tiles of (16,8,y)
     if (sh == 8) return q1_stats_launch<LT, 8, 8, DEC, true, false>(c, a, st);      // tiles of 4096 vectors

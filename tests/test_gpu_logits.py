@@ -234,15 +234,18 @@ def test_incremental_logits_encode_mixes_with_pmf_steps():
 
 @pytest.mark.parametrize("dtype,V", [("bf16", 32000), ("f32", 32000), ("bf16", 128256), ("f32", 65536),
                                      ("bf16", 128512), ("bf16", 128520), ("f32", 65540), ("f32", 128256),
-                                     ("f32", 128512), ("f32", 128520), ("bf16", 131080)])
+                                     ("f32", 128512), ("f32", 128520), ("bf16", 131080), ("bf16", 151936),
+                                     ("f32", 151936), ("bf16", 262144), ("f32", 256000), ("f32", 262144)])
 def test_every_q1_shape_gives_the_same_bits(dtype, V):
     """Every forced row-stats shape (8/16-wave blocks, tiles, rolling prefetch,
     registers + LDS slots) yields the AUTO shape's bytes and decodes; shapes that
     cannot hold the row are refused with LAC_E_ARG.  V = 128256 bf16 and 65536
     f32 fill the register + LDS shape (15) exactly up to its 16384 vectors; bf16
     128512 / 128520 sit on either side of its 16-copy form's 16064-vector limit.
-    Rows past 16384 vectors (f32 65540 .. 128520, bf16 131080) take the paired
-    blocks (19), whose halves sit on either side of the same limit."""
+    Rows past 16384 vectors take groups of 2..4 blocks (19): pairs at f32 65540 ..
+    128520 and bf16 131080 .. 151936 (halves on either side of the same limit),
+    three blocks at f32 151936 (Qwen2) and bf16 262144, four at f32 256000 and,
+    in the 8-copy form, f32 262144 (Gemma 3)."""
     from lac_amd._lib import LacError
     B, steps, prec = 12, 3, 48
     x = _logits(777, steps, B, V, specials=True)
@@ -269,9 +272,10 @@ def test_every_q1_shape_gives_the_same_bits(dtype, V):
 
 
 @pytest.mark.parametrize("dtype,V,B,steps", [("f32", 65540, 300, 70), ("f32", 128256, 520, 3),
-                                             ("bf16", 256000, 300, 3), ("bf16", 262144, 64, 3)])
+                                             ("bf16", 256000, 300, 3), ("bf16", 262144, 64, 3),
+                                             ("f32", 151936, 256, 3), ("f32", 262144, 128, 3)])
 def test_paired_row_stats_many_rows(dtype, V, B, steps):
-    """Rows split over a pair of blocks (shape 19) with many rows per pair and, at
+    """Rows split over a group of blocks (shape 19) with many rows per group and, at
     70 steps, two launches per job (the per-row arrival counts rearm, the maximum
     words are cleared): logits path bytes == quantise + pmf path, decode round trip,
     and == the tiled shape's bytes."""
