@@ -2278,7 +2278,7 @@ typedef __attribute__((address_space(3))) void lvoid_t;
 // exceeds the CU count (one block per CU: every member is resident), and the wait
 // is bounded: a partner that never posts poisons the row's total (+2^62:
 // LAC_E_TABLE at the coder) instead of hanging the GPU.
-constexpr uint32_t kPairSpinMax = 1u << 21;                 // polls: a few seconds (s_sleep 2 + a device-scope load each)
+constexpr uint32_t kGroupSpinMax = 1u << 21;                 // polls: a few seconds (s_sleep 2 + a device-scope load each)
 
 // DEC: a row's 64 chunk totals are stored after the NEXT row's maximum, not at the
 // row's end, where the store's completion sat in front of the next row's vmcnt(0)
@@ -2288,7 +2288,7 @@ constexpr uint32_t kPairSpinMax = 1u << 21;                 // polls: a few seco
 #define LAC_Q1_DEFER 1
 #endif
 
-__device__ inline uint64_t pair_ld(const uint64_t *p) {
+__device__ inline uint64_t group_ld(const uint64_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -2307,10 +2307,10 @@ __device__ inline uint32_t group_exchange(uint64_t *xch, uint32_t seq, uint32_t 
         const unsigned pb = (g0 + k) * 8 + xcd;
         if (pb == b) continue;
         const uint64_t *px = &xch[2 * pb + sl];
-        uint64_t v = pair_ld(px);
-        for (uint32_t n = 0; (uint32_t)(v >> 32) != seq && n < kPairSpinMax; n++) {
+        uint64_t v = group_ld(px);
+        for (uint32_t n = 0; (uint32_t)(v >> 32) != seq && n < kGroupSpinMax; n++) {
             __builtin_amdgcn_s_sleep(2);
-            v = pair_ld(px);
+            v = group_ld(px);
         }
         all = all && (uint32_t)(v >> 32) == seq;
         acc = op(acc, (uint32_t)v);
@@ -2319,15 +2319,15 @@ __device__ inline uint32_t group_exchange(uint64_t *xch, uint32_t seq, uint32_t 
     return acc;
 }
 
-// fmaxf of two halves' maxima (as bits): = fmaxf over the whole row
+// fmaxf of two segments' maxima (as bits): folded over all, = fmaxf over the whole row
 __device__ inline uint32_t f32_max_bits(uint32_t a, uint32_t b) {
     return __float_as_uint(fmaxf(__uint_as_float(a), __uint_as_float(b)));
 }
 
-__device__ inline void pair_add(uint64_t *p, uint64_t v) {
+__device__ inline void group_add(uint64_t *p, uint64_t v) {
     (void)__hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-constexpr uint64_t kPairPoison = 1ull << 62;                 // a failed exchange: the row's total is >= 2^62
+constexpr uint64_t kGroupPoison = 1ull << 62;                 // a failed exchange: the row's total is >= 2^62
 
 template <typename LT, bool DEC, int REP = kRLRep, int LASTN = 1024, int NT = 1024, int KG = 1>
 __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ lg, int64_t step_stride,
@@ -2340,8 +2340,8 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
     constexpr int SL = (L - 1) * NT + LASTN;                   // slot vectors per row
     constexpr bool IMAX = LAC_Q1_IMAX && sizeof(LT) == 2;
     static_assert((R + L) * N <= 128, "lane sums must fit 32 bits");
-    constexpr bool PAIR = KG > 1;                              // a row over a group of KG blocks
-    static_assert(!PAIR || NT == 1024, "groups: one row segment per block");
+    constexpr bool GROUP = KG > 1;                              // a row over a group of KG blocks
+    static_assert(!GROUP || NT == 1024, "groups: one row segment per block");
     // (not the bf16 8-copy decode forms, which sit at the 128-VGPR cap: two more live
     // registers there add spills)
     constexpr bool DEFER = LAC_Q1_DEFER && !(sizeof(LT) == 2 && REP == kRLRep);
@@ -2362,13 +2362,13 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
     // kernel at its 128-VGPR cap: 2.52 -> 2.70 ms at bf16 V = 128256)
     q1_load_tab_rep<REP>(tabr, xsh);
     const uint32_t loff = (uint32_t)(lane & (REP - 1)) << 2;
-    // PAIR: block b = slot * 8 + xcd holds segment hh = slot % KG of the rows of group
+    // GROUP: block b = slot * 8 + xcd holds segment hh = slot % KG of the rows of group
     // (slot / KG) * 8 + xcd; segments are split vectors long, the last one the rest
     const int slotb = (int)(blockIdx.x >> 3);
-    const int hh = PAIR ? slotb % KG : 0;
-    const int64_t bix = PAIR ? (int64_t)((slotb / KG) * 8 + (blockIdx.x & 7)) : (int64_t)blockIdx.x;
+    const int hh = GROUP ? slotb % KG : 0;
+    const int64_t bix = GROUP ? (int64_t)((slotb / KG) * 8 + (blockIdx.x & 7)) : (int64_t)blockIdx.x;
     const int vofs = hh * split;                                // vectors of the row before this segment
-    const int nvec = PAIR ? (hh < KG - 1 ? split : (int)(V / N) - (KG - 1) * split) : (int)(V / N);
+    const int nvec = GROUP ? (hh < KG - 1 ? split : (int)(V / N) - (KG - 1) * split) : (int)(V / N);
     // TRIM: waves past LASTN have no last slot (their vectors there lie beyond the row)
     const bool noslot = TRIM && wg * 64 >= LASTN;
     const int64_t stride = (int64_t)(gridDim.x / KG) * NRB;
@@ -2377,10 +2377,10 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
     };
     __shared__ uint32_t sxv;
     __shared__ int sxok;
-    uint32_t seq = 0;                                           // PAIR: exchanges done
-    bool pok = true;                                            // PAIR: every exchange of this row came
-    // PAIR: this half's value for the row, combined with the partner's (block-wide)
-    auto pair_combine = [&](uint32_t v, auto op) {
+    uint32_t seq = 0;                                           // GROUP: exchanges done
+    bool pok = true;                                            // GROUP: every exchange of this row came
+    // GROUP: this segment's value for the row, folded with the partners' (block-wide)
+    auto group_combine = [&](uint32_t v, auto op) {
         seq++;
         if (tid == 0) {
             bool ok;
@@ -2396,8 +2396,8 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
     auto flush_chunks = [&]() {
         if (pend_r < 0) return;
         const int ln = lane_fresh();
-        if constexpr (PAIR) {                                  // into the zeroed chunk totals
-            if (pend) pair_add(&chunks[pend_r * 64 + ln], pend);
+        if constexpr (GROUP) {                                  // into the zeroed chunk totals
+            if (pend) group_add(&chunks[pend_r * 64 + ln], pend);
         } else {
             chunks[pend_r * 64 + ln] = pend;
         }
@@ -2481,11 +2481,11 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
                 all_ok = all_ok && bm >= 0 && bm <= 0x7F80;
                 bi = gg == g ? bm : bi;
             }
-            if constexpr (PAIR) {                              // one row: the int max of both halves
-                bi = (int)pair_combine((uint32_t)bi, [](uint32_t a, uint32_t b) {
+            if constexpr (GROUP) {                              // one row: the int max of all segments
+                bi = (int)group_combine((uint32_t)bi, [](uint32_t a, uint32_t b) {
                     return (int)a > (int)b ? a : b;
                 });
-                all_ok = bi >= 0 && bi <= 0x7F80;              // (both halves: the same branch)
+                all_ok = bi >= 0 && bi <= 0x7F80;              // (every segment: the same branch)
             }
             if (all_ok) {                                      // (see k_q1_stats)
                 m = __uint_as_float((uint32_t)bi << 16);
@@ -2507,7 +2507,7 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
                 m = smax[g * NWR];
 #pragma unroll
                 for (int i = 1; i < NWR; i++) m = fmaxf(m, smax[g * NWR + i]);
-                if constexpr (PAIR) m = __uint_as_float(pair_combine(__float_as_uint(m), [](uint32_t a, uint32_t b) { return f32_max_bits(a, b); }));
+                if constexpr (GROUP) m = __uint_as_float(group_combine(__float_as_uint(m), [](uint32_t a, uint32_t b) { return f32_max_bits(a, b); }));
             }
         } else {
             float mx = -INFINITY;
@@ -2528,7 +2528,7 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
             m = smax[g * NWR];
 #pragma unroll
             for (int i = 1; i < NWR; i++) m = fmaxf(m, smax[g * NWR + i]);
-            if constexpr (PAIR) m = __uint_as_float(pair_combine(__float_as_uint(m), [](uint32_t a, uint32_t b) { return f32_max_bits(a, b); }));
+            if constexpr (GROUP) m = __uint_as_float(group_combine(__float_as_uint(m), [](uint32_t a, uint32_t b) { return f32_max_bits(a, b); }));
         }
         if (DEC && valid && gti() == 0 && hh == 0) mrow[r] = m;   // now: m is not held over pass 2
         if constexpr (DEC) flush_chunks();                    // the previous row's (LAC_Q1_DEFER)
@@ -2540,7 +2540,7 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
             const int sc = (int)(s < 0 ? 0 : (s > V ? V : s));
             sfull = sc / N;
             sr = sc - sfull * N;
-            sfull -= vofs;                                     // PAIR: < 0 in the second half when s is in the first
+            sfull -= vofs;                                     // GROUP: < 0 in a segment past the one holding s
         }
         uint32_t tot = 0, lo = 0, sv[8];                     // DEC: one half's vector sums
         if (!DEC && sfull >= 0 && sfull < nvec && (sfull & (NT - 1)) == gti()) {
@@ -2630,13 +2630,13 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
         if (DEC) {
             if (wg == 0 && valid) {
                 // chunk c = groups [c G, (c + 1) G) of the row's ngrp groups
-                // PAIR: this half's groups are the row's [gofs, gofs + ngrp) (split is a multiple of 64)
+                // GROUP: this segment's groups are the row's [gofs, gofs + ngrp) (split is a multiple of 64)
                 const int ngrp = (nvec + 63) / 64, ln = lane_fresh(), gofs = vofs / 64;
                 const int g0 = ln * (int)G, ga = g0 > gofs ? g0 : gofs;
                 const int gb = g0 + (int)G < gofs + ngrp ? g0 + (int)G : gofs + ngrp;
                 uint64_t ct = 0;
                 for (int gi = ga; gi < gb; gi++) ct += gtot[g * NWR * (R + L) + gi - gofs];
-                pend = ct + (PAIR && !pok ? kPairPoison : 0);
+                pend = ct + (GROUP && !pok ? kGroupPoison : 0);
                 pend_r = r;
                 if (!DEFER) flush_chunks();
             }
@@ -2644,11 +2644,11 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
             uint64_t T = 0, Ls = 0, ps = sps[g];
 #pragma unroll
             for (int i = 0; i < NWR; i++) { T += ssum[g * NWR + i][0]; Ls += ssum[g * NWR + i][1]; }
-            if constexpr (PAIR) {                              // the halves' partials add up
+            if constexpr (GROUP) {                              // the segments' partials add up
                 RowStats *o = out + r;                         // (zeroed; inv_tot 0: the coder divides)
-                pair_add(&o->tot, T + (pok ? 0 : kPairPoison));
-                pair_add(&o->lo, Ls);
-                pair_add(&o->hi, Ls + ps);
+                group_add(&o->tot, T + (pok ? 0 : kGroupPoison));
+                group_add(&o->lo, Ls);
+                group_add(&o->hi, Ls + ps);
                 if (hh == 0) __hip_atomic_store(&o->minp, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 continue;
             }
@@ -3235,7 +3235,7 @@ static int q1_group_kernel(lac_ctx *c, const Q1Args &a, hipStream_t st, int spli
     const int64_t need = 8 * K * ((a.rows + 7) / 8), cap = (int64_t)(c->cus / (8 * K)) * (8 * K);
     const unsigned grid = (unsigned)(need < cap ? need : cap);
     HIPCHK(hipMemsetAsync(c->pxch, 0, sizeof(uint64_t) * 2 * grid, st));   // no stale sequence numbers
-    // the halves add into zeroed outputs
+    // the segments add into zeroed outputs
     if (DEC) HIPCHK(hipMemsetAsync(c->q1chunks, 0, sizeof(uint64_t) * 64 * a.rows, st));
     else HIPCHK(hipMemsetAsync(c->stats, 0, sizeof(RowStats) * a.rows, st));
     ProfScope ps(c, KID_Q1_STATS, st);
