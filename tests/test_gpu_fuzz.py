@@ -72,6 +72,8 @@ def _logits_case(i):
     dtype = "bf16" if rng.random() < 0.6 else "f32"
     sizes = [8, 64, 1000, 4096, 8200, 32000, 32768 + 8, 65536]
     sizes += [128256, 128512, 128520, 131072] if dtype == "bf16" else [65536 - 8]
+    # rows over groups of 2..4 blocks (shape 19)
+    sizes += [131080, 151936, 262144, 300000] if dtype == "bf16" else [65540, 128256, 151936, 200000, 262144]
     V = int(rng.choice(sizes))
     lo = max(int(np.ceil(np.log2(V))) + 2, 8)
     prec = int(rng.integers(lo, 62))
@@ -80,7 +82,7 @@ def _logits_case(i):
     while B * steps * V > 2_000_000 and B > 1:
         B //= 2
     scale = float(rng.choice([0.25, 3.0, 12.0]))
-    shape = int(rng.choice([0, 0, 0] + list(range(1, 19))))
+    shape = int(rng.choice([0, 0, 0] + list(range(1, 20))))
     return dtype, V, prec, B, steps, scale, shape
 
 
