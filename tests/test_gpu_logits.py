@@ -301,3 +301,16 @@ def test_paired_row_stats_many_rows(dtype, V, B, steps):
     c.decode_open()
     assert torch.equal(c.decode_logits(dl), sym)
     c.raise_on_error()
+
+
+def test_q1_shape_option_range():
+    """LAC_OPT_Q1_SHAPE takes 0 (AUTO) .. 19; anything else is refused with LAC_E_ARG."""
+    from lac_amd._lib import LacError, LAC_E_ARG
+    c = _coder(1024, 4, 40)
+    for bad in (-1, 20, 99):
+        with pytest.raises(LacError) as e:
+            c.set_q1_shape(bad)
+        assert e.value.code == LAC_E_ARG
+    for ok in (0, 19):
+        c.set_q1_shape(ok)
+    c.close()
