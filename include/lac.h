@@ -85,8 +85,10 @@ enum {                       /* lac_set_option */
                                       <= 8192 vectors per 16-wave block, 19 = one row of
                                       16385..65536 vectors over a group of 2..4 16-wave blocks
                                       (one segment each in the form of 15; f32 V = 128256 /
-                                      151936 / 262144, bf16 V = 151936 / 256000); identical
-                                      results, only speed differs */
+                                      151936 / 262144, bf16 V = 256000), 20 = 19 with two rows
+                                      of segments of <= 8192 vectors per block (bf16 V =
+                                      151936, f32 V = 65540); identical results, only speed
+                                      differs */
     LAC_OPT_DECODE_FINE = 7,       /* one-wave decode (FUSED path): 1 = one total per 64 vectors of
                                       the row, so only 1 KB is re-read after the search (default,
                                       rows <= 131072 u32 / 65536 u64 entries); 0 = <= 64 chunk totals */

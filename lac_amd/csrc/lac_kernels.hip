@@ -2296,17 +2296,19 @@ __device__ inline uint64_t group_ld(const uint64_t *p) {
 // exchange: a block posts seq + 1 only after reading all its partners' seq, so no
 // partner's word for seq is overwritten unread) and fold in the K - 1 partners'
 // (blocks ((slot / K) * K + k) * 8 + xcd) with op; *ok = false when one never came
-template <int K, typename Op>
-__device__ inline uint32_t group_exchange(uint64_t *xch, uint32_t seq, uint32_t m, Op op, bool *ok) {
+// (NRB rows per block: row g of the block uses word pair b * NRB + g)
+template <int K, int NRB, typename Op>
+__device__ inline uint32_t group_exchange(uint64_t *xch, int g, uint32_t seq, uint32_t m, Op op, bool *ok) {
     const unsigned b = blockIdx.x, sl = seq & 1, xcd = b & 7, g0 = ((b >> 3) / K) * K;
-    __hip_atomic_store(&xch[2 * b + sl], ((uint64_t)seq << 32) | m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&xch[2 * (b * NRB + g) + sl], ((uint64_t)seq << 32) | m, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
     uint32_t acc = m;
     bool all = true;
 #pragma unroll
     for (int k = 0; k < K; k++) {
         const unsigned pb = (g0 + k) * 8 + xcd;
         if (pb == b) continue;
-        const uint64_t *px = &xch[2 * pb + sl];
+        const uint64_t *px = &xch[2 * (pb * NRB + g) + sl];
         uint64_t v = group_ld(px);
         for (uint32_t n = 0; (uint32_t)(v >> 32) != seq && n < kGroupSpinMax; n++) {
             __builtin_amdgcn_s_sleep(2);
@@ -2341,7 +2343,7 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
     constexpr bool IMAX = LAC_Q1_IMAX && sizeof(LT) == 2;
     static_assert((R + L) * N <= 128, "lane sums must fit 32 bits");
     constexpr bool GROUP = KG > 1;                              // a row over a group of KG blocks
-    static_assert(!GROUP || NT == 1024, "groups: one row segment per block");
+    static_assert(!GROUP || NT >= 512, "groups: one or two row segments per block");
     // (not the bf16 8-copy decode forms, which sit at the 128-VGPR cap: two more live
     // registers there add spills)
     constexpr bool DEFER = LAC_Q1_DEFER && !(sizeof(LT) == 2 && REP == kRLRep);
@@ -2375,21 +2377,21 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
     auto row_of = [&](int64_t r) {
         return lg + (t0 + r / B) * step_stride + (r % B) * stream_stride + (int64_t)vofs * N;
     };
-    __shared__ uint32_t sxv;
-    __shared__ int sxok;
+    __shared__ uint32_t sxv[NRB];
+    __shared__ int sxok[NRB];
     uint32_t seq = 0;                                           // GROUP: exchanges done
     bool pok = true;                                            // GROUP: every exchange of this row came
     // GROUP: this segment's value for the row, folded with the partners' (block-wide)
     auto group_combine = [&](uint32_t v, auto op) {
         seq++;
-        if (tid == 0) {
+        if (tid == g * NT) {                                    // each row's leader
             bool ok;
-            sxv = group_exchange<KG>(xch, seq, v, op, &ok);
-            sxok = ok;
+            sxv[g] = group_exchange<KG, NRB>(xch, g, seq, v, op, &ok);
+            sxok[g] = ok;
         }
         __syncthreads();
-        pok = pok && sxok != 0;
-        return sxv;
+        pok = pok && sxok[g] != 0;
+        return sxv[g];
     };
     int64_t pend_r = -1;                                        // DEC, LAC_Q1_DEFER: a row's chunk totals
     uint64_t pend = 0;                                          //   (lane ln: chunk ln) not yet stored
@@ -2485,7 +2487,9 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
                 bi = (int)group_combine((uint32_t)bi, [](uint32_t a, uint32_t b) {
                     return (int)a > (int)b ? a : b;
                 });
-                all_ok = bi >= 0 && bi <= 0x7F80;              // (every segment: the same branch)
+                all_ok = true;                                 // (block-uniform: every row's combined max)
+#pragma unroll
+                for (int gg = 0; gg < NRB; gg++) all_ok = all_ok && (int)sxv[gg] >= 0 && (int)sxv[gg] <= 0x7F80;
             }
             if (all_ok) {                                      // (see k_q1_stats)
                 m = __uint_as_float((uint32_t)bi << 16);
@@ -3204,15 +3208,17 @@ static int q1_rl_kernel(lac_ctx *c, const Q1Args &a, hipStream_t st) {
 // vectors (a multiple of 64), the last one the rest; every segment must fit one
 // block's registers + slots -- the 16-copy form (<= 16064 vectors) with the fewest
 // blocks if any K allows it, else the 8-copy form (<= 16384).
+// Shape 20: the same with two rows per block (8 waves each), segments of <= 7999
+// vectors (16-copy form) else <= 8192.
 struct Q1Group {
     int k = 0, split = 0;
     bool rep16 = false;
 };
-static bool q1_group(lac_ctx *c, int64_t nvec, Q1Group *g) {
-    if (nvec <= 16384) return false;
+static bool q1_group(lac_ctx *c, int64_t nvec, Q1Group *g, bool two = false) {
+    if (nvec <= (two ? 8192 : 16384)) return false;
     const int64_t ngrp = (nvec + 63) / 64;
     for (int pass = 0; pass < 2; pass++) {
-        const int64_t lim = pass ? 16384 : kRLTrimMaxVec;
+        const int64_t lim = two ? (pass ? 8192 : 15 * 512 + 320) : (pass ? 16384 : kRLTrimMaxVec);
         for (int k = 2; k <= 4 && 8 * k <= c->cus; k++) {
             const int64_t sp = 64 * ((ngrp + k - 1) / k), last = nvec - (k - 1) * sp;
             if (last > 0 && sp <= lim && last <= lim) {
@@ -3226,37 +3232,42 @@ static bool q1_group(lac_ctx *c, int64_t nvec, Q1Group *g) {
     return false;
 }
 
-template <typename LT, bool DEC, int REP, int LASTN, int K>
+template <typename LT, bool DEC, int REP, int LASTN, int K, int NT = 1024>
 static int q1_group_kernel(lac_ctx *c, const Q1Args &a, hipStream_t st, int split) {
+    constexpr int NRB = 1024 / NT;
     const int64_t nvec = c->V / LogitN<LT>::N;
-    if (!c->pxch) HIPCHK(hipMalloc(&c->pxch, sizeof(uint64_t) * 2 * c->cus));
+    if (!c->pxch) HIPCHK(hipMalloc(&c->pxch, sizeof(uint64_t) * 4 * c->cus));   // (<= 2 rows per block)
     // groups of K blocks in runs of 8 K (one per XCD each); never more blocks than CUs
     // (one per CU: every member of every group resident at once)
-    const int64_t need = 8 * K * ((a.rows + 7) / 8), cap = (int64_t)(c->cus / (8 * K)) * (8 * K);
+    const int64_t need = 8 * K * ((a.rows + 8 * NRB - 1) / (8 * NRB)), cap = (int64_t)(c->cus / (8 * K)) * (8 * K);
     const unsigned grid = (unsigned)(need < cap ? need : cap);
-    HIPCHK(hipMemsetAsync(c->pxch, 0, sizeof(uint64_t) * 2 * grid, st));   // no stale sequence numbers
+    HIPCHK(hipMemsetAsync(c->pxch, 0, sizeof(uint64_t) * 2 * NRB * grid, st));   // no stale sequence numbers
     // the segments add into zeroed outputs
     if (DEC) HIPCHK(hipMemsetAsync(c->q1chunks, 0, sizeof(uint64_t) * 64 * a.rows, st));
     else HIPCHK(hipMemsetAsync(c->stats, 0, sizeof(RowStats) * a.rows, st));
     ProfScope ps(c, KID_Q1_STATS, st);
-    k_q1_stats_rl<LT, DEC, REP, LASTN, 1024, K><<<grid, 1024, 0, st>>>(
+    k_q1_stats_rl<LT, DEC, REP, LASTN, NT, K><<<grid, 1024, 0, st>>>(
         (const LT *)a.lg, a.ss, a.bs, a.sym, c->B, a.rows, c->V, a.t0, a.xsh, q1_groups_per_chunk(nvec), c->stats,
         c->q1chunks, c->q1m, c->pxch, split);
     CHECK_LAUNCH();
     return LAC_OK;
 }
 
-template <typename LT, bool DEC, int REP, int LASTN>
+template <typename LT, bool DEC, int REP, int LASTN, int NT>
 static int q1_group_k(lac_ctx *c, const Q1Args &a, hipStream_t st, const Q1Group &g) {
-    if (g.k == 2) return q1_group_kernel<LT, DEC, REP, LASTN, 2>(c, a, st, g.split);
-    if (g.k == 3) return q1_group_kernel<LT, DEC, REP, LASTN, 3>(c, a, st, g.split);
-    return q1_group_kernel<LT, DEC, REP, LASTN, 4>(c, a, st, g.split);
+    if (g.k == 2) return q1_group_kernel<LT, DEC, REP, LASTN, 2, NT>(c, a, st, g.split);
+    if (g.k == 3) return q1_group_kernel<LT, DEC, REP, LASTN, 3, NT>(c, a, st, g.split);
+    return q1_group_kernel<LT, DEC, REP, LASTN, 4, NT>(c, a, st, g.split);
 }
 
 template <typename LT, bool DEC>
-static int q1_stats_group_launch(lac_ctx *c, const Q1Args &a, hipStream_t st, const Q1Group &g) {
-    if (g.rep16) return q1_group_k<LT, DEC, 16, kRLLastTrim>(c, a, st, g);
-    return q1_group_k<LT, DEC, kRLRep, 1024>(c, a, st, g);
+static int q1_stats_group_launch(lac_ctx *c, const Q1Args &a, hipStream_t st, const Q1Group &g, bool two = false) {
+    if (two) {
+        if (g.rep16) return q1_group_k<LT, DEC, 16, 320, 512>(c, a, st, g);
+        return q1_group_k<LT, DEC, kRLRep, 512, 512>(c, a, st, g);
+    }
+    if (g.rep16) return q1_group_k<LT, DEC, 16, kRLLastTrim, 1024>(c, a, st, g);
+    return q1_group_k<LT, DEC, kRLRep, 1024, 1024>(c, a, st, g);
 }
 
 // The register + LDS-slot shapes (k_q1_stats_rl), by rows per block:
@@ -3323,8 +3334,13 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
         if (sh == 0 && nvec <= 16384) sh = 15;
         // longer rows that two blocks' registers + slots hold: one half per block (shape 19)
         // (bf16: V = 256000 encode 4.36 -> 2.68 ms, 48 -> 78 % of peak; profiles/r02/q1_pair_bf16/)
-        Q1Group g0;
-        if (sh == 0 && q1_group(c, nvec, &g0)) sh = 19;
+        // two rows per block (shape 20) where shape 19's segments would be small (<= 11000
+        // vectors: the per-row exchange is then amortised over two rows): bf16 V = 131080
+        // 50 -> 58 %, 151936 (Qwen2) 57 -> 65 %, f32 65540 60 -> 66 %; at 12500-vector
+        // segments 19 stays ahead (bf16 200000 70 vs 66 %, f32 100000 77 vs 73 %;
+        // profiles/r02/q1_groups2/)
+        Q1Group g0, g1;
+        if (sh == 0 && q1_group(c, nvec, &g0)) sh = g0.split <= 11000 && q1_group(c, nvec, &g1, true) ? 20 : 19;
         // measured at V = 128256 f32: encode tiles of (16,8) with the tile-rolling
         // prefetch 1.98 ms vs 2.18 for tiles of (8,8) (shape 13, its (8,8) form: 2.20)
         if (sh == 0) sh = nvec <= 64 * 16 * 16 ? 9 : (DEC ? 10 : (sizeof(LT) == 4 ? 14 : 8));
@@ -3342,6 +3358,7 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
     if (sh == 18 && nvec <= 8192) return q1_stats_rl_launch<LT, DEC>(c, a, st, 18);
     Q1Group grp;
     if (sh == 19 && q1_group(c, nvec, &grp)) return q1_stats_group_launch<LT, DEC>(c, a, st, grp);
+    if (sh == 20 && q1_group(c, nvec, &grp, true)) return q1_stats_group_launch<LT, DEC>(c, a, st, grp, true);
     if (sh == 13) return q1_stats_launch<LT, 8, 8, DEC, true, true>(c, a, st);         // tiles of (8,8,y)
     if (sh == 14) return q1_stats_launch<LT, 16, 8, DEC, true, true, 16>(c, a, st);    // tiles of (16,8,y)
     if (sh == 8) return q1_stats_launch<LT, 8, 8, DEC, true, false>(c, a, st);      // tiles of 4096 vectors
@@ -3540,7 +3557,7 @@ int lac_set_option(lac_ctx *c, int option, int64_t value) {
         c->fine_decode = (int)value;
         return LAC_OK;
     case LAC_OPT_Q1_SHAPE:
-        if (value < 0 || value > 19) return fail(LAC_E_ARG, "bad q1 shape");
+        if (value < 0 || value > 20) return fail(LAC_E_ARG, "bad q1 shape");
         c->q1_shape = (int)value;
         return LAC_OK;
     case LAC_OPT_MAPPING:

@@ -82,7 +82,7 @@ def _logits_case(i):
     while B * steps * V > 2_000_000 and B > 1:
         B //= 2
     scale = float(rng.choice([0.25, 3.0, 12.0]))
-    shape = int(rng.choice([0, 0, 0] + list(range(1, 20))))
+    shape = int(rng.choice([0, 0, 0] + list(range(1, 21))))
     return dtype, V, prec, B, steps, scale, shape
 
 

@@ -256,7 +256,7 @@ def test_every_q1_shape_gives_the_same_bits(dtype, V):
     c.encode_logits_job(dl, sym)
     want, wn = c.to_bytes()
     ran = 0
-    for sh in range(1, 20):
+    for sh in range(1, 21):
         c.set_q1_shape(sh)
         try:
             c.encode_logits_job(dl, sym)
@@ -304,13 +304,13 @@ def test_paired_row_stats_many_rows(dtype, V, B, steps):
 
 
 def test_q1_shape_option_range():
-    """LAC_OPT_Q1_SHAPE takes 0 (AUTO) .. 19; anything else is refused with LAC_E_ARG."""
+    """LAC_OPT_Q1_SHAPE takes 0 (AUTO) .. 20; anything else is refused with LAC_E_ARG."""
     from lac_amd._lib import LacError, LAC_E_ARG
     c = _coder(1024, 4, 40)
-    for bad in (-1, 20, 99):
+    for bad in (-1, 21, 99):
         with pytest.raises(LacError) as e:
             c.set_q1_shape(bad)
         assert e.value.code == LAC_E_ARG
-    for ok in (0, 19):
+    for ok in (0, 19, 20):
         c.set_q1_shape(ok)
     c.close()
