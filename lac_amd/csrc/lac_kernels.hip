@@ -3340,7 +3340,9 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
         // segments 19 stays ahead (bf16 200000 70 vs 66 %, f32 100000 77 vs 73 %;
         // profiles/r02/q1_groups2/)
         Q1Group g0, g1;
-        if (sh == 0 && q1_group(c, nvec, &g0)) sh = g0.split <= 11000 && q1_group(c, nvec, &g1, true) ? 20 : 19;
+        // (and only in shape 20's 16-copy form, the one measured)
+        if (sh == 0 && q1_group(c, nvec, &g0))
+            sh = g0.split <= 11000 && q1_group(c, nvec, &g1, true) && g1.rep16 ? 20 : 19;
         // measured at V = 128256 f32: encode tiles of (16,8) with the tile-rolling
         // prefetch 1.98 ms vs 2.18 for tiles of (8,8) (shape 13, its (8,8) form: 2.20)
         if (sh == 0) sh = nvec <= 64 * 16 * 16 ? 9 : (DEC ? 10 : (sizeof(LT) == 4 ? 14 : 8));
