@@ -37,6 +37,10 @@
  *   LAC_E_DECODE_RANGE  decoded range misses the value  arith_code.py:277-278
  *   LAC_E_CAPACITY      stream exceeded capacity_bits
  *   LAC_E_PREC          prec outside [2, 61] or 2^(prec-1) < V
+ *   LAC_E_FLUSH_ZERO_WIDTH  A_from_bin.flush met a zero-width candidate symbol
+ *                       (the reference raises ZeroDivisionError, arith_code.py:307)
+ *   LAC_E_FLUSH_LOOP    A_from_bin.flush emits symbols that leave [l, h]
+ *                       unchanged (the reference loops forever, :308-313)
  */
 #ifndef LAC_H
 #define LAC_H
@@ -59,7 +63,9 @@ enum {
     LAC_E_DECODE_RANGE = -6,
     LAC_E_CAPACITY = -7,
     LAC_E_HIP = -8,
-    LAC_E_STATE = -9
+    LAC_E_STATE = -9,
+    LAC_E_FLUSH_ZERO_WIDTH = -10,
+    LAC_E_FLUSH_LOOP = -11
 };
 
 enum {                       /* lac_set_option */
@@ -277,11 +283,53 @@ typedef struct lac_dec_state {
  * for the bits that arrived since, this resumes a decoder: the bit-serial
  * A_from_bin.step(bit) of the reference (arith_code.py:291-298) is built on it
  * (lac_amd.coder).  set_state refuses (LAC_E_ARG, nothing copied) register sets
- * no decoder reaches: l outside [0, 2^prec), h < l, h - l >= 2^prec, pos < prec
+ * no decoder reaches: l outside [0, 2^(prec+1)), h < l, h - l >= 2^prec, pos < prec
  * (streams with err set are copied as they are).  Not thread-safe with launches
  * on the same context. */
 int lac_decode_get_state(lac_ctx *ctx, lac_dec_state *host_out, void *stream);
 int lac_decode_set_state(lac_ctx *ctx, const lac_dec_state *host_in, void *stream);
+
+/* ---- decoder tail in the reference's register frame (arith_code.py:248-334) ----
+ * A_from_bin holds l, h and the received window [lb, hb] (the bits so far read
+ * with 0s / 1s past the end).  lac_decode_tail_begin converts every stream's
+ * value-form registers (after its determined symbols: lac_decode_determined ==
+ * symbols decoded, else the stream gets LAC_E_STATE) into that frame; then each
+ * lac_decode_tail_step runs one step per stream:
+ *   LAC_TAIL_DECIDE  decide_symbol + emit_symbol + emit_bit (:268-291) on the
+ *                    window: emits the symbol both window ends map to, or
+ *                    nothing (undetermined).  Where the window leaves [l, h]
+ *                    (foreign or corrupt bits) it reproduces the reference:
+ *                    LAC_E_SYMBOL_RANGE naming V for tables (AssertionError
+ *                    'unknown symbol'), out-of-range symbols for LAC_MAP_FLOOR
+ *                    (the uniform Predictor(n) has no range check).
+ *   LAC_TAIL_FLUSH   one iteration of A_from_bin.flush (:300-317): while [l, h]
+ *                    is not inside [lb, hb], the candidate of largest overlap
+ *                    ratio (CPython float ranking, first maximum kept), emitted
+ *                    without renormalisation; once inside, the registers reset
+ *                    and the stream reports idle.
+ * sym_out_dev[b] (int64: uniform symbols can be negative) and code_out_dev[b]:
+ * 0 = a symbol, 1 = nothing (undetermined / flushed), < 0 = the stream's sticky
+ * error (LAC_E_SYMBOL_RANGE with sym_out = the symbol named, LAC_E_DECODE_RANGE
+ * for emit_symbol's AssertionError :277-278, LAC_E_FLUSH_*).  Row b of the
+ * stream's current table at pmf_dev + b*stream_stride (LAC_MAP_CEIL; ignored,
+ * may be NULL, for LAC_MAP_FLOOR, whose alphabet is the context's vocab).
+ * Asynchronous on `stream`. */
+#define LAC_TAIL_DECIDE 0
+#define LAC_TAIL_FLUSH 1
+typedef struct lac_tail_state {
+    int64_t l, h, lb, hb;
+    int32_t err, done;
+    int64_t still, nsym;      /* flush emits with [l, h] unchanged; symbols emitted */
+} lac_tail_state;
+
+int lac_decode_tail_begin(lac_ctx *ctx, void *stream);
+int lac_decode_tail_step(lac_ctx *ctx, const void *pmf_dev, int64_t stream_stride, int mode,
+                         int64_t *sym_out_dev, int32_t *code_out_dev, void *stream);
+/* Copy the tail registers to / from the host (synchronise).  set_state refuses
+ * (LAC_E_ARG) h < l, hb < lb or values beyond +-2^62; receive_bit (:264-267) is a
+ * host-side update of lb, hb between steps. */
+int lac_decode_tail_get_state(lac_ctx *ctx, lac_tail_state *host_out, void *stream);
+int lac_decode_tail_set_state(lac_ctx *ctx, const lac_tail_state *host_in, void *stream);
 
 /* Live kernel timing: with profiling on, every kernel launch is bracketed by
  * hipEvents recorded on its own stream.  lac_profile_read synchronises and

@@ -23,12 +23,15 @@ LAC_E_DECODE_RANGE = -6
 LAC_E_CAPACITY = -7
 LAC_E_HIP = -8
 LAC_E_STATE = -9
+LAC_E_FLUSH_ZERO_WIDTH = -10
+LAC_E_FLUSH_LOOP = -11
 
 STATUS_NAMES = {
     LAC_OK: "LAC_OK", LAC_E_ARG: "LAC_E_ARG", LAC_E_PREC: "LAC_E_PREC",
     LAC_E_SYMBOL_RANGE: "LAC_E_SYMBOL_RANGE", LAC_E_ZERO_WIDTH: "LAC_E_ZERO_WIDTH",
     LAC_E_TABLE: "LAC_E_TABLE", LAC_E_DECODE_RANGE: "LAC_E_DECODE_RANGE",
     LAC_E_CAPACITY: "LAC_E_CAPACITY", LAC_E_HIP: "LAC_E_HIP", LAC_E_STATE: "LAC_E_STATE",
+    LAC_E_FLUSH_ZERO_WIDTH: "LAC_E_FLUSH_ZERO_WIDTH", LAC_E_FLUSH_LOOP: "LAC_E_FLUSH_LOOP",
 }
 
 # (name, restype, argtypes) for every symbol include/lac.h declares
@@ -58,6 +61,10 @@ PROTOTYPES = [
     ("lac_decode_determined", _i, [_vp, _vp, _vp]),
     ("lac_decode_get_state", _i, [_vp, _vp, _vp]),
     ("lac_decode_set_state", _i, [_vp, _vp, _vp]),
+    ("lac_decode_tail_begin", _i, [_vp, _vp]),
+    ("lac_decode_tail_step", _i, [_vp, _vp, _i64, _i, _vp, _vp, _vp]),
+    ("lac_decode_tail_get_state", _i, [_vp, _vp, _vp]),
+    ("lac_decode_tail_set_state", _i, [_vp, _vp, _vp]),
     ("lac_profile_enable", _i, [_vp, _i]),
     ("lac_profile_read", _i, [_vp, _vp, _vp, _i]),
     ("lac_q1_k", _i, [_i, _i64]),
@@ -81,6 +88,7 @@ LAC_OPT_DECODE_FINE = 7
 LAC_OPT_BLOCK_WAVES = 8
 LAC_MAP_CEIL, LAC_MAP_FLOOR = 0, 1
 LAC_TERM_FLUSH, LAC_TERM_ACSAMPLER = 0, 1
+LAC_TAIL_DECIDE, LAC_TAIL_FLUSH = 0, 1
 
 
 class LacLibraryError(RuntimeError):

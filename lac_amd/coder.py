@@ -225,7 +225,7 @@ class A_to_bin:
         need = (steps + 2) * per + self._SLACK
         if self._coder is not None and self._V == V:
             return
-        if self._coder is not None and self._plane_bits:
+        if self._coder is not None and (self._plane_bits or self._nsym):
             raise RuntimeError(f"table size changed mid-stream ({self._V} -> {V} symbols); flush() first")
         if self._coder is not None:
             self._coder.close()
@@ -239,11 +239,14 @@ class A_to_bin:
         """Encode rows/syms (chunked to the coder's capacity); -> (digit lists, (rc, n_ok))."""
         steps = len(syms)
         V = len(rows[0])
-        if self._coder is not None and self._V == V and self._plane_bits == 0:
+        if self._coder is not None and self._V == V and self._plane_bits == 0 and self._nsym == 0:
+            # a fresh coder (nothing coded since the last reset: a symbol of p > 1/2
+            # narrows l, h without emitting a digit, so empty planes alone do not
+            # mean fresh registers): reallocate at the new size
             per = self.precision + 1
             if self._coder.capacity_bits < (steps + 2) * per + self._SLACK:
                 self._coder.close()
-                self._coder = None    # empty planes: reallocate at the new size
+                self._coder = None
         self._ensure(V, steps)
         per = self.precision + 1
         out = []
@@ -377,12 +380,198 @@ class A_to_bin:
 
 
 # ------------------------------------------------------------------ decoder
+_DEC_STATE = np.dtype([("l", "<i8"), ("h", "<i8"), ("x", "<i8"), ("pos", "<u8"), ("nsym", "<i8"),
+                       ("err", "<i4"), ("det", "<i4"), ("err_step", "<i8"), ("ndet", "<i8")])   # lac_dec_state
+_TAIL_STATE = np.dtype([("l", "<i8"), ("h", "<i8"), ("lb", "<i8"), ("hb", "<i8"), ("err", "<i4"),
+                        ("done", "<i4"), ("still", "<i8"), ("nsym", "<i8")])                     # lac_tail_state
+
+
+def _raise_decoder(code, sym=None):
+    """The reference's exception for a decoder status (include/lac.h)."""
+    if code == _lib.LAC_E_SYMBOL_RANGE:
+        raise AssertionError("unknown symbol", sym)                       # arith_code.py:100-101
+    if code == _lib.LAC_E_DECODE_RANGE:
+        raise AssertionError("predictor range does not correspond to val")   # :277-278
+    if code == _lib.LAC_E_FLUSH_ZERO_WIDTH:
+        raise ZeroDivisionError("division by zero")                       # flush's k(s), :307
+    if code == _lib.LAC_E_FLUSH_LOOP:
+        raise RuntimeError("A_from_bin.flush does not terminate here (the reference loops forever, "
+                           "arith_code.py:308-313)")
+    raise _lib.LacError(code, "decoder error")
+
+
+class _Session:
+    """One bit-serial decoding session of an A_from_bin: the bits received so far
+    (host copy, packed MSB first, and its device copy), the predictor's tables,
+    and the decoder registers parked on the host between calls -- in the value
+    form of the fast decoders (lac_dec_state) while the received window lies
+    inside [l, h], in the reference frame (lac_tail_state: l, h, lb, hb) after the
+    window has left it or for the flush.  Every symbol decision runs on the GPU."""
+
+    def __init__(self, dec):
+        self.dec = dec
+        self.prec = dec.precision
+        self.tab = _Tables(dec.predictor)
+        self.bits = []
+        self.buf = np.zeros(64, dtype=np.uint8)
+        self.dev = None
+        self.nb = None
+        self.coder = None
+        self.st = np.zeros(1, dtype=_DEC_STATE)          # value form: nothing received yet
+        self.st["h"] = dec.denom - 1
+        self.st["pos"] = self.prec
+        self.st["det"] = 1
+        self.st["err_step"] = -1
+        self.tst = None                                   # reference frame (tail mode)
+        if self.tab.uniform:
+            # Predictor(n)'s val_to_symbol is not the inverse of its floor
+            # symbol_to_range, so emit_symbol's overlap check (arith_code.py:277)
+            # depends on the window at the bit where a symbol became determined:
+            # these streams are decoded bit-serially in the reference frame
+            self.tst = np.zeros(1, dtype=_TAIL_STATE)
+            self.tst["h"] = dec.denom - 1
+            self.tst["hb"] = dec.denom - 1
+
+    # -- plumbing
+    def _coder_for(self, V):
+        import torch
+        if self.coder is None or self.coder.vocab != V:
+            if self.coder is not None:
+                self.coder.close()
+            self.coder = BatchCoder(V, 1, prec=self.prec, pmf_bits=64, capacity_bits=64)
+            self.coder.set_mapping(self.tab.mapping)
+            self.dev = None
+        c = self.coder
+        if self.dev is None or self.dev.device != c.device:
+            self.dev = torch.from_numpy(self.buf.reshape(1, -1).copy()).to(c.device)
+            self.nb = torch.zeros(1, dtype=torch.int64, device=c.device)
+        self.nb.fill_(len(self.bits))
+        return c
+
+    def _row_dev(self, row, c):
+        import torch
+        return torch.from_numpy(row.view(np.int64).reshape(1, 1, len(row))).to(c.device)
+
+    def add_bit(self, bit):
+        if (len(self.bits) >> 3) + 8 >= len(self.buf):
+            self.buf = np.concatenate([self.buf, np.zeros(len(self.buf), dtype=np.uint8)])
+            self.dev = None
+        n = len(self.bits)
+        self.bits.append(bit)
+        if bit:
+            self.buf[n >> 3] |= 0x80 >> (n & 7)
+        if self.dev is not None and (n >> 3) < self.dev.shape[1]:
+            self.dev[0, n >> 3] = int(self.buf[n >> 3])      # only the byte the new bit went into
+        if self.tst is not None:                             # receive_bit (arith_code.py:264-267)
+            t = self.tst
+            wb = (int(t["hb"][0]) - int(t["lb"][0]) + 1) // 2
+            t["lb"] += wb * bit
+            t["hb"] = int(t["lb"][0]) + wb - 1
+            return
+        st = self.st
+        pos = int(st["pos"][0])
+        if bit and pos - self.prec <= n < pos:               # was read as a padding 0
+            st["x"] += 1 << (pos - 1 - n)
+
+    def load_bits(self, bl, data):
+        """Take a whole bit list at once (the fast path): the same buffers add_bit builds."""
+        self.bits = list(bl)
+        self.buf = np.zeros(max(64, ((len(bl) >> 3) + 8) * 2 + 7 & ~7), dtype=np.uint8)   # rows 8-byte aligned
+        self.buf[:len(data)] = np.frombuffer(data, dtype=np.uint8)
+        self.dev = None
+        x = 0
+        for i in range(self.prec):                        # the first window, 0s past the end
+            x = (x << 1) | (self.bits[i] if i < len(self.bits) else 0)
+        self.st["x"] = x
+
+    # -- decisions
+    def decide(self):
+        """Every symbol the bits received so far determine (decide_symbol /
+        emit_symbol / emit_bit, arith_code.py:268-299), yielded one at a time."""
+        while self.tst is None:
+            row = self.tab.row()
+            c = self._coder_for(len(row))
+            c.decode_open(self.dev, self.nb)
+            trial = self.st.copy()
+            trial["det"] = 1
+            trial["ndet"] = 0
+            check(c.lib.lac_decode_set_state(c.ctx, trial.ctypes.data_as(C.c_void_p), c._stream))
+            s = int(c.decode(self._row_dev(row, c)).cpu()[0, 0])
+            new = np.zeros(1, dtype=_DEC_STATE)
+            check(c.lib.lac_decode_get_state(c.ctx, new.ctypes.data_as(C.c_void_p), c._stream))
+            if int(new["err"][0]):
+                # the window has left [l, h] (foreign or corrupt bits): continue in the
+                # reference's frame, where the reference raises or (uniform
+                # Predictor) emits out-of-range symbols
+                self.to_tail()
+                break
+            if int(new["ndet"][0]) != 1:
+                return                                       # not determined by the bits so far
+            self.st = new
+            self.dec.predictor.accept(s)
+            yield s
+        while True:
+            code, s = self.tail_step(_lib.LAC_TAIL_DECIDE)
+            if code == 1:
+                return
+            self.dec.predictor.accept(s)
+            yield s
+
+    def to_tail(self):
+        """Value-form registers -> l, h, lb, hb (lac_decode_tail_begin)."""
+        row = self.tab.row()
+        c = self._coder_for(len(row))
+        c.decode_open(self.dev, self.nb)
+        st = self.st.copy()
+        check(c.lib.lac_decode_set_state(c.ctx, st.ctypes.data_as(C.c_void_p), c._stream))
+        check(c.lib.lac_decode_tail_begin(c.ctx, c._stream))
+        self.tst = np.zeros(1, dtype=_TAIL_STATE)
+        check(c.lib.lac_decode_tail_get_state(c.ctx, self.tst.ctypes.data_as(C.c_void_p), c._stream))
+
+    def tail_step(self, mode):
+        """One DECIDE / FLUSH step on the GPU -> (code, symbol); raises the
+        reference's exception on an error."""
+        import torch
+        row = self.tab.row()
+        c = self._coder_for(len(row))
+        check(c.lib.lac_decode_tail_set_state(c.ctx, self.tst.ctypes.data_as(C.c_void_p), c._stream))
+        pmf = None if self.tab.uniform else self._row_dev(row, c)
+        out = torch.zeros(2, dtype=torch.int64, device=c.device)
+        check(c.lib.lac_decode_tail_step(c.ctx, C.c_void_p(pmf.data_ptr()) if pmf is not None else None, 0, mode,
+                                         C.c_void_p(out.data_ptr()), C.c_void_p(out.data_ptr() + 8), c._stream))
+        check(c.lib.lac_decode_tail_get_state(c.ctx, self.tst.ctypes.data_as(C.c_void_p), c._stream))
+        sym, code = out.cpu().tolist()
+        code = int(np.int64(code).astype(np.int32))           # int32 code in the low half
+        if code < 0:
+            _raise_decoder(code, sym)
+        return code, sym
+
+    def flush(self):
+        """A_from_bin.flush (arith_code.py:300-317), one GPU step per symbol."""
+        if self.tst is None:
+            self.to_tail()
+        while True:
+            code, s = self.tail_step(_lib.LAC_TAIL_FLUSH)
+            if code == 1:
+                return
+            self.dec.predictor.accept(s)
+            yield s
+
+    def close(self):
+        if self.coder is not None:
+            self.coder.close()
+            self.coder = None
+
+
 class A_from_bin:
     """Decoder (arith_code.py:248-334) backed by liblac.so (one stream).
 
-    The reference decodes bit-serially and stops when the bits run out; the
-    stream itself does not record its symbol count (SURVEY.md finding 5), so
-    ``run``/``decode`` take ``n``, the number of symbols to produce.
+    ``run(bits, stop)``, ``step(bit)`` / ``__call__(bit)``, ``flush()`` /
+    ``__call__(None)`` and ``decode(R, L, stop)`` yield exactly the symbols the
+    reference yields, in the same order, and raise where it raises (its flush
+    included: SURVEY.md finding 5; golden vectors tests/golden/flush_cases.json).
+    The stream does not record its symbol count; ``run(bits, n=...)`` is this
+    build's extension that decodes exactly n symbols (zero bits past the end).
     """
 
     def __init__(self, predictor=ternary, prec=16):
@@ -390,47 +579,112 @@ class A_from_bin:
         self.precision = prec
         self.denom = 1 << prec
         self.decision = 1 << (prec - 1)
+        self._sess = None
 
     def run(self, bits, stop=1, n=None, max_symbols=1 << 24):
-        """Decode ``bits`` (an iterable of 0/1).
+        """A_from_bin.run (arith_code.py:322-326), a generator like the reference's.
 
-        With ``n`` given: exactly n symbols (reads zero bits past the end).
-        Without: every symbol the bits determine -- the count the reference's
-        bit-serial ``run(bits, stop=0)`` emits (arith_code.py:268-299, 322-326).
-        ``stop=1`` does not run the reference's heuristic flush (:300-317),
-        which raises on about a fifth of valid streams (SURVEY.md finding 5).
-        """
-        if hasattr(self, "_sbits") and n is None:
-            # bits already fed through step(): the reference's run is step() over each
-            # bit (arith_code.py:322-326), continuing from where those left off
-            return iter([s for b in bits for s in self._step_bit(int(b))])
-        bl = [int(b) for b in bits]
+        A fresh decoder takes the whole bit list at once: the fast value-form
+        decoder finds the determined symbols (one GPU decode per symbol), the
+        reference-frame tail continues where the window leaves [l, h], and
+        ``stop`` runs the flush.  A decoder that already holds a stream (step()
+        calls, a run(..., stop=0)) continues it bit by bit, as the reference does.
+        With ``n``: exactly n symbols of a fresh stream, no flush (this build's
+        extension; ``max_symbols`` bounds the count-free form)."""
+        if n is not None:
+            bl = [int(b) for b in bits]
+            if _is_uniform(self.predictor):
+                return iter(self._uniform_n(bl, n))
+            return iter(self._decode_bytes(bytes(group_bits(iter(bl))), len(bl), n))
+        return self._run(bits, stop, max_symbols)
+
+    def _uniform_n(self, bl, n):
+        """n symbols of a Predictor(n) stream: the reference's bit-serial decoder
+        over the bits, then zero bits, until n symbols are out."""
+        out = []
+        sess = _Session(self)
+        try:
+            i = 0
+            while len(out) < n:
+                sess.add_bit(bl[i] if i < len(bl) else 0)
+                out.extend(sess.decide())
+                i += 1
+                if i > len(bl) + 4 * (n + 1) * self.precision:
+                    raise AssertionError("predictor range does not correspond to val")
+        finally:
+            sess.close()
+        return out[:n]
+
+    def _run(self, bits, stop, max_symbols):
+        if self._sess is not None:
+            for b in bits:
+                yield from self.step(b)
+        else:
+            bl = [int(b) for b in bits]
+            if any(b not in (0, 1) for b in bl):
+                raise ValueError("bits are 0 or 1")
+            yield from self._fast(bl, max_symbols)
+        if stop:
+            yield from self.flush()
+
+    def _fast(self, bl, max_symbols):
+        """Determined symbols of a whole bit list: value-form decode per symbol;
+        the registers before a symbol the bits do not determine (or that fails)
+        are restored and parked as this decoder's session."""
+        sess = self._sess = _Session(self)
+        if sess.tst is not None:                   # Predictor(n): bit-serial (see _Session)
+            for b in bl:
+                sess.add_bit(b)
+                yield from sess.decide()
+            return
         data = bytes(group_bits(iter(bl)))
-        return iter(self._decode_bytes(data, len(bl), n, max_symbols))
+        sess.load_bits(bl, data)
+        tab = sess.tab
+        for _ in range(max_symbols):
+            row = tab.row()
+            c = sess._coder_for(len(row))
+            c.decode_open(sess.dev, sess.nb)
+            st = sess.st.copy()
+            check(c.lib.lac_decode_set_state(c.ctx, st.ctypes.data_as(C.c_void_p), c._stream))
+            s = int(c.decode(sess._row_dev(row, c)).cpu()[0, 0])
+            new = np.zeros(1, dtype=_DEC_STATE)
+            check(c.lib.lac_decode_get_state(c.ctx, new.ctypes.data_as(C.c_void_p), c._stream))
+            if int(new["err"][0]) or int(new["ndet"][0]) != int(st["ndet"][0]) + 1:
+                break
+            sess.st = new
+            self.predictor.accept(s)
+            yield s
+        yield from sess.decide()                   # undetermined: nothing; window off [l, h]: the reference's way
 
     # ---- registers (arith_code.py:249-263): l, h and the received-bit interval [lb, hb]
-    # in the same frame; bit-serial decoding keeps them on the host between bits
+    def _regs(self):
+        d = self.denom
+        if self._sess is None:
+            return 0, d - 1, 0, d - 1
+        if self._sess.tst is not None:
+            t = self._sess.tst
+            return int(t["l"][0]), int(t["h"][0]), int(t["lb"][0]), int(t["hb"][0])
+        st = self._sess.st
+        past = int(st["pos"][0]) - len(self._sess.bits)
+        pad = min(max(past, 0), self.precision)
+        x = int(st["x"][0])
+        return int(st["l"][0]), int(st["h"][0]), x, x + (1 << pad) - 1
+
     @property
     def l(self):
-        return int(self._sstate["l"][0]) if hasattr(self, "_sstate") else 0
+        return self._regs()[0]
 
     @property
     def h(self):
-        return int(self._sstate["h"][0]) if hasattr(self, "_sstate") else self.denom - 1
-
-    def _pad(self):
-        if not hasattr(self, "_sstate"):
-            return self.precision
-        past = int(self._sstate["pos"][0]) - len(self._sbits)
-        return min(max(past, 0), self.precision)
+        return self._regs()[1]
 
     @property
     def lb(self):
-        return int(self._sstate["x"][0]) if hasattr(self, "_sstate") else 0
+        return self._regs()[2]
 
     @property
     def hb(self):
-        return self.lb + (1 << self._pad()) - 1
+        return self._regs()[3]
 
     def __repr__(self):
         sl = bin(self.l + (self.denom << 1))[3:]
@@ -440,97 +694,59 @@ class A_from_bin:
         slb = "".join(slb[i] for i in range(len(slb)) if slb[i] == shb[i])
         return f"A_from_bin([{sl[0]}.{sl[1:]},{sh[0]}.{sh[1:]}],{slb[0]}.{slb[1:]})"
 
-    # ---- bit-serial decoding: step(bit) / __call__(bit) (arith_code.py:291-298, 318-321)
-    _DEC_STATE = np.dtype([("l", "<i8"), ("h", "<i8"), ("x", "<i8"), ("pos", "<u8"), ("nsym", "<i8"),
-                           ("err", "<i4"), ("det", "<i4"), ("err_step", "<i8"), ("ndet", "<i8")])   # lac_dec_state
-
+    # ---- bit-serial decoding: step(bit) / __call__ (arith_code.py:291-298, 318-321)
     def step(self, bit):
         """receive_bit + the decide_symbol / emit_symbol loop (arith_code.py:291-298):
         yields, once each, the symbols that the bits received so far determine --
-        the same symbols after the same bits as the reference.
+        the same symbols after the same bits as the reference, raising where it
+        raises.
 
-        The GPU decodes; between calls the decoder's registers wait on the host
-        (include/lac.h lac_decode_get_state / set_state).  Each call tries the next
-        symbol against the bits so far, zero-padded: when both the 0- and 1-padded
-        ends of the available bits map to one symbol (the reference's ls == hs)
-        it is committed, the predictor accepts it and the next is tried; otherwise
-        the registers stay as they were.  A new bit inside the value window of
-        the committed registers is added to x where it sits (it was read as 0)."""
-        return iter(self._step_bit(int(bit)))
+        The GPU decides; between calls the decoder's registers wait on the host
+        (include/lac.h lac_decode_get_state / set_state, lac_decode_tail_*).  In
+        the value form each call tries the next symbol against the bits so far,
+        zero-padded, and commits it only when the 0- and 1-padded ends of the
+        window agree (the reference's ls == hs); a bit inside the value window is
+        added to x where it was read as 0.  A window that leaves [l, h] moves the
+        session to the reference frame (l, h, lb, hb), where receive_bit is a
+        host-side halving and each decision one tail step."""
+        bit = int(bit)
+        if bit not in (0, 1):
+            raise ValueError("bits are 0 or 1")
+        if self._sess is None:
+            self._sess = _Session(self)
+        self._sess.add_bit(bit)
+        return self._sess.decide()
+
+    def flush(self):
+        """A_from_bin.flush (arith_code.py:300-317): while [l, h] is not inside the
+        received window, emit the straddled symbol of largest overlap ratio; then
+        the registers reset (the next bits start a new stream)."""
+        sess, self._sess = self._sess, None
+        if sess is None:
+            return                                  # fresh registers: [l, h] == [lb, hb], nothing to emit
+        try:
+            yield from sess.flush()
+        finally:
+            sess.close()
 
     def __call__(self, bit):
         if bit is None:
-            raise NotImplementedError("A_from_bin.flush (arith_code.py:300-317) is not provided: its heuristic "
-                                      "raises on about a fifth of valid streams (SURVEY.md finding 5)")
+            return tuple(self.flush())
         return tuple(self.step(bit))
 
-    def _step_bit(self, bit):
-        import torch
-        if bit not in (0, 1):
-            raise ValueError("bits are 0 or 1")
-        if not hasattr(self, "_sbits"):
-            self._sbits = []
-            self._stab = _Tables(self.predictor)
-            self._scoder = None
-            self._sstate = np.zeros(1, dtype=self._DEC_STATE)
-            self._sstate["h"] = self.denom - 1
-            self._sstate["pos"] = self.precision
-            self._sstate["det"] = 1
-            self._sstate["err_step"] = -1
-            self._sbuf = np.zeros(64, dtype=np.uint8)        # packed bits, MSB first (host copy)
-            self._sdev = None                                # its device copy, re-sent when it grows
-        if (len(self._sbits) >> 3) + 8 >= len(self._sbuf):
-            self._sbuf = np.concatenate([self._sbuf, np.zeros(len(self._sbuf), dtype=np.uint8)])
-            self._sdev = None
-        n = len(self._sbits)
-        self._sbits.append(bit)
-        if bit:
-            self._sbuf[n >> 3] |= 0x80 >> (n & 7)
-        st = self._sstate
-        pos = int(st["pos"][0])
-        if bit and pos - self.precision <= n < pos:          # was read as a padding 0
-            st["x"] += 1 << (pos - 1 - n)
-        out = []
-        while True:
-            row = self._stab.row()
-            V = len(row)
-            if self._scoder is None or self._scoder.vocab != V:
-                if self._scoder is not None:
-                    self._scoder.close()
-                self._scoder = BatchCoder(V, 1, prec=self.precision, pmf_bits=64, capacity_bits=64)
-                self._scoder.set_mapping(self._stab.mapping)
-            c = self._scoder
-            nb = len(self._sbits)
-            if self._sdev is None or self._sdev.device != c.device:
-                self._sdev = torch.from_numpy(self._sbuf.reshape(1, -1)).to(c.device)
-                self._snb = torch.zeros(1, dtype=torch.int64, device=c.device)
-            else:                                        # only the byte the new bit went into
-                self._sdev[0, n >> 3] = int(self._sbuf[n >> 3])
-            self._snb.fill_(nb)
-            c.decode_open(self._sdev, self._snb)
-            trial = st.copy()
-            trial["det"] = 1
-            trial["ndet"] = 0
-            check(c.lib.lac_decode_set_state(c.ctx, trial.ctypes.data_as(C.c_void_p), c._stream))
-            pmf = torch.from_numpy(row.view(np.int64).reshape(1, 1, V)).to(c.device)
-            s = int(c.decode(pmf).cpu()[0, 0])
-            new = np.zeros(1, dtype=self._DEC_STATE)
-            check(c.lib.lac_decode_get_state(c.ctx, new.ctypes.data_as(C.c_void_p), c._stream))
-            # not determined by the bits so far -- or not decodable from them yet: the
-            # 0-padded window can fall below l (the reference's lb - l < 0 then maps
-            # the two ends to different symbols and it emits nothing either)
-            if int(new["err"][0]) or int(new["ndet"][0]) != 1:
-                break
-            st = new
-            out.append(s)
-            self.predictor.accept(s)
-        self._sstate = st
-        return out
-
     def decode(self, bits, length, stop=1, n=None):
-        """A_from_bin.decode(int, length) -- arith_code.py:327-334."""
+        """A_from_bin.decode(int, length, stop) -- arith_code.py:327-334 (run over
+        the length bits of ``bits``, MSB first; with stop, the flush and a second,
+        idle one)."""
         bl = [(bits >> (length - 1 - i)) & 1 for i in range(length)]
-        return self.run(bl, stop, n)
+        if n is not None:
+            return self.run(bl, stop, n)
+        return self._decode_gen(bl, stop)
+
+    def _decode_gen(self, bl, stop):
+        yield from self._run(bl, stop, 1 << 24)
+        if stop:
+            yield from self.flush()
 
     def _decode_bytes(self, data, nbits, n, max_symbols=1 << 24):
         import torch

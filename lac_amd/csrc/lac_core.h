@@ -216,6 +216,39 @@ __host__ __device__ inline int64_t overlap(int64_t a, int64_t b, int64_t c, int6
     return r > 0 ? r : 0;
 }
 
+// Python's `a / b` for ints 0 <= a <= b, 0 < b < 2^63: the double nearest the
+// exact quotient, ties to even (CPython divides ints with correct rounding).
+// A_from_bin.flush ranks its candidate symbols by such quotients
+// (arith_code.py:305-307, :312), so the ranking -- ties included -- needs the
+// same double.  Operands below 2^53 convert exactly and the IEEE divide rounds
+// correctly; larger ones take an exact integer quotient with 55-56 significant
+// bits plus a sticky remainder, rounded here to 53.
+__host__ __device__ inline int bitlen_u128(u128 x) {
+    const uint64_t hi = (uint64_t)(x >> 64);
+    return hi ? 64 + bitlen64(hi) : bitlen64((uint64_t)x);
+}
+__host__ __device__ inline double cr_ratio(uint64_t a, uint64_t b) {
+    if (a == 0) return 0.0;
+    if (a == b) return 1.0;
+    if (a < (1ull << 53) && b < (1ull << 53)) return (double)a / (double)b;
+    const int s = 55 + bitlen64(b) - bitlen64(a);        // quotient a*2^s/b in (2^54, 2^56)
+    const u128 N = (u128)a << s;
+    const u128 Q = N / b;
+    const bool sticky = (N - Q * b) != 0;
+    const int drop = bitlen_u128(Q) - 53;                  // 2 or 3
+    uint64_t m = (uint64_t)(Q >> drop);
+    const uint64_t rest = (uint64_t)Q & ((1ull << drop) - 1), half = 1ull << (drop - 1);
+    if (rest > half || (rest == half && (sticky || (m & 1)))) m += 1;
+    return ldexp((double)m, drop - s);                     // m <= 2^53: exact
+}
+
+// Python's a // b (floor) for a signed 128-bit numerator and b > 0.
+__host__ __device__ inline i128 floordiv_i128(i128 a, uint64_t b) {
+    if (a >= 0) return (i128)((u128)a / b);
+    const u128 m = (u128)(-a);
+    return -(i128)((m + b - 1) / b);
+}
+
 // A_to_bin.flush (arith_code.py:193-202), literal.  Returns the digit count (<= 8
 // in practice: <= 2 observed), digits may be -1..3.  Returns -1 on overrun.
 __host__ __device__ inline int flush_digits(int64_t l, int64_t h, int prec, int8_t *out) {

@@ -2826,6 +2826,8 @@ __global__ __launch_bounds__(256) void k_quantize_logits(const LT *__restrict__ 
     }
 }
 
+#include "lac_tail.h"
+
 }  // namespace
 
 // ====================================================================== C-ABI
@@ -2836,6 +2838,7 @@ struct lac_ctx {
     RowStats *stats = nullptr;
     EncState *enc = nullptr;
     DecState *dec = nullptr;
+    TailState *tail = nullptr;          // decoder tail in the reference frame (lac_decode_tail_*)
     uint64_t *planeA = nullptr, *planeC = nullptr, *nbits = nullptr;
     const uint8_t *dbits = nullptr;
     uint64_t dstride = 0;
@@ -3493,6 +3496,7 @@ int lac_close(lac_ctx *c) {
     (void)hipFree(c->stats);
     (void)hipFree(c->enc);
     (void)hipFree(c->dec);
+    (void)hipFree(c->tail);
     (void)hipFree(c->planeA);
     (void)hipFree(c->planeC);
     (void)hipFree(c->nbits);
@@ -3720,13 +3724,14 @@ int lac_decode_get_state(lac_ctx *c, lac_dec_state *host_out, void *stream) {
 int lac_decode_set_state(lac_ctx *c, const lac_dec_state *host_in, void *stream) {
     if (!c || !host_in) return fail(LAC_E_ARG, "NULL argument");
     if (c->mode != 1) return fail(LAC_E_STATE, "call lac_decode_open first");
-    // only register sets a decoder can reach: 0 <= l < 2^prec, l <= h, h - l < 2^prec,
-    // pos >= prec (the kernels check x against [l, h] themselves)
+    // only register sets a decoder can reach: 0 <= l < 2^(prec+1) (A_to_bin's l stays below
+    // 2*denom, SURVEY finding 9), l <= h, h - l < 2^prec, pos >= prec (the kernels check x
+    // against [l, h] themselves)
     const int64_t D = (int64_t)1 << c->prec;
     for (int64_t b = 0; b < c->B; b++) {
         const lac_dec_state &q = host_in[b];
         if (q.err) continue;
-        if (q.l < 0 || q.l >= D || q.h < q.l || q.h - q.l >= D || q.pos < (uint64_t)c->prec ||
+        if (q.l < 0 || q.l >= 2 * D || q.h < q.l || q.h - q.l >= D || q.pos < (uint64_t)c->prec ||
             q.pos > ((uint64_t)1 << 60) || q.nsym < 0 || q.ndet < 0 || (q.det != 0 && q.det != 1))
             return fail(LAC_E_ARG, "stream %lld: decoder registers out of range", (long long)b);
     }
@@ -3832,6 +3837,68 @@ int lac_decode_determined(lac_ctx *c, int64_t *ndet_host, void *stream) {
     std::vector<DecState> v(c->B);
     HIPCHK(hipMemcpy(v.data(), c->dec, sizeof(DecState) * c->B, hipMemcpyDeviceToHost));
     for (int64_t b = 0; b < c->B; b++) ndet_host[b] = v[b].ndet;
+    return LAC_OK;
+}
+
+int lac_decode_tail_begin(lac_ctx *c, void *stream) {
+    if (!c) return fail(LAC_E_ARG, "ctx is NULL");
+    if (c->mode != 1) return fail(LAC_E_STATE, "call lac_decode_open first");
+    HIPCHK(hipSetDevice(c->device));
+    if (!c->tail) HIPCHK(hipMalloc(&c->tail, sizeof(TailState) * c->B));
+    k_decode_tail_begin<<<(unsigned)((c->B + 255) / 256), 256, 0, S(stream)>>>(c->dec, c->dnbits, c->B, c->prec,
+                                                                               c->tail);
+    CHECK_LAUNCH();
+    return LAC_OK;
+}
+
+int lac_decode_tail_step(lac_ctx *c, const void *pmf_dev, int64_t stream_stride, int mode, int64_t *sym_out_dev,
+                         int32_t *code_out_dev, void *stream) {
+    if (!c || !sym_out_dev || !code_out_dev) return fail(LAC_E_ARG, "NULL argument");
+    if (!c->tail) return fail(LAC_E_STATE, "call lac_decode_tail_begin (or lac_decode_tail_set_state) first");
+    if (mode != LAC_TAIL_DECIDE && mode != LAC_TAIL_FLUSH) return fail(LAC_E_ARG, "bad tail mode %d", mode);
+    if (c->mapping == LAC_MAP_CEIL && !pmf_dev) return fail(LAC_E_ARG, "pmf_dev is NULL");
+    if (stream_stride < 0) return fail(LAC_E_ARG, "negative stride");
+    HIPCHK(hipSetDevice(c->device));
+    const int m = mode == LAC_TAIL_DECIDE ? kTailDecide : kTailFlush;
+    if (c->pmf_bits == 32)
+        k_decode_tail<uint32_t><<<(unsigned)c->B, kTailThreads, 0, S(stream)>>>(
+            (const uint32_t *)pmf_dev, stream_stride, c->V, c->prec, c->mapping, m, c->tail, sym_out_dev, code_out_dev);
+    else
+        k_decode_tail<uint64_t><<<(unsigned)c->B, kTailThreads, 0, S(stream)>>>(
+            (const uint64_t *)pmf_dev, stream_stride, c->V, c->prec, c->mapping, m, c->tail, sym_out_dev, code_out_dev);
+    CHECK_LAUNCH();
+    return LAC_OK;
+}
+
+static_assert(sizeof(lac_tail_state) == sizeof(TailState) && offsetof(lac_tail_state, err) == offsetof(TailState, err) &&
+                  offsetof(lac_tail_state, nsym) == offsetof(TailState, nsym),
+              "lac_tail_state mirrors TailState");
+
+int lac_decode_tail_get_state(lac_ctx *c, lac_tail_state *host_out, void *stream) {
+    if (!c || !host_out) return fail(LAC_E_ARG, "NULL argument");
+    if (!c->tail) return fail(LAC_E_STATE, "no tail state: call lac_decode_tail_begin first");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemcpyAsync(host_out, c->tail, sizeof(TailState) * c->B, hipMemcpyDeviceToHost, S(stream)));
+    HIPCHK(hipStreamSynchronize(S(stream)));
+    return LAC_OK;
+}
+
+int lac_decode_tail_set_state(lac_ctx *c, const lac_tail_state *host_in, void *stream) {
+    if (!c || !host_in) return fail(LAC_E_ARG, "NULL argument");
+    // registers any A_from_bin holds: l <= h, lb <= hb, all within +-2^62 (the flush
+    // lets l fall below 0 and h, hb exceed 2^prec; 2^62 leaves the arithmetic room)
+    const int64_t lim = (int64_t)1 << 62;
+    for (int64_t b = 0; b < c->B; b++) {
+        const lac_tail_state &q = host_in[b];
+        if (q.err) continue;
+        if (q.h < q.l || q.hb < q.lb || q.l <= -lim || q.h >= lim || q.lb <= -lim || q.hb >= lim || q.still < 0 ||
+            q.nsym < 0 || (q.done != 0 && q.done != 1))
+            return fail(LAC_E_ARG, "stream %lld: tail registers out of range", (long long)b);
+    }
+    HIPCHK(hipSetDevice(c->device));
+    if (!c->tail) HIPCHK(hipMalloc(&c->tail, sizeof(TailState) * c->B));
+    HIPCHK(hipMemcpyAsync(c->tail, host_in, sizeof(TailState) * c->B, hipMemcpyHostToDevice, S(stream)));
+    HIPCHK(hipStreamSynchronize(S(stream)));
     return LAC_OK;
 }
 

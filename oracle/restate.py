@@ -206,6 +206,99 @@ def decode_bitserial(rows, bits, prec, counts=None):
     return out
 
 
+class _Uniform:
+    """Predictor(n): floor mapping, no table (arith_code.py:64-74)."""
+
+    def __init__(self, n):
+        self.n = n
+
+    def val_to_symbol(self, v, denom):
+        return (v * self.n) // denom
+
+    def symbol_to_range(self, s, denom):
+        return (s * denom) // self.n, ((s + 1) * denom) // self.n
+
+
+class _Table:
+    """CDFPredictor over replayed rows: step i uses rows[min(i, len-1)]."""
+
+    def __init__(self, rows):
+        self.R = _Rows(rows)
+        self.i = 0
+
+    def val_to_symbol(self, v, denom):
+        cdf, minp = self.R.get(self.i)
+        return val_to_symbol(cdf, minp, v, denom)
+
+    def symbol_to_range(self, s, denom):
+        cdf, minp = self.R.get(self.i)
+        return symbol_to_range(cdf, minp, s, denom)
+
+
+def decode_run(rows, bits, prec, stop=1, uniform=None):
+    """A_from_bin.run(bits, stop) restated as a generator -- arith_code.py:248-326:
+    the bit-serial decoder of :264-299, then (stop) flush (:300-317), which picks
+    among the symbols the window [lb, hb] straddles the one of largest overlap
+    ratio (a Python float, ties to the first) and emits it without renormalising,
+    until [l, h] lies inside [lb, hb].  Exceptions and partial output are the
+    reference's: AssertionError('unknown symbol', V), ZeroDivisionError for a
+    zero-width candidate, AssertionError from emit_symbol's overlap check.
+    ``uniform=n`` decodes with Predictor(n) instead of the table rows."""
+    P = _Uniform(uniform) if uniform else _Table(rows)
+    denom, decision = 1 << prec, 1 << (prec - 1)
+    st = {"l": 0, "h": denom - 1, "lb": 0, "hb": denom - 1}
+
+    def emit_symbol(s):                               # :274-283
+        r = P.symbol_to_range(s, st["h"] - st["l"] + 1)
+        if region_overlap(st["l"] + r[0], st["l"] + r[1] - 1, st["lb"], st["hb"]) == 0:
+            raise AssertionError("predictor range does not correspond to val")
+        st["h"] = st["l"] + r[1] - 1
+        st["l"] += r[0]
+        if not uniform:
+            P.i += 1
+        return s
+
+    for bit in bits:
+        wb = (st["hb"] - st["lb"] + 1) // 2           # receive_bit :264-267
+        st["lb"] += wb * bit
+        st["hb"] = st["lb"] + wb - 1
+        while True:
+            w = st["h"] - st["l"] + 1                 # decide_symbol :268-273
+            ls = P.val_to_symbol(st["lb"] - st["l"], w)
+            hs = P.val_to_symbol(st["hb"] - st["l"], w)
+            if ls != hs:
+                break
+            s = emit_symbol(ls)
+            while st["h"] - st["l"] < decision:       # emit_bit :284-291
+                d = st["l"] // decision
+                st["l"] = st["l"] * 2 - d * denom
+                st["h"] = st["h"] * 2 + 1 - d * denom
+                st["lb"] = st["lb"] * 2 - d * denom
+                st["hb"] = st["hb"] * 2 + 1 - d * denom
+            yield s
+    if not stop:
+        return
+
+    def k(s):                                         # :305-307
+        r = P.symbol_to_range(s, st["h"] - st["l"] + 1)
+        return region_overlap(st["lb"] - st["l"], st["hb"] - st["l"], r[0], r[1] - 1) / (r[1] - r[0])
+
+    still = 0
+    while not (st["lb"] <= st["l"] and st["h"] <= st["hb"]):   # :308-313
+        w = st["h"] - st["l"] + 1
+        ls = P.val_to_symbol(st["lb"] - st["l"], w)
+        hs = P.val_to_symbol(st["hb"] - st["l"], w)
+        before = (st["l"], st["h"])
+        yield emit_symbol(max(range(ls, hs + 1), key=k))
+        still = still + 1 if (st["l"], st["h"]) == before else 0
+        if still >= FLUSH_STILL_LIMIT:                # a full-range symbol: the reference loops forever
+            raise RuntimeError("flush does not terminate")
+    st.update(l=0, h=denom - 1, lb=0, hb=denom - 1)
+
+
+FLUSH_STILL_LIMIT = 1000
+
+
 def decode_value(rows, data_bits, nsym, prec):
     """Value-register decoder, n symbols out.
 

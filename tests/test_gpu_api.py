@@ -408,6 +408,29 @@ def test_run_then_steps_then_long_run_without_flush():
     assert got == restate.encode_digits([pmf.tolist()], syms, prec)
 
 
+def test_silent_step_then_long_run_keeps_registers():
+    """step() on a symbol of p > 1/2 narrows l, h without emitting a digit; a
+    following run() longer than the first coder's capacity must continue those
+    registers, not reallocate from l = 0."""
+    from lac_amd.coder import AC, CDFPredictor
+    from oracle import restate
+    rng = np.random.default_rng(12)
+    pmf = np.array([900] + rng.integers(1, 20, 15).tolist(), dtype=np.uint64)
+    syms = [0] + rng.choice(16, size=3000, p=pmf / pmf.sum()).tolist()
+    prec = 16
+    enc = AC(CDFPredictor(np.cumsum(pmf).tolist()), prec).to_bin
+    first = list(enc.step(0))
+    assert first == [] and (enc.l, enc.h) != (0, (1 << prec) - 1)
+    got = first + list(enc.run(syms[1:], stop=1))
+    assert got == restate.encode_digits([pmf.tolist()], syms, prec)
+    # a table-size change after a silent step is refused (the registers are live)
+    enc = AC(CDFPredictor(np.cumsum(pmf).tolist()), prec).to_bin
+    list(enc.step(0))
+    enc.predictor = CDFPredictor(list(range(1, 9)))
+    with pytest.raises(RuntimeError):
+        list(enc.step(1))
+
+
 def test_batch_decode_rejects_bad_shapes():
     """BatchCoder.decode / decode_open validate tables, outputs and bit buffers
     instead of letting the kernels read or write out of bounds."""

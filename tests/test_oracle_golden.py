@@ -160,3 +160,19 @@ def test_bitserial_restatement_per_bit_counts():
         counts = []
         assert restate.decode_bitserial(rows, bits, case["prec"], counts) == case["syms"], case["src"]
         assert counts == case["counts"], case["src"]
+
+
+def test_restated_flush_matches_reference():
+    """oracle.restate.decode_run (A_from_bin.run(bits, stop=1) restated, flush
+    included) == the reference on 2180 recorded cases: whole streams, prefixes,
+    flipped bits, uniform Predictor(n), V up to 32000; symbols and exceptions."""
+    import flush_util
+    gen = {c["name"]: c for c in GEN}
+    n = 0
+    for c in flush_util.cases():
+        rows = flush_util.rows_for(c, SMALL, gen)
+        got = flush_util.drain(restate.decode_run(rows, flush_util.bits_for(c), c["prec"], 1,
+                                                  uniform=c.get("uniform")))
+        assert got == (c["out"], c["exc"]), (c["src"], c["variant"])
+        n += 1
+    assert n > 2000
