@@ -24,12 +24,15 @@ from .coder import ProbPredictor
 
 
 def quantise_logits(logits) -> np.ndarray:
-    """logits -> inclusive int64 CDF, the reference's quantiser (llama_compress.py:24-30):
-    exp, normalise, scale by 2^60, clip at 2, float64 running sum, truncate."""
-    pdf = np.exp(np.asarray(logits, dtype=np.float64))
+    """logits -> inclusive int64 CDF, the reference's quantiser (llama_compress.py:24-30),
+    the same numpy operations in the same order and dtypes: exp and normalise in the
+    logits' own dtype (float32 for llama.cpp's scores), scale by the Python int
+    2^60 (a weak scalar: the product keeps that dtype), widen to float64, clip at 2,
+    float64 running sum, truncate to int64.  Pinned to the reference by
+    tests/golden/llama_cases.json (tests/test_llama_host.py)."""
+    pdf = np.exp(logits)
     pdf /= np.sum(pdf)
-    scaled = np.clip((pdf * float(1 << 60)).astype(float), 2, None)
-    return np.cumsum(scaled).astype(np.int64)
+    return np.cumsum(np.clip((pdf * (1 << 60)).astype(float), 2, None)).astype(np.int64)
 
 
 class Llama_AC(ProbPredictor):

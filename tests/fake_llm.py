@@ -1,0 +1,28 @@
+"""A duck-typed stand-in for llama_cpp.Llama: reset(),
+eval(tokens), n_ctx() and _scores, whose last row -- the next-token logits --
+is a seeded float32 function of the context window.  Used to drive the
+reference's Llama_AC (tools/gen_golden_llama.py) and this build's
+lac_amd.llm.Llama_AC (tests) with identical logits."""
+import numpy as np
+
+
+class FakeLlama:
+    def __init__(self, vocab, n_ctx, seed, scale=3.0):
+        self.vocab, self._n_ctx, self.seed, self.scale = vocab, n_ctx, seed, scale
+        self.toks = []
+        self._scores = None
+
+    def n_ctx(self):
+        return self._n_ctx
+
+    def reset(self):
+        self.toks = []
+        self._scores = None
+
+    def eval(self, tokens):
+        self.toks.extend(int(t) for t in tokens)
+        h = self.seed
+        for t in self.toks[-self._n_ctx:]:
+            h = (h * 1000003 + t + 1) % (1 << 61)
+        logits = (np.random.default_rng(h).standard_normal(self.vocab) * self.scale).astype(np.float32)
+        self._scores = logits[None, :]

@@ -138,8 +138,8 @@ def test_bit_serial_step_matches_reference():
     # lac_decode_set_state refuses registers no decoder reaches (nothing is copied)
     import ctypes as C
     from lac_amd._lib import LacError, check
-    c = dec._scoder
-    st = dec._sstate.copy()
+    c = dec._sess.coder
+    st = dec._sess.st.copy()
     for field, bad in (("l", -1), ("h", -5), ("pos", 3)):
         b = st.copy()
         b[field] = bad
@@ -345,14 +345,20 @@ def test_logits_compressor_vocab_not_a_multiple_of_8():
         assert pad_logits(raw).shape[-1] == lc.vcode
 
 
-def test_quantiser_matches_reference_numpy_ops():
-    """quantise_logits is the reference's float64 numpy quantiser (llama_compress.py:24-30)."""
-    from lac_amd.llm import quantise_logits
-    logits = np.random.default_rng(3).standard_normal(1000).astype(np.float32) * 3
-    pdf = np.exp(logits.astype(np.float64))
-    pdf /= np.sum(pdf)
-    want = np.cumsum(np.clip((pdf * (1 << 60)).astype(float), 2, None)).astype(int)
-    assert (quantise_logits(logits) == want).all()
+@pytest.mark.parametrize("case", load_golden("llama_cases.json")["cases"], ids=lambda c: c["name"])
+def test_llama_ac_bits_match_reference_fixture(case):
+    """AC(lac_amd Llama_AC(llm), 48) on the GPU == the reference's A_to_bin on the
+    CDFs the reference's own Llama_AC computed (exact ints), for a fake llm whose
+    sliding window wraps (tests/golden/llama_cases.json, tools/gen_golden_llama.py);
+    the decoder returns the tokens."""
+    from fake_llm import FakeLlama
+    from lac_amd.coder import AC, group_bits
+    from lac_amd.llm import Llama_AC
+    llm = FakeLlama(case["vocab"], case["n_ctx"], case["seed"])
+    ac = AC(Llama_AC(llm), case["prec"])
+    bits = list(ac.to_bin.bits(case["tokens"]))
+    assert len(bits) == case["exact_L"] and bytes(group_bits(iter(bits))).hex() == case["exact_bytes"]
+    assert list(ac.from_bin.run(bits, stop=0, n=len(case["tokens"]))) == case["tokens"]
 
 
 def _static_case(V=300, n=10000, seed=7):

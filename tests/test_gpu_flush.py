@@ -86,21 +86,32 @@ def test_decode_R_L_matches_reference():
         assert got == (c["decode_out"], c["decode_exc"]), c["src"]
 
 
-def test_step_then_call_none_matches_reference():
-    """The bit-serial form: step(bit) / __call__(bit) over every bit, then
-    __call__(None) (arith_code.py:318-321) -- the same symbols and exception."""
+def test_step_then_flush_matches_reference():
+    """The bit-serial form: step(bit) / __call__(bit) over every bit, then the
+    flush as flush() (a generator: symbols before an exception are seen) or as
+    __call__(None) (arith_code.py:318-321: tuple(flush()), which loses them when
+    the flush raises, in the reference as here)."""
     from lac_amd.coder import AC
     cases = [c for i, c in enumerate(flush_util.cases()) if i % 7 == 0 and c["nbits"] <= 400]
     assert len(cases) > 200
-    for c in cases:
+    for k, c in enumerate(cases):
         dec = AC(_predictor(c), c["prec"]).from_bin
+        head = []
 
         def gen():
             for i, b in enumerate(flush_util.bits_for(c)):
-                yield from (dec(b) if i % 2 else dec.step(b))
-            yield from dec(None)
+                out = dec(b) if i % 2 else tuple(dec.step(b))
+                head.extend(out)
+                yield from out
+            if k % 2:
+                yield from dec.flush()
+            else:
+                yield from dec(None)
         got = flush_util.drain(gen())
-        assert got == (c["out"], c["exc"]), (c["src"], c["variant"])
+        if k % 2 or c["exc"] is None:
+            assert got == (c["out"], c["exc"]), (c["src"], c["variant"])
+        else:
+            assert got[1] == c["exc"] and got[0] == head and c["out"][:len(head)] == head, c["src"]
 
 
 def test_run_stop0_then_run_continues_and_flush_resets():

@@ -1,0 +1,53 @@
+"""The caller-side quantiser pinned to the reference.
+
+tests/golden/llama_cases.json records what the reference's own Llama_AC
+(llama_compress.py:14-61) computes when driven by tests/fake_llm.py: per step
+the logits, the int64 CDF of calc_dist (:24-30), minp (:43-45) and the sliding
+window (:31-39), and the exact-int A_to_bin bits on those CDFs
+(tools/gen_golden_llama.py).  lac_amd.llm.Llama_AC must reproduce all of it.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+from conftest import load_golden
+from fake_llm import FakeLlama
+
+CASES = load_golden("llama_cases.json")["cases"]
+
+
+def _sha(b):
+    return hashlib.sha256(b).hexdigest()
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_llama_ac_tables_match_reference(case):
+    from lac_amd.llm import Llama_AC, quantise_logits
+    llm = FakeLlama(case["vocab"], case["n_ctx"], case["seed"])
+    p = Llama_AC(llm)
+    for i, (t, want) in enumerate(zip(case["tokens"], case["steps"])):
+        logits = np.asarray(llm._scores[-1], dtype=np.float32)
+        assert _sha(logits.tobytes()) == want["logits_sha256"], i
+        cdf = p.dist
+        assert _sha(np.asarray(cdf, dtype="<i8").tobytes()) == want["cdf_sha256"], i
+        assert _sha(np.asarray(quantise_logits(logits), dtype="<i8").tobytes()) == want["cdf_sha256"], i
+        assert p.minp == want["minp"] and len(p.past) == want["window"], i
+        if "cdf" in want:
+            assert [int(x) for x in cdf] == want["cdf"], i
+        p.accept(t)
+    assert max(s["window"] for s in case["steps"]) == case["n_ctx"] - 1     # the window wrapped
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_oracle_exact_bits_on_reference_tables(case):
+    """The oracle, on the CDFs this adapter yields, gives the reference's exact-int bits."""
+    from lac_amd.llm import Llama_AC
+    from oracle import restate
+    p = Llama_AC(FakeLlama(case["vocab"], case["n_ctx"], case["seed"]))
+    rows = []
+    for t in case["tokens"]:
+        rows.append([int(x) for x in p.pmf_row()])
+        p.accept(t)
+    data, L = restate.encode_bytes(rows, case["tokens"], case["prec"])
+    assert L == case["exact_L"] and data.hex() == case["exact_bytes"]
