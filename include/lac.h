@@ -331,6 +331,25 @@ int lac_decode_tail_step(lac_ctx *ctx, const void *pmf_dev, int64_t stream_strid
 int lac_decode_tail_get_state(lac_ctx *ctx, lac_tail_state *host_out, void *stream);
 int lac_decode_tail_set_state(lac_ctx *ctx, const lac_tail_state *host_in, void *stream);
 
+/* ---- predictor-mapped coding (host, no device work) ----------------------------
+ * A predictor whose symbol_to_range / val_to_symbol are its own code (the
+ * reference's toy Predictor subclasses, e.g. ModifiedMarkov arith_code.py:468-522)
+ * has no table for the GPU: its caller evaluates the mapping and these functions
+ * do the coder's register arithmetic.  Registers stay within +-2^62 (LAC_E_ARG
+ * otherwise); prec in [2, 61].
+ *   lac_hc_encode_symbol  receive_symbol's narrowing to [l+lo, l+hi-1] plus the
+ *                         decide_bit / emit_bit loop (arith_code.py:169-186):
+ *                         the digits emitted (<= 64, int8); lo >= hi is
+ *                         LAC_E_ZERO_WIDTH (the reference loops forever)
+ *   lac_hc_encode_flush   A_to_bin.flush (:193-202): its digits
+ *   lac_hc_decode_emit    emit_symbol (:274-283) on regs = {l, h, lb, hb}
+ *                         (LAC_E_DECODE_RANGE when the range misses [lb, hb]),
+ *                         then, if renormalise, the emit_bit loop (:284-291) */
+int lac_hc_encode_symbol(int prec, int64_t *l, int64_t *h, int64_t lo, int64_t hi, int8_t *digits,
+                         int32_t *ndigits);
+int lac_hc_encode_flush(int prec, int64_t l, int64_t h, int8_t *digits, int32_t *ndigits);
+int lac_hc_decode_emit(int prec, int64_t *regs, int64_t lo, int64_t hi, int renormalise);
+
 /* Live kernel timing: with profiling on, every kernel launch is bracketed by
  * hipEvents recorded on its own stream.  lac_profile_read synchronises and
  * returns, per kernel id (0 row_stats, 1 encode, 2 finish, 3 decode_step,

@@ -65,6 +65,9 @@ PROTOTYPES = [
     ("lac_decode_tail_step", _i, [_vp, _vp, _i64, _i, _vp, _vp, _vp]),
     ("lac_decode_tail_get_state", _i, [_vp, _vp, _vp]),
     ("lac_decode_tail_set_state", _i, [_vp, _vp, _vp]),
+    ("lac_hc_encode_symbol", _i, [_i, _vp, _vp, _i64, _i64, _vp, _vp]),
+    ("lac_hc_encode_flush", _i, [_i, _i64, _i64, _vp, _vp]),
+    ("lac_hc_decode_emit", _i, [_i, _vp, _i64, _i64, _i]),
     ("lac_profile_enable", _i, [_vp, _i]),
     ("lac_profile_read", _i, [_vp, _vp, _vp, _i]),
     ("lac_q1_k", _i, [_i, _i64]),

@@ -14,11 +14,14 @@ Drop-in counterparts of /root/reference/arith_code.py:
 
 The predictor classes keep the reference's arithmetic so that third-party
 subclasses (History, Markov, an LLM adapter overriding ``calc_dist``) keep
-working, but the coders never call ``symbol_to_range``/``val_to_symbol``: they
-hand each step's integer pmf row (from ``predictor.dist``) to liblac.so, whose
-kernels implement exactly that arithmetic on the device.  A ``Predictor`` that
-is not table-based (custom ``symbol_to_range`` with no ``dist``) is rejected with
-TypeError: there is no CPU coder behind this API.
+working.  For them the coders never call ``symbol_to_range``/``val_to_symbol``:
+they hand each step's integer pmf row (from ``predictor.dist``) to liblac.so,
+whose kernels implement exactly that arithmetic on the device.  A predictor
+whose mapping is its own code (``mapping_of`` == 'mapped': overridden
+``symbol_to_range`` / ``val_to_symbol`` / ``fudged_dist``, e.g. the reference's
+ModifiedMarkov) has no table to scan; ``AC`` gives it the coders of
+lac_amd.mapped, which call its methods where the reference does and do the
+register arithmetic in liblac's host functions.
 
 Coding one symbol at a time through ``step`` is correct but launch-bound; use
 ``run``/``bits``/``encode`` (one launch for the whole sequence) or the batched
@@ -37,6 +40,7 @@ import numpy as np
 from . import _lib
 from ._lib import check
 from .batch import BatchCoder, digits_of
+from .mapped import MappedDecoderMixin, MappedEncoderMixin
 
 
 def region_overlap(a, b, c, d):
@@ -162,13 +166,52 @@ def _row_of(predictor):
     return np.array([int(x) for x in pmf], dtype=np.uint64)
 
 
+_REF_MODULES = ("lac_amd.coder", "arith_code")          # this module and the reference's own
+
+
+def _impl(predictor, name):
+    """(qualname, module) of the function ``type(predictor).<name>`` resolves to."""
+    f = getattr(type(predictor), name, None)
+    return getattr(f, "__qualname__", None), getattr(f, "__module__", None)
+
+
 def _is_uniform(predictor):
     """A table-less Predictor(n) with the base class's floor mapping (arith_code.py:64-74)."""
     if getattr(predictor, "dist", None) is not None or not hasattr(predictor, "n"):
         return False
-    stv = getattr(type(predictor), "symbol_to_range", None)
-    return stv is Predictor.symbol_to_range or (type(predictor).__name__ == "Predictor"
-                                                 and type(predictor).__module__ != __name__)
+    return all(_impl(predictor, m) in ((f"Predictor.{m}", mod) for mod in _REF_MODULES)
+               for m in ("symbol_to_range", "val_to_symbol"))
+
+
+def _is_table(predictor):
+    """A predictor whose mapping is CDFPredictor's over its ``dist`` (arith_code.py:83-110):
+    symbol_to_range, val_to_symbol and fudged_dist not overridden.  The reference's
+    Llama_AC (llama_compress.py:46-61) restates the first two on numpy arrays; on
+    exact integers -- the parity contract, SURVEY.md finding 3 -- they are
+    CDFPredictor's, so it counts as a table predictor too."""
+    for m in ("symbol_to_range", "val_to_symbol", "fudged_dist"):
+        q, mod = _impl(predictor, m)
+        if (q, mod) in ((f"CDFPredictor.{m}", x) for x in _REF_MODULES):
+            continue
+        if q == f"Llama_AC.{m}" and mod in ("llama_compress", "lac_amd.llm"):
+            continue
+        return False
+    return True
+
+
+def mapping_of(predictor):
+    """How AC codes this predictor: 'uniform' (Predictor(n): the floor mapping on the
+    GPU), 'table' (CDF tables: the GPU kernels) or 'mapped' (its own
+    symbol_to_range / val_to_symbol, evaluated in Python around liblac's host
+    register arithmetic, lac_amd.mapped)."""
+    if _is_uniform(predictor):
+        return "uniform"
+    if _is_table(predictor):
+        return "table"
+    if callable(getattr(predictor, "symbol_to_range", None)) and callable(getattr(predictor, "val_to_symbol", None)):
+        return "mapped"
+    raise TypeError(f"{type(predictor).__name__} is not a predictor: it needs symbol_to_range and val_to_symbol "
+                    "(arith_code.py:64-74) or a CDF table (.dist)")
 
 
 def _raise_for(code, sym=None):
@@ -193,12 +236,30 @@ class _Tables:
     def row(self):
         if self.uniform:
             return np.ones(int(self.p.n), dtype=np.uint64)
-        return _row_of(self.p)
+        r = _row_of(self.p)
+        # fudged_dist decides with the predictor's own minp (arith_code.py:84); the
+        # kernels take the row's smallest positive entry (:79-82): refuse a predictor
+        # whose minp says otherwise (a stale attribute, Llama_AC's zero-including
+        # minp on a row with zeros) instead of coding a different table
+        m = getattr(self.p, "minp", None)
+        if m is not None:
+            pos = r[r > 0]
+            if pos.size and int(m) != int(pos.min()):
+                raise ValueError(f"{type(self.p).__name__}.minp = {int(m)} but its table's smallest positive "
+                                 f"entry is {int(pos.min())}: the GPU coder derives minp from the table")
+        return r
 
 
 # ------------------------------------------------------------------ encoder
 class A_to_bin:
-    """Encoder (arith_code.py:156-246) backed by liblac.so (one stream)."""
+    """Encoder (arith_code.py:156-246) backed by liblac.so (one stream).  A
+    predictor with its own mapping (mapping_of == 'mapped') gets the
+    lac_amd.mapped encoder instead."""
+
+    def __new__(cls, predictor=ternary, prec=16):
+        if cls is A_to_bin and mapping_of(predictor) == "mapped":
+            return object.__new__(_MappedA_to_bin)
+        return object.__new__(cls)
 
     def __init__(self, predictor=ternary, prec=16):
         self.predictor = predictor
@@ -304,11 +365,27 @@ class A_to_bin:
     def step(self, symbol):
         tab = _Tables(self.predictor)
         row = tab.row()
+        if self.debug_log:                             # arith_code.py:170 (a truthy list, as there)
+            self.debug_log.append((self.l, self.h, "recv", symbol))
         digs, (rc, n_ok) = self._encode_rows([row], [symbol])
         if rc:
             _raise_for(rc, symbol)
+        if self.debug_log:
+            self._log_emits_back(digs[0])
         self.predictor.accept(symbol)
         yield from digs[0]
+
+    def _log_emits_back(self, digits):
+        """debug_log's (l, h, 'emit', d) entries (arith_code.py:182) of one symbol: the
+        registers before each emit_bit, recovered from the registers after the
+        symbol by inverting emit_bit (l = (l' + dD) / 2, h = (h' - 1 + dD) / 2)."""
+        l, h = self.l, self.h
+        before = []
+        for d in reversed(digits):
+            l, h = (l + d * self.denom) >> 1, (h - 1 + d * self.denom) >> 1
+            before.append((l, h))
+        for (l, h), d in zip(reversed(before), digits):
+            self.debug_log.append((l, h, "emit", d))
 
     def __call__(self, symbol):
         if symbol is None:
@@ -319,11 +396,16 @@ class A_to_bin:
         if self._coder is None:
             tab = _Tables(self.predictor)
             self._ensure(len(tab.row()), 0)
+        l, h = (self.l, self.h) if self.debug_log else (0, 0)
         self._coder.finish()
         rc, err, step = self._coder.status()
         if rc:
             _raise_for(rc)
         fd = self._coder.flush_digits()[0]
+        if self.debug_log:
+            for d in fd:
+                self.debug_log.append((l, h, "emit", d))
+                l, h = l * 2 - d * self.denom, h * 2 + 1 - d * self.denom
         self.emitted_bits += len(fd)
         yield from fd
         self._coder.reset()
@@ -342,6 +424,12 @@ class A_to_bin:
         return rows, syms
 
     def run(self, symbols, stop=1):
+        if self.debug_log:                             # per-symbol registers for the log
+            for sym in symbols:
+                yield from self.step(sym)
+            if stop:
+                yield from self.flush()
+            return
         rows, syms = self._collect(symbols)
         if syms:
             digs, (rc, n_ok) = self._encode_rows(rows, syms)
@@ -574,6 +662,11 @@ class A_from_bin:
     build's extension that decodes exactly n symbols (zero bits past the end).
     """
 
+    def __new__(cls, predictor=ternary, prec=16):
+        if cls is A_from_bin and mapping_of(predictor) == "mapped":
+            return object.__new__(_MappedA_from_bin)
+        return object.__new__(cls)
+
     def __init__(self, predictor=ternary, prec=16):
         self.predictor = predictor
         self.precision = prec
@@ -780,6 +873,16 @@ class A_from_bin:
         if coder is not None:
             coder.close()
         return out
+
+
+class _MappedA_to_bin(MappedEncoderMixin, A_to_bin):
+    def __init__(self, predictor=ternary, prec=16):
+        self._mapped_init(predictor, prec)
+
+
+class _MappedA_from_bin(MappedDecoderMixin, A_from_bin):
+    def __init__(self, predictor=ternary, prec=16):
+        self._mapped_init(predictor, prec)
 
 
 class AC:

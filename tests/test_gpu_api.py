@@ -437,6 +437,23 @@ def test_silent_step_then_long_run_keeps_registers():
         list(enc.step(1))
 
 
+def test_debug_log_matches_reference():
+    """A_to_bin.debug_log (arith_code.py:164, 170, 182) of the GPU coder: the
+    reference's (l, h, 'recv' | 'emit', x) entries for CDFPredictor encodes
+    (tests/golden/custom_cases.json table_logs, tools/gen_golden_custom.py)."""
+    from lac_amd.coder import AC, CDFPredictor
+    for c in load_golden("custom_cases.json")["table_logs"]:
+        enc = AC(CDFPredictor(c["cdf"]), c["prec"]).to_bin
+        enc.debug_log = ["start"]                    # logged only into a truthy list, as there
+        bits = list(enc.bits(c["syms"]))
+        assert "".join(map(str, bits)) == c["bits"]
+        assert [list(x) if isinstance(x, tuple) else x for x in enc.debug_log] == c["debug_log"]
+        enc = AC(CDFPredictor(c["cdf"]), c["prec"]).to_bin
+        enc.debug_log = []                           # falsy: nothing logged
+        list(enc.bits(c["syms"]))
+        assert enc.debug_log == []
+
+
 def test_batch_decode_rejects_bad_shapes():
     """BatchCoder.decode / decode_open validate tables, outputs and bit buffers
     instead of letting the kernels read or write out of bounds."""

@@ -1,0 +1,92 @@
+"""Predictors with their own mapping against the reference.
+
+tests/golden/custom_cases.json records what the reference coder does with the
+predictors of tests/custom_predictors.py (tools/gen_golden_custom.py): encoded
+bits, A_to_bin.debug_log, and A_from_bin.run(bits, stop=1 / 0) with its
+exception.  AC routes these predictors to lac_amd.mapped (their Python mapping
+around liblac's host register functions, no GPU needed), never to the table
+kernels; table predictors are refused when their minp disagrees with the table.
+"""
+import numpy as np
+import pytest
+
+import custom_predictors
+from conftest import load_golden
+
+DATA = load_golden("custom_cases.json")
+
+
+def _classes():
+    from lac_amd.coder import CDFPredictor, Predictor
+    return custom_predictors.make(Predictor, CDFPredictor)
+
+
+def _drain(gen):
+    out = []
+    try:
+        for v in gen:
+            out.append(int(v))
+    except Exception as e:                      # noqa: BLE001 -- compared with the recorded one
+        return out, [type(e).__name__, str(e.args[0]) if e.args else ""]
+    return out, None
+
+
+def test_dispatch_by_mapping():
+    from lac_amd import coder
+    from lac_amd.llm import Llama_AC
+    from lac_amd.mapped import MappedDecoderMixin, MappedEncoderMixin
+    Fixed, FloorCDF, Counting = _classes()
+    assert coder.mapping_of(coder.Predictor(3)) == "uniform"
+    assert coder.mapping_of(coder.CDFPredictor([1, 3, 4])) == "table"
+    assert coder.mapping_of(coder.ProbPredictor(5)) == "table"
+    assert coder.mapping_of(Llama_AC.__new__(Llama_AC)) == "table"
+    for p in (Fixed([1, 2, 3]), FloorCDF([1, 3, 4]), Counting(4)):
+        assert coder.mapping_of(p) == "mapped"
+        ac = coder.AC(p, 16)
+        assert isinstance(ac.to_bin, coder.A_to_bin) and isinstance(ac.to_bin, MappedEncoderMixin)
+        assert isinstance(ac.from_bin, coder.A_from_bin) and isinstance(ac.from_bin, MappedDecoderMixin)
+    with pytest.raises(TypeError):
+        coder.mapping_of(object())
+
+
+@pytest.mark.parametrize("i", range(len(DATA["cases"])))
+def test_mapped_coder_matches_reference(i):
+    from lac_amd.coder import AC
+    c = DATA["cases"][i]
+    cls = _classes()
+
+    def mk():
+        return custom_predictors.build(c["kind"], *cls, c["params"])
+    enc = AC(mk(), c["prec"]).to_bin
+    enc.debug_log = ["start"]
+    if "encode_exc" in c:                       # the reference loops forever on a zero-width range
+        assert c["encode_exc"] == "timeout"
+        with pytest.raises(AssertionError):
+            list(enc.bits(c["syms"]))
+        return
+    bits = list(enc.bits(c["syms"]))
+    assert "".join(map(str, bits)) == c["bits"]
+    assert [list(x) if isinstance(x, tuple) else x for x in enc.debug_log] == c["debug_log"]
+    for stop in (1, 0):
+        want = c[f"stop{stop}"]
+        got = _drain(AC(mk(), c["prec"]).from_bin.run(iter(bits), stop=stop))
+        assert [got[0], got[1]] == [want[0], want[1]], stop
+
+
+def test_table_predictor_with_stale_minp_is_refused():
+    """CDFPredictor's fudge test uses the predictor's minp (arith_code.py:84); a
+    subclass that swaps tables without updating it would be coded with another
+    decision by kernels that take minp from the table: refused, not silently coded."""
+    from lac_amd.coder import CDFPredictor, _Tables
+
+    class Swap(CDFPredictor):
+        def accept(self, s):
+            self.dist = [5, 8, 40]               # minp stays the first table's
+
+    p = Swap([2, 9, 10])
+    assert list(_Tables(p).row()) == [2, 7, 1]
+    p.accept(0)
+    with pytest.raises(ValueError):
+        _Tables(p).row()
+    p.minp = 3
+    assert list(_Tables(p).row()) == [5, 3, 32]
