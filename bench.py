@@ -49,6 +49,32 @@ def read_traffic(cfg, kernel):
     return None
 
 
+def host_cores():
+    """CPU threads for the cpu_baseline leg, as `nproc` counts them: the CPUs this
+    process may run on (sched_getaffinity), limited by OMP_NUM_THREADS /
+    OMP_THREAD_LIMIT when set (the GPU box sets them to its CPU share per GPU)."""
+    n = len(os.sched_getaffinity(0))
+    for var in ("OMP_NUM_THREADS", "OMP_THREAD_LIMIT"):
+        try:
+            v = int(os.environ.get(var, "").split(",")[0])
+        except ValueError:
+            continue
+        if v > 0:
+            n = min(n, v)
+    return max(1, n)
+
+
+def workload_name(V, B, world):
+    """The BASELINE.json config a run measures."""
+    if V == 32000 and B == 1 and world == 1:
+        return "c2"
+    if V == 32000 and B == 4096:
+        return "c3" if world == 1 else f"c3 weak-scaled over {world} GPUs"
+    if V == 128256 and B == 4096:
+        return "c4" if world == 1 else ("c5" if world == 8 else f"c5 shape on {world} GPUs ({world}x4096 streams)")
+    return "custom"
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
@@ -59,8 +85,11 @@ def main():
     ap.add_argument("--tokens", type=int, default=16, help="symbols per stream per job")
     ap.add_argument("--prec", type=int, default=48)
     ap.add_argument("--pmf-bits", type=int, default=32, choices=(32, 64))
+    ap.add_argument("--scale-bits", type=int, default=0,
+                    help="pmf = max(1 or 2, floor(softmax * 2^k)); 0 = 31 for u32, 60 (llama-scale) for u64")
     ap.add_argument("--cpu-baseline", default="on", choices=("on", "off"))
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="cpu_baseline threads (0 = nproc: host_cores())")
+    ap.add_argument("--decode-reps", type=int, default=3, help="timed decode passes after a warm one (median)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="minimum CPU-baseline sample time")
     ap.add_argument("--cpu-streams", type=int, default=0, help="oracle sample streams (0 = all)")
     ap.add_argument("--path", default="auto", choices=("auto", "split", "fused"), help="encode kernel path")
@@ -109,8 +138,9 @@ def main():
                                          quantise=coder.quantize_logits)
         pmf = logits
     else:
-        pmf, sym = synth.softmax_tables(T, B, V, seed=1234 + 7919 * rank, device=dev,
-                                        scale_bits=31 if args.pmf_bits == 32 else 60)
+        scale_bits = args.scale_bits or (31 if args.pmf_bits == 32 else 60)
+        pmf, sym = synth.softmax_tables(T, B, V, seed=1234 + 7919 * rank, device=dev, scale_bits=scale_bits,
+                                        storage_bits=args.pmf_bits)
     torch.cuda.synchronize()
     log(f"[rank {rank}] inputs {tuple(pmf.shape)} {pmf.dtype} ({pmf.numel() * ebytes / 2**30:.2f} GiB) "
         f"in {time.time() - t_gen:.1f}s")
@@ -178,28 +208,35 @@ def main():
     data, nbits = coder.to_bytes() if rc == 0 else ([], None)
     decode = coder.decode_logits if logits_in else coder.decode
     coder.decode_open()
-    dec = decode(pmf)                                      # warm
+    dec = decode(pmf)                                      # warm (the clocks ramp after a workload switch)
     torch.cuda.synchronize()
-    coder.lib.lac_profile_read(coder.ctx, None, None, 1)
-    coder.lib.lac_profile_enable(coder.ctx, 1)
-    d0 = time.perf_counter()
-    coder.decode_open()
-    dec = decode(pmf)
-    torch.cuda.synchronize()
-    d1 = time.perf_counter()
-    coder.lib.lac_profile_enable(coder.ctx, 0)
-    dms = (C.c_double * 8)()
-    dcnt = (C.c_int64 * 8)()
-    coder.lib.lac_profile_read(coder.ctx, C.cast(dms, C.c_void_p), C.cast(dcnt, C.c_void_p), 1)
-    dkids = [k for k in (3, 5, 6, 7) if dcnt[k]]              # decode_step|stats path, decode_wave, q1 pair
-    dstep_ms = sum(dms[k] for k in dkids) / max(T, 1)
+    round_trip = bool(torch.equal(dec, sym)) and rc == 0
+    passes = []                                            # (wall s, {kernel id: ms}) per timed pass
+    for _ in range(max(1, args.decode_reps)):
+        coder.lib.lac_profile_read(coder.ctx, None, None, 1)
+        coder.lib.lac_profile_enable(coder.ctx, 1)
+        d0 = time.perf_counter()
+        coder.decode_open()
+        dec = decode(pmf)
+        torch.cuda.synchronize()
+        d1 = time.perf_counter()
+        coder.lib.lac_profile_enable(coder.ctx, 0)
+        dms = (C.c_double * 8)()
+        dcnt = (C.c_int64 * 8)()
+        coder.lib.lac_profile_read(coder.ctx, C.cast(dms, C.c_void_p), C.cast(dcnt, C.c_void_p), 1)
+        passes.append((d1 - d0, {k: dms[k] for k in (3, 5, 6, 7) if dcnt[k]}))
+        round_trip = round_trip and bool(torch.equal(dec, sym))
+    mid = sorted(passes, key=lambda p: p[0])[len(passes) // 2]          # the median pass
+    dkids = sorted(mid[1])                                     # decode_step|stats path, decode_wave, q1 pair
+    dstep_ms = sum(mid[1].values()) / max(T, 1)
     names = {3: "k_decode_step or k_dec_stats+k_decode_seq", 5: "k_decode_wave(_fine) or k_decode_block", 6: "k_q1_stats",
              7: "k_q1_decode"}
-    decode_info = {"symbols_per_s": B * T / (d1 - d0), "kernel": "+".join(names[k] for k in dkids),
+    decode_info = {"symbols_per_s": B * T / mid[0], "kernel": "+".join(names[k] for k in dkids),
+                   "passes": f"median of {len(passes)} timed passes after a warm one",
+                   "symbols_per_s_each": [B * T / p[0] for p in passes],
                    "kernel_ms_per_step": dstep_ms,
-                   "kernel_ms_per_step_each": {names[k]: dms[k] / max(T, 1) for k in dkids},
+                   "kernel_ms_per_step_each": {names[k]: mid[1][k] / max(T, 1) for k in dkids},
                    "achieved_GBps": B * (V * ebytes + 4) / (dstep_ms * 1e-3) / 1e9 if dkids else None}
-    round_trip = bool(torch.equal(dec, sym)) and rc == 0
     if dist:
         ok = torch.tensor([1 if round_trip else 0], device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
@@ -222,7 +259,7 @@ def main():
             host = pmf[:, :S, :].cpu().numpy()
             host = host.view(np.uint32) if args.pmf_bits == 32 else host.view(np.uint64)
         hsym = sym[:, :S].cpu().numpy()
-        nthreads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        nthreads = args.cpu_threads if args.cpu_threads > 0 else host_cores()
         # cpu_baseline: repeat the same bounded sample until >= --cpu-seconds of CPU
         # work (the first repetition is also the parity check)
         reps = 0
@@ -243,7 +280,10 @@ def main():
             what = "q1 quantise (1 thread) + encode" if logits_in else "encode"
             cpu = {"value": reps * S * T / (c1 - c0), "unit": "symbols/s", "cores": nthreads, "kind": "port",
                    "sample": f"C oracle (oracle/lac_oracle.c) {what} on {S} streams x {T} symbols of the same "
-                             f"inputs, repeated {reps}x, {nthreads} threads, {c1 - c0:.1f}s"}
+                             f"inputs, repeated {reps}x, {nthreads} threads, {c1 - c0:.1f}s",
+                   "cores_rule": f"nproc semantics: {len(os.sched_getaffinity(0))} CPUs in this process's affinity "
+                                 f"mask, OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', 'unset')}, "
+                                 f"os.cpu_count()={os.cpu_count()}"}
         avg_bits = float(np.mean(nbits.astype(np.float64))) / T if nbits is not None else None
         parity["bits_per_symbol"] = avg_bits
 
@@ -255,7 +295,7 @@ def main():
         alg_bytes = units * (V * ebytes + 4)
         achieved = alg_bytes / (rs_launch_ms * 1e-3) / 1e9 if cnt[kid] else None
         rows = (f"{args.input[7:]} logit rows, q1 tables in-kernel" if logits_in else f"uint{args.pmf_bits} pmf rows")
-        cname = {32000: "c3", 128256: "c4"}.get(V, "custom")      # BASELINE.json configs
+        cname = workload_name(V, B, world)                      # BASELINE.json configs
         cfg = {"workload": f"{cname}: vocab={V}, {B} streams/GPU, {T} symbols/stream per job, prec={P}, {rows}",
                "vocab": V, "streams": B, "tokens": T, "prec": P, "pmf_bits": args.pmf_bits, "input": args.input,
                "parallelism": f"streams sharded over {world} GPU(s)" + (f", {'RCCL' if backend == 'nccl' else backend} bitstream all-gather" if world > 1 else "")}
@@ -270,7 +310,8 @@ def main():
             "data": ("synthetic: logits 3*N(0,1) (torch.Generator seeded), symbols by inverse CDF of their q1 tables"
                      if logits_in else
                      "synthetic: logits 3*N(0,1) per step (torch.Generator seeded 1234+t), "
-                     f"pmf=max(1,floor(softmax*2^{31 if args.pmf_bits == 32 else 60})), symbols by inverse CDF"),
+                     f"pmf=max({2 if (args.scale_bits or (31 if args.pmf_bits == 32 else 60)) >= 60 else 1},"
+                     f"floor(softmax*2^{args.scale_bits or (31 if args.pmf_bits == 32 else 60)})), symbols by inverse CDF"),
             "config": cfg,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None,

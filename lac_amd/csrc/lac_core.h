@@ -62,13 +62,35 @@ __host__ __device__ inline int bitlen64(uint64_t x) { return x ? 64 - __builtin_
 
 __host__ __device__ inline uint64_t div_floor_inv(u128 N, uint64_t d, double inv);
 
-// 1/d for the quotient estimates of div_floor_inv.  On the device one v_rcp_f64
-// (no IEEE divide sequence on the coder's latency chain); its small relative
-// error only moves the first estimate, which the two exact remainder corrections
-// of div_floor_inv absorb, so results stay exact.
+// The first quotient estimate of div_floor / div_floor_inv is a double; one at or
+// above 2^64 (a quotient near 2^64 - 1, estimated high) starts from the largest
+// double below 2^64 instead, so the estimate stays within a few thousand of the
+// quotient and the second estimate leaves at most two +-1 corrections
+// (tests/test_core_host.py, also with the reciprocal 4 ULPs off).
+constexpr uint64_t kTopQ = 0xFFFFFFFFFFFFF800ull;
+
+// A remainder as a double: one rounding when it fits 64 bits (the split form
+// below rounds the low word of a small negative remainder to a multiple of 2^11,
+// which cost up to ~1024/d final corrections).
+__host__ __device__ inline double i128_to_double(i128 r) {
+    const int64_t lo = (int64_t)(uint64_t)r;
+    if ((i128)lo == r) return (double)lo;
+    return (double)(int64_t)(r >> 64) * 18446744073709551616.0 + (double)(uint64_t)r;
+}
+
+// 1/d for the quotient estimates of div_floor_inv.  On the device v_rcp_f64 plus
+// one Newton step (no IEEE divide sequence on the coder's latency chain).
+// v_rcp_f64 alone is good to only ~2^-25 relative (measured on the MI355X: up to
+// 2.6e8 ULPs, tools/rcp_probe.hip, profiles/r03/rcp_probe_before.json): the
+// second estimate of a quotient near 2^60 was then still ~2^10 off, and the +-1
+// correction loop of div_floor_inv ran up to 35 000 times (u64-table decode
+// targets).  The Newton step squares the error (two FMAs); results were exact
+// either way.
 __host__ __device__ inline double recip(uint64_t d) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    return __builtin_amdgcn_rcp((double)d);
+    const double dd = (double)d;
+    const double r = __builtin_amdgcn_rcp(dd);
+    return __builtin_fma(r, __builtin_fma(-dd, r, 1.0), r);
 #else
     return 1.0 / (double)d;
 #endif
@@ -86,9 +108,9 @@ __host__ __device__ inline uint64_t div_floor(u128 N, uint64_t d) {
     const double dd = (double)d;
     const double dn = (double)(uint64_t)(N >> 64) * two64 + (double)(uint64_t)N;
     double qd = dn / dd;
-    uint64_t q = qd >= 1.8e19 ? (uint64_t)1.8e19 : (uint64_t)qd;
+    uint64_t q = qd >= two64 ? kTopQ : (uint64_t)qd;
     i128 r = (i128)(N - (u128)q * d);
-    const double rd = (double)(int64_t)(r >> 64) * two64 + (double)(uint64_t)r;
+    const double rd = i128_to_double(r);
     const int64_t adj = (int64_t)(rd / dd);
     q += (uint64_t)adj;
     r -= (i128)adj * (i128)d;
@@ -102,20 +124,25 @@ __host__ __device__ inline uint64_t div_ceil(u128 N, uint64_t d) {
 }
 
 // div_floor with a precomputed inv = 1.0 / d (same estimate accuracy, no
-// float64 divide on the latency chain of the sequential coder).
-__host__ __device__ inline uint64_t div_floor_inv(u128 N, uint64_t d, double inv) {
+// float64 divide on the latency chain of the sequential coder).  `fixups`, when
+// not null, counts the final +-1 corrections (host checks bound them for an
+// inv off the correctly rounded 1/d by the device reciprocal's error).
+__host__ __device__ inline uint64_t div_floor_inv_n(u128 N, uint64_t d, double inv, int *fixups) {
     const double two64 = 18446744073709551616.0;
     const double dn = (double)(uint64_t)(N >> 64) * two64 + (double)(uint64_t)N;
     double qd = dn * inv;
-    uint64_t q = qd >= 1.8e19 ? (uint64_t)1.8e19 : (uint64_t)qd;
+    uint64_t q = qd >= two64 ? kTopQ : (uint64_t)qd;
     i128 r = (i128)(N - (u128)q * d);
-    const double rd = (double)(int64_t)(r >> 64) * two64 + (double)(uint64_t)r;
+    const double rd = i128_to_double(r);
     const int64_t adj = (int64_t)(rd * inv);
     q += (uint64_t)adj;
     r -= (i128)adj * (i128)d;
-    while (r < 0) { q -= 1; r += d; }
-    while (r >= (i128)d) { q += 1; r -= d; }
+    while (r < 0) { q -= 1; r += d; if (fixups) ++*fixups; }
+    while (r >= (i128)d) { q += 1; r -= d; if (fixups) ++*fixups; }
     return q;
+}
+__host__ __device__ inline uint64_t div_floor_inv(u128 N, uint64_t d, double inv) {
+    return div_floor_inv_n(N, d, inv, nullptr);
 }
 
 // CDFPredictor.fudged_dist test (arith_code.py:84): fudged iff T > w*minp.

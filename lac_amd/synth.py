@@ -116,22 +116,23 @@ def make_batch(seed: int, steps: int, streams: int, V: int, kind: str = "logunif
 
 # ----------------------------------------------------------- device tables
 def softmax_tables(steps: int, streams: int, V: int, seed: int = 1234, device="cuda",
-                   sigma: float = 3.0, scale_bits: int = 31, out=None):
+                   sigma: float = 3.0, scale_bits: int = 31, out=None, storage_bits: int | None = None):
     """Random-logit tables on the GPU (the BASELINE.json workload).
 
     Per step t: logits = sigma * N(0, 1) from ``torch.Generator(device)`` seeded
     ``seed + t``; pmf = max(1, floor(softmax * 2^scale_bits)) (scale_bits <= 31 ->
     uint32 bit patterns in int32 storage, else int64 for the 2^60 llama scale of
     llama_compress.py:29 with floor 2); symbols by inverse CDF of a seeded uniform.
+    ``storage_bits`` (default: 64 above scale 31) picks int64 / int32 storage.
     Returns (pmf [steps, streams, V], sym int32 [steps, streams]).
     """
     import torch
-    wide = scale_bits > 31
+    wide = (storage_bits or (64 if scale_bits > 31 else 32)) == 64
     dt = torch.int64 if wide else torch.int32
     if out is None:
         out = torch.empty((steps, streams, V), dtype=dt, device=device)
     sym = torch.empty((steps, streams), dtype=torch.int32, device=device)
-    floor_v = 2 if wide else 1
+    floor_v = 2 if scale_bits >= 60 else 1
     for t in range(steps):
         g = torch.Generator(device=device)
         g.manual_seed(seed + t)

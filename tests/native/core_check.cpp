@@ -5,6 +5,7 @@
 // resolution) sequentially on the CPU, so tests can compare it with the oracle
 // before any GPU is involved.  The wave-parallel parts (row scans, chunk search)
 // are exercised only by the GPU parity tests.
+#include <math.h>
 #include <stdint.h>
 #include <string.h>
 
@@ -19,6 +20,23 @@ extern "C" {
 uint64_t cc_div_floor(uint64_t nh, uint64_t nl, uint64_t d) { return div_floor(((u128)nh << 64) | nl, d); }
 uint64_t cc_div_floor_inv(uint64_t nh, uint64_t nl, uint64_t d) {
     return div_floor_inv(((u128)nh << 64) | nl, d, 1.0 / (double)d);
+}
+
+// div_floor_inv with the reciprocal moved `ulps` ULPs off the correctly rounded
+// 1/d (the device's v_rcp_f64 is an approximation); *fixups = final corrections.
+uint64_t cc_div_floor_inv_ulp(uint64_t nh, uint64_t nl, uint64_t d, int ulps, int *fixups) {
+    double inv = 1.0 / (double)d;
+    for (int i = 0; i < (ulps < 0 ? -ulps : ulps); i++) inv = nextafter(inv, ulps < 0 ? 0.0 : 1.0e300);
+    *fixups = 0;
+    return div_floor_inv_n(((u128)nh << 64) | nl, d, inv, fixups);
+}
+
+// Python's a / b for 0 <= a <= b < 2^63 (lac_core.h cr_ratio), as its bit pattern.
+uint64_t cc_cr_ratio(uint64_t a, uint64_t b) {
+    const double r = cr_ratio(a, b);
+    uint64_t u;
+    memcpy(&u, &r, 8);
+    return u;
 }
 
 // floor/ceil(c*w/T) through the row fraction (~0 for rows without one).

@@ -106,3 +106,44 @@ def test_core_random_vs_oracle(core, seed):
         want = coracle.encode(rows, sym[:, 0], prec)
         rc, data, L = _enc(core, rows, sym[:, 0], prec)
         assert rc == 0 and (data, L) == want[:2], (V, prec, kind)
+
+
+def test_div_floor_inv_with_an_inexact_reciprocal(core):
+    """The device's div_floor_inv estimates with v_rcp_f64, an approximation of 1/d
+    (lac_core.h recip).  With the reciprocal up to 4 ULPs off the correctly rounded
+    one (tools/rcp_probe.hip measures the hardware's own error on the MI355X) the
+    quotient stays exact and the final correction loops run at most twice."""
+    core.cc_div_floor_inv_ulp.restype = C.c_uint64
+    core.cc_div_floor_inv_ulp.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, C.POINTER(C.c_int)]
+    rng = random.Random(17)
+    worst = 0
+    fix = C.c_int()
+    for i in range(60000):
+        d = rng.choice([1, 3, rng.randrange(1, 1 << 20), rng.randrange(1, 1 << 47), rng.randrange(1, 1 << 64),
+                        (1 << 64) - rng.randrange(1, 1 << 10), (1 << 63) + rng.randrange(0, 1 << 10)])
+        q = rng.choice([rng.randrange(0, 1 << 64), (1 << 64) - 1 - rng.randrange(0, 1 << 12), rng.randrange(0, 1 << 48)])
+        r = rng.randrange(0, d)
+        N = q * d + r
+        if N >> 128:
+            continue
+        ulps = rng.choice([-4, -2, -1, 0, 1, 2, 4])
+        got = core.cc_div_floor_inv_ulp(N >> 64, N & ((1 << 64) - 1), d, ulps, C.byref(fix))
+        assert got == q, (N, d, ulps)
+        worst = max(worst, fix.value)
+    assert worst <= 2, worst
+
+
+def test_cr_ratio_is_pythons_division(core):
+    """lac_core.h cr_ratio == CPython's int / int (correctly rounded) -- the float
+    A_from_bin.flush ranks candidates by (arith_code.py:305-312)."""
+    import struct
+    core.cc_cr_ratio.restype = C.c_uint64
+    core.cc_cr_ratio.argtypes = [C.c_uint64, C.c_uint64]
+    rng = random.Random(23)
+    for i in range(60000):
+        b = rng.choice([1, 2, 3, rng.randrange(1, 1 << 20), rng.randrange(1, 1 << 53), rng.randrange(1 << 53, 1 << 63),
+                        (1 << 62) + rng.randrange(0, 1 << 8)])
+        a = rng.choice([0, b, b - 1, rng.randrange(0, b + 1), b // 2, b // 3 + 1])
+        a = max(0, min(a, b))
+        want = struct.unpack("<Q", struct.pack("<d", a / b))[0]
+        assert core.cc_cr_ratio(a, b) == want, (a, b)
