@@ -257,6 +257,15 @@ int lac_encode_logits(lac_ctx *ctx, const void *logits_dev, int logit_type, int6
 int lac_decode_logits_steps(lac_ctx *ctx, const void *logits_dev, int logit_type, int64_t step_stride,
                             int64_t stream_stride, int64_t steps, int32_t *sym_out_dev, void *stream);
 
+/* Rows longer than a CU holds (LAC_OPT_Q1_SHAPE 19 / 20, AUTO for e.g. f32 V =
+ * 128256) are split over groups of 2..4 workgroups that exchange each row's
+ * maximum, which needs every member resident.  When a member is not (another
+ * kernel holds CUs) the waiting ones give up after ~0.1 s, raise the launch's
+ * abort flag, and a tiled two-pass launch queued behind it recomputes every row:
+ * results are identical either way.  Synchronises `stream`; *aborted = 1 if the
+ * last such launch of this context took that path. */
+int lac_q1_group_aborted(lac_ctx *ctx, int64_t *aborted, void *stream);
+
 /* Materialise the q1 tables: pmf_out_dev[(t*streams + b)*vocab + i] (uint32). */
 int lac_quantize_logits(lac_ctx *ctx, const void *logits_dev, int logit_type, int64_t step_stride,
                         int64_t stream_stride, int64_t steps, uint32_t *pmf_out_dev, void *stream);

@@ -68,6 +68,7 @@ PROTOTYPES = [
     ("lac_hc_encode_symbol", _i, [_i, _vp, _vp, _i64, _i64, _vp, _vp]),
     ("lac_hc_encode_flush", _i, [_i, _i64, _i64, _vp, _vp]),
     ("lac_hc_decode_emit", _i, [_i, _vp, _i64, _i64, _i]),
+    ("lac_q1_group_aborted", _i, [_vp, _vp, _vp]),
     ("lac_profile_enable", _i, [_vp, _i]),
     ("lac_profile_read", _i, [_vp, _vp, _vp, _i]),
     ("lac_q1_k", _i, [_i, _i64]),
@@ -120,7 +121,12 @@ def load():
     except OSError as e:
         raise LacLibraryError(f"cannot load {LIB_PATH}: {e}") from e
     for name, res, args in PROTOTYPES:
-        f = getattr(lib, name)
+        try:
+            f = getattr(lib, name)
+        except AttributeError:
+            if os.environ.get("LAC_LIB"):      # an older tuning variant (A/B runs): newer entry points absent
+                continue
+            raise LacLibraryError(f"{LIB_PATH} lacks {name}: rebuild it (python -m lac_amd.build)") from None
         f.restype = res
         f.argtypes = args
     _lib = lib

@@ -213,6 +213,34 @@ __device__ inline u128 wave_sum_u128(u128 v) {
 }
 constexpr i128 kI128Min = (i128)((u128)1 << 127);
 
+// Inclusive max-scan of an i128 over the wave on DPP (the Hillis-Steele steps of
+// wave_incl_scan_u64, with lanes outside the source range reading kI128Min
+// instead of 0: bound_ctrl off, `old` = the minimum's words).
+template <int CTRL, int ROWS = 0xF>
+__device__ inline i128 dpp_i128_or_min(i128 v) {
+    const u128 u = (u128)v;
+    const uint32_t w0 = (uint32_t)u, w1 = (uint32_t)(u >> 32), w2 = (uint32_t)(u >> 64), w3 = (uint32_t)(u >> 96);
+    const uint32_t r0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w0, CTRL, ROWS, 0xF, false);
+    const uint32_t r1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w1, CTRL, ROWS, 0xF, false);
+    const uint32_t r2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w2, CTRL, ROWS, 0xF, false);
+    const uint32_t r3 = (uint32_t)__builtin_amdgcn_update_dpp((int)0x80000000, (int)w3, CTRL, ROWS, 0xF, false);
+    return (i128)(((u128)r3 << 96) | ((u128)r2 << 64) | ((u128)r1 << 32) | r0);
+}
+__device__ inline i128 i128_vmax(i128 a, i128 b) { return a > b ? a : b; }
+__device__ inline i128 wave_incl_max_i128(i128 v) {
+    v = i128_vmax(v, dpp_i128_or_min<0x111>(v));             // row_shr:1
+    v = i128_vmax(v, dpp_i128_or_min<0x112>(v));             // row_shr:2
+    v = i128_vmax(v, dpp_i128_or_min<0x114>(v));             // row_shr:4
+    v = i128_vmax(v, dpp_i128_or_min<0x118>(v));             // row_shr:8
+    v = i128_vmax(v, dpp_i128_or_min<0x142, 0xA>(v));        // row_bcast:15 into rows 1, 3
+    v = i128_vmax(v, dpp_i128_or_min<0x143, 0xC>(v));        // row_bcast:31 into rows 2, 3
+    return v;
+}
+__device__ inline i128 readlane_i128(i128 v, int l) {
+    const u128 u = (u128)v;
+    return (i128)(((u128)readlane_u64((uint64_t)(u >> 64), l) << 64) | readlane_u64((uint64_t)u, l));
+}
+
 // ------------------------------------------------------------------ row loads
 template <typename E, int VEC> struct VecT;
 template <> struct VecT<uint32_t, 4> { typedef uint32_t type __attribute__((ext_vector_type(4))); };
@@ -884,59 +912,100 @@ __device__ inline bool scan_chunk(const E *row, int64_t nvec, int64_t cv0, int G
     return false;
 }
 
-// Fudged val_to_symbol + symbol_to_range (fudged_dist closed form).  f is
-// strictly increasing and f_e = e + g(Xmax_e) with g monotone, so f_e > v  <=>
-// some j <= e has e > v - g(X_j); the first such e is
-//     s = min_j max(j, v + 1 - g(X_j)),
-// a plain min-reduction over the row (no ordered scan of the maxima).
+// Fudged val_to_symbol + symbol_to_range (fudged_dist closed form, lac_core.h
+// fudge_f): f_e = e + g(Xmax_e), g(X) = max(1, min(C, floor(X / T))), C = w - V + 1,
+// Xmax_e = max_{j<=e} (c_j w - j T), is strictly increasing, and val_to_symbol
+// (bisect_right of floor(v*f_last/w) = v, arith_code.py:94-97) is the first e with
+// f_e > v, i.e. with
+//     e >= v   or   (v - e < C  and  Xmax_e >= (v - e + 1) T)
+// -- one 128-bit product and compare per entry, no division.  One wave walks the
+// row in chunks of 64 * VEC entries (one 16-B vector per lane, the next chunk in
+// flight), the running maximum carried across chunks; the chunk holding s also
+// holds Xmax_{s-1} and Xmax_s, so the range (f_{s-1}, f_s) needs no second pass
+// and just two divisions.
 template <typename E>
 __device__ inline int decode_fudged(const E *row, int64_t V, uint64_t w, uint64_t v, uint64_t T, int64_t *s_out,
                                     uint64_t *a, uint64_t *bb) {
+    constexpr int VEC = 16 / sizeof(E);
     const int lane = (int)lane_id();
-    const uint64_t C = w - (uint64_t)V + 1;
+    const int64_t C = (int64_t)(w - (uint64_t)V + 1);
+    const int64_t nvec = (V + VEC - 1) / VEC;
+    const bool vec_ok = (V % VEC) == 0 && ((uintptr_t)row & 15) == 0;
+    auto load = [&](int64_t vi) {                           // entries past V read as 0
+        typename VecT<E, 1>::type out[VEC];
+        const int64_t e0 = vi * VEC;
+        if (vec_ok && vi < nvec) {
+            const typename VecT<E, VEC>::type x = load_vec<E, VEC>(row, vi);
+#pragma unroll
+            for (int j = 0; j < VEC; j++) out[j] = vget<E, VEC>(x, j);
+        } else {
+#pragma unroll
+            for (int j = 0; j < VEC; j++) out[j] = e0 + j < V ? row[e0 + j] : (E)0;
+        }
+        struct R { E x[VEC]; } r;
+#pragma unroll
+        for (int j = 0; j < VEC; j++) r.x[j] = out[j];
+        return r;
+    };
     uint64_t base = 0;
-    int64_t best = V;
-    constexpr int FV = 2;                                   // cold path: keep register pressure low
-    for (int64_t r0 = 0; r0 < V; r0 += 64 * FV) {
-        E xe[FV];
+    i128 xcarry = kI128Min;
+    auto nxt = load(lane);
+    for (int64_t r0 = 0; r0 < V; r0 += 64 * VEC) {
+        const auto cur = nxt;
+        if (r0 + 64 * VEC < V) nxt = load((r0 + 64 * VEC) / VEC + lane);
         uint64_t ls = 0;
 #pragma unroll
-        for (int j = 0; j < FV; j++) {
-            const int64_t e = r0 + lane * FV + j;
-            xe[j] = e < V ? row[e] : (E)0;
-            ls += (uint64_t)xe[j];
-        }
-        const uint64_t in = wave_incl_scan_u64(ls);
-        uint64_t c = base + in - ls;
+        for (int j = 0; j < VEC; j++) ls += (uint64_t)cur.x[j];
+        const uint64_t incl = wave_incl_scan_u64(ls);
+        uint64_t c = base + incl - ls;
+        i128 run[VEC], lm = kI128Min;
 #pragma unroll
-        for (int j = 0; j < FV; j++) {
-            const int64_t e = r0 + lane * FV + j;
-            c += (uint64_t)xe[j];
-            if (e < V) {
-                const i128 X = fudge_x(c, e, w, T);
-                uint64_t g = 1;
-                if (X >= (i128)2 * (i128)T) {
-                    const uint64_t m = div_floor((u128)X, T);
-                    g = m < C ? m : C;
-                }
-                int64_t cand = (int64_t)v + 1 - (int64_t)g;
-                cand = cand > e ? cand : e;
-                best = cand < best ? cand : best;
-            }
+        for (int j = 0; j < VEC; j++) {
+            const int64_t e = r0 + lane * VEC + j;
+            c += (uint64_t)cur.x[j];
+            const i128 X = e < V ? fudge_x(c, e, w, T) : kI128Min;
+            lm = X > lm ? X : lm;
+            run[j] = lm;                                      // lane-local prefix max
         }
-        base += readlane_u64(in, 63);
-        const int64_t wb = (int64_t)wave_min_u64((uint64_t)best);
-        if (wb < r0 + 64 * FV) break;                      // later j cannot beat it
+        // exclusive wave max-scan of the lane maxima, after the carry
+        const i128 pre = wave_incl_max_i128(lm);
+        const i128 tot = readlane_i128(pre, 63);
+        i128 excl = shfl_i128(pre, lane ? lane - 1 : 0);
+        excl = lane ? (excl > xcarry ? excl : xcarry) : xcarry;
+        int hit = -1;
+#pragma unroll
+        for (int j = VEC - 1; j >= 0; j--) {
+            const int64_t e = r0 + lane * VEC + j;
+            const i128 xm = run[j] > excl ? run[j] : excl;
+            bool ok = e < V && (e >= (int64_t)v);
+            if (e < V && !ok && (int64_t)v - e < C)
+                ok = xm >= (i128)((u128)(uint64_t)((int64_t)v - e + 1) * T);
+            hit = ok ? j : hit;
+        }
+        const uint64_t mask = __ballot(hit >= 0);
+        if (mask) {
+            const int L = __ffsll((unsigned long long)mask) - 1;
+            const int jh = __shfl(hit, L);
+            const int64_t s = r0 + (int64_t)L * VEC + jh;
+            // Xmax_{s-1} and Xmax_s from lane L's registers
+            i128 xprev = excl, xs = excl;
+#pragma unroll
+            for (int j = 0; j < VEC; j++) {
+                const i128 xm = run[j] > excl ? run[j] : excl;
+                if (j == jh - 1) xprev = xm;
+                if (j == jh) xs = xm;
+            }
+            xprev = shfl_i128(xprev, L);
+            xs = shfl_i128(xs, L);
+            *a = s > 0 ? fudge_f(s - 1, xprev, T, w, V) : 0;
+            *bb = fudge_f(s, xs, T, w, V);
+            *s_out = s;
+            return 0;
+        }
+        base += readlane_u64(incl, 63);
+        xcarry = tot > xcarry ? tot : xcarry;
     }
-    const int64_t s = (int64_t)wave_min_u64((uint64_t)best);
-    if (s < 0 || s >= V) return LAC_E_DECODE_RANGE;
-    uint64_t cprev = 0;
-    const i128 xprev = s > 0 ? wave_xmax_prefix<E>(row, s, w, T, &cprev) : kI128Min;
-    const i128 xs = fudge_x(cprev + (uint64_t)row[s], s, w, T);
-    *a = s > 0 ? fudge_f(s - 1, xprev, T, w, V) : 0;
-    *bb = fudge_f(s, xs > xprev ? xs : xprev, T, w, V);
-    *s_out = s;
-    return 0;
+    return LAC_E_DECODE_RANGE;
 }
 
 // Narrow to symbol s and renormalise, pulling k fresh bits into x
@@ -2026,7 +2095,10 @@ __global__ __launch_bounds__(64 * NWB, LAC_Q1_MINW) void k_q1_stats(const LT *__
                                                               int64_t B, int64_t rows, int64_t V, int64_t t0,
                                                               uint32_t xsh, int64_t G, RowStats *__restrict__ out,
                                                               uint64_t *__restrict__ chunks,
-                                                              float *__restrict__ mrow) {
+                                                              float *__restrict__ mrow, const uint64_t *gate) {
+    // gate (the repair launch after a row-group launch, k_q1_stats_rl): run only if
+    // that launch aborted its exchanges
+    if (gate && __hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
     constexpr int N = LogitN<LT>::N, NT = 64 * RW, NR = NWB / RW;
     constexpr bool IMAX = LAC_Q1_IMAX && sizeof(LT) == 2 && NR == 1 && !MULTI;
     constexpr bool BUF = R <= 8 && !MULTI;                    // row-load form (RowSrc)
@@ -2278,7 +2350,8 @@ typedef __attribute__((address_space(3))) void lvoid_t;
 // exceeds the CU count (one block per CU: every member is resident), and the wait
 // is bounded: a partner that never posts poisons the row's total (+2^62:
 // LAC_E_TABLE at the coder) instead of hanging the GPU.
-constexpr uint32_t kGroupSpinMax = 1u << 21;                 // polls: a few seconds (s_sleep 2 + a device-scope load each)
+constexpr uint32_t kGroupSpinMax = 1u << 17;                 // polls (s_sleep 2 + a device-scope load each): ~0.1 s,
+                                                             // far beyond any wait for a resident partner
 
 // DEC: a row's 64 chunk totals are stored after the NEXT row's maximum, not at the
 // row's end, where the store's completion sat in front of the next row's vmcnt(0)
@@ -2297,24 +2370,36 @@ __device__ inline uint64_t group_ld(const uint64_t *p) {
 // partner's word for seq is overwritten unread) and fold in the K - 1 partners'
 // (blocks ((slot / K) * K + k) * 8 + xcd) with op; *ok = false when one never came
 // (NRB rows per block: row g of the block uses word pair b * NRB + g)
+// The launch's abort word (after the exchange words, zeroed with them): a block
+// whose partner did not post within kGroupSpinMax polls -- not resident, e.g.
+// while another kernel holds CUs -- sets it; every block then stops waiting at
+// once (its rows are poisoned) and the gated tiled launch queued behind this one
+// (q1_group_kernel) recomputes every row without row groups.
 template <int K, int NRB, typename Op>
-__device__ inline uint32_t group_exchange(uint64_t *xch, int g, uint32_t seq, uint32_t m, Op op, bool *ok) {
+__device__ inline uint32_t group_exchange(uint64_t *xch, uint64_t *abortw, int g, uint32_t seq, uint32_t m, Op op,
+                                          bool *ok) {
     const unsigned b = blockIdx.x, sl = seq & 1, xcd = b & 7, g0 = ((b >> 3) / K) * K;
     __hip_atomic_store(&xch[2 * (b * NRB + g) + sl], ((uint64_t)seq << 32) | m, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
     uint32_t acc = m;
-    bool all = true;
+    bool all = group_ld(abortw) == 0;
 #pragma unroll
     for (int k = 0; k < K; k++) {
         const unsigned pb = (g0 + k) * 8 + xcd;
-        if (pb == b) continue;
+        if (pb == b || !all) continue;
         const uint64_t *px = &xch[2 * (pb * NRB + g) + sl];
         uint64_t v = group_ld(px);
-        for (uint32_t n = 0; (uint32_t)(v >> 32) != seq && n < kGroupSpinMax; n++) {
+        uint32_t n = 0;
+        for (; (uint32_t)(v >> 32) != seq && n < kGroupSpinMax; n++) {
             __builtin_amdgcn_s_sleep(2);
+            if ((n & 63) == 63 && group_ld(abortw)) break;       // another block gave up
             v = group_ld(px);
         }
-        all = all && (uint32_t)(v >> 32) == seq;
+        if ((uint32_t)(v >> 32) != seq) {
+            all = false;
+            if (n >= kGroupSpinMax)
+                __hip_atomic_store(abortw, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         acc = op(acc, (uint32_t)v);
     }
     *ok = all;
@@ -2386,7 +2471,7 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
         seq++;
         if (tid == g * NT) {                                    // each row's leader
             bool ok;
-            sxv[g] = group_exchange<KG, NRB>(xch, g, seq, v, op, &ok);
+            sxv[g] = group_exchange<KG, NRB>(xch, xch + 2 * NRB * gridDim.x, g, seq, v, op, &ok);
             sxok[g] = ok;
         }
         __syncthreads();
@@ -2867,6 +2952,7 @@ struct lac_ctx {
     void *dmeta = nullptr;              // stats-path decode: [chunk_steps * B] DecRowMeta
     float *q1m = nullptr;               //                [chunk_steps * B] row maxima
     uint64_t *pxch = nullptr;           // paired row stats (shape 19): [2 * cus] maximum words
+    int64_t xch_abort = -1;             // word of pxch holding the last row-group launch's abort flag
     // live kernel timing (lac_profile_enable): hipEvent pairs around launches
     bool prof = false;
     std::vector<hipEvent_t> ev_pool;
@@ -2894,7 +2980,7 @@ struct ProfScope {
     hipStream_t st;
     hipEvent_t a = nullptr, b = nullptr;
     ProfScope(lac_ctx *c_, int kid_, hipStream_t st_) : c(c_), kid(kid_), st(st_) {
-        if (c->prof) {
+        if (c->prof && kid >= 0) {
             a = ev_get(c);
             b = ev_get(c);
             if (a && b) (void)hipEventRecord(a, st);
@@ -3171,7 +3257,7 @@ struct Q1Args {
 };
 
 template <typename LT, int RW, int R, bool DEC, bool MULTI, bool PF, int NWB = kQ1Waves>
-static int q1_stats_launch(lac_ctx *c, const Q1Args &a, hipStream_t st) {
+static int q1_stats_launch(lac_ctx *c, const Q1Args &a, hipStream_t st, const uint64_t *gate = nullptr) {
     static int per_cu = 0;                                       // resident blocks per CU (occupancy API)
     if (!per_cu) {
         int n = 0;
@@ -3185,10 +3271,10 @@ static int q1_stats_launch(lac_ctx *c, const Q1Args &a, hipStream_t st) {
     const int64_t need = (a.rows + NR - 1) / NR, cap = (int64_t)c->cus * per_cu;
     const unsigned grid = (unsigned)(need < cap ? need : cap);
     const int64_t nvec = c->V / LogitN<LT>::N;
-    ProfScope ps(c, KID_Q1_STATS, st);
+    ProfScope ps(c, gate ? -1 : KID_Q1_STATS, st);            // (a gated repair launch is not profiled)
     k_q1_stats<LT, RW, R, DEC, MULTI, PF, NWB><<<grid, 64 * NWB, 0, st>>>(
         (const LT *)a.lg, a.ss, a.bs, a.sym, c->B, a.rows, c->V, a.t0, a.xsh, q1_groups_per_chunk(nvec), c->stats,
-        c->q1chunks, c->q1m);
+        c->q1chunks, c->q1m, gate);
     CHECK_LAUNCH();
     return LAC_OK;
 }
@@ -3239,21 +3325,30 @@ template <typename LT, bool DEC, int REP, int LASTN, int K, int NT = 1024>
 static int q1_group_kernel(lac_ctx *c, const Q1Args &a, hipStream_t st, int split) {
     constexpr int NRB = 1024 / NT;
     const int64_t nvec = c->V / LogitN<LT>::N;
-    if (!c->pxch) HIPCHK(hipMalloc(&c->pxch, sizeof(uint64_t) * 4 * c->cus));   // (<= 2 rows per block)
+    if (!c->pxch) HIPCHK(hipMalloc(&c->pxch, sizeof(uint64_t) * (4 * c->cus + 1)));   // (<= 2 rows per block) + abort
     // groups of K blocks in runs of 8 K (one per XCD each); never more blocks than CUs
     // (one per CU: every member of every group resident at once)
     const int64_t need = 8 * K * ((a.rows + 8 * NRB - 1) / (8 * NRB)), cap = (int64_t)(c->cus / (8 * K)) * (8 * K);
     const unsigned grid = (unsigned)(need < cap ? need : cap);
-    HIPCHK(hipMemsetAsync(c->pxch, 0, sizeof(uint64_t) * 2 * NRB * grid, st));   // no stale sequence numbers
+    HIPCHK(hipMemsetAsync(c->pxch, 0, sizeof(uint64_t) * (2 * NRB * grid + 1), st));   // no stale sequence numbers,
+                                                                                      // abort word clear
     // the segments add into zeroed outputs
     if (DEC) HIPCHK(hipMemsetAsync(c->q1chunks, 0, sizeof(uint64_t) * 64 * a.rows, st));
     else HIPCHK(hipMemsetAsync(c->stats, 0, sizeof(RowStats) * a.rows, st));
-    ProfScope ps(c, KID_Q1_STATS, st);
-    k_q1_stats_rl<LT, DEC, REP, LASTN, NT, K><<<grid, 1024, 0, st>>>(
-        (const LT *)a.lg, a.ss, a.bs, a.sym, c->B, a.rows, c->V, a.t0, a.xsh, q1_groups_per_chunk(nvec), c->stats,
-        c->q1chunks, c->q1m, c->pxch, split);
-    CHECK_LAUNCH();
-    return LAC_OK;
+    {
+        ProfScope ps(c, KID_Q1_STATS, st);
+        k_q1_stats_rl<LT, DEC, REP, LASTN, NT, K><<<grid, 1024, 0, st>>>(
+            (const LT *)a.lg, a.ss, a.bs, a.sym, c->B, a.rows, c->V, a.t0, a.xsh, q1_groups_per_chunk(nvec), c->stats,
+            c->q1chunks, c->q1m, c->pxch, split);
+        CHECK_LAUNCH();
+    }
+    // repair: the tiled two-pass shape over the same rows, gated on the abort word
+    // (its blocks exit at once when the groups completed: one small launch per job)
+    const uint64_t *gate = c->pxch + 2 * NRB * grid;
+    c->xch_abort = 2 * NRB * (int64_t)grid;
+    if (DEC) return q1_stats_launch<LT, 16, 16, DEC, true, false, 16>(c, a, st, gate);            // shape 10
+    if (sizeof(LT) == 4) return q1_stats_launch<LT, 16, 8, DEC, true, true, 16>(c, a, st, gate);  // shape 14
+    return q1_stats_launch<LT, 8, 8, DEC, true, false>(c, a, st, gate);                            // shape 8
 }
 
 template <typename LT, bool DEC, int REP, int LASTN, int NT>
@@ -3977,6 +4072,18 @@ int lac_hc_decode_emit(int prec, int64_t *regs, int64_t lo, int64_t hi, int reno
         if (++n > 128 || !hc_regs_ok(l, h) || !hc_regs_ok(lb, hb)) return fail(LAC_E_ARG, "registers out of range");
     }
     regs[0] = l; regs[1] = h; regs[2] = lb; regs[3] = hb;
+    return LAC_OK;
+}
+
+int lac_q1_group_aborted(lac_ctx *c, int64_t *aborted, void *stream) {
+    if (!c || !aborted) return fail(LAC_E_ARG, "NULL argument");
+    *aborted = 0;
+    if (c->xch_abort < 0 || !c->pxch) return LAC_OK;
+    HIPCHK(hipSetDevice(c->device));
+    uint64_t v = 0;
+    HIPCHK(hipMemcpyAsync(&v, c->pxch + c->xch_abort, sizeof v, hipMemcpyDeviceToHost, S(stream)));
+    HIPCHK(hipStreamSynchronize(S(stream)));
+    *aborted = v ? 1 : 0;
     return LAC_OK;
 }
 

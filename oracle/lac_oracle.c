@@ -286,6 +286,59 @@ int lacref_decode(const void *pmf, int elem_bytes, int64_t V, int64_t nsym, int6
     return rc;
 }
 
+/* A_from_bin.run(bits, stop=0) literally (arith_code.py:264-299, :322-326): per
+ * bit receive_bit halves [lb, hb]; while val_to_symbol of both window ends agree,
+ * emit_symbol (with its overlap check) and the emit_bit loop over l, h, lb, hb.
+ * Rows: step t uses row min(t, nrows-1).  Writes at most max_out symbols and
+ * returns how many the bits determine (or a negative status). */
+int64_t lacref_decode_bitserial(const void *pmf, int elem_bytes, int64_t V, int64_t nrows, int64_t step_stride,
+                                const uint8_t *bytes, uint64_t nbits, int prec, int32_t *syms_out,
+                                int64_t max_out) {
+    int rc = check_prec(prec, V);
+    if (rc) return rc;
+    const int64_t D = (int64_t)1 << prec, Hd = (int64_t)1 << (prec - 1);
+    uint64_t *cdf = malloc(sizeof(uint64_t) * V), *scr = malloc(sizeof(uint64_t) * V);
+    if (!cdf || !scr) { free(cdf); free(scr); return R_E_ARG; }
+    int64_t l = 0, h = D - 1, lb = 0, hb = D - 1, n = 0, row_of = -1;
+    uint64_t minp = 0;
+    for (uint64_t i = 0; i < nbits && rc == R_OK; i++) {
+        const int64_t half = (hb - lb + 1) / 2;
+        lb += half * getbit(bytes, nbits, i);
+        hb = lb + half - 1;
+        for (;;) {
+            const int64_t r = n < nrows ? n : nrows - 1;
+            if (r != row_of) {
+                if ((rc = build_cdf((const char *)pmf + (size_t)(r * step_stride) * elem_bytes, elem_bytes, V, cdf,
+                                    &minp)))
+                    break;
+                row_of = r;
+            }
+            const uint64_t w = (uint64_t)(h - l + 1);
+            const uint64_t *dist = fudged_dist(cdf, minp, V, w, scr);
+            /* lb >= l always holds here (a symbol is emitted only inside its range) */
+            const int64_t ls = val_to_symbol(dist, V, (uint64_t)(lb - l), w);
+            const int64_t hs = (hb - l) >= (int64_t)w ? V : val_to_symbol(dist, V, (uint64_t)(hb - l), w);
+            if (ls != hs) break;
+            uint64_t a, b;
+            if ((rc = symbol_to_range(dist, V, ls, w, &a, &b))) break;
+            if (region_overlap(l + (int64_t)a, l + (int64_t)b - 1, lb, hb) == 0) { rc = R_E_DECODE_RANGE; break; }
+            h = l + (int64_t)b - 1;
+            l += (int64_t)a;
+            if (n < max_out) syms_out[n] = (int32_t)ls;
+            n++;
+            while (h - l < Hd) {
+                const int64_t d = floordiv(l, Hd);
+                l = l * 2 - d * D;
+                h = h * 2 + 1 - d * D;
+                lb = lb * 2 - d * D;
+                hb = hb * 2 + 1 - d * D;
+            }
+        }
+    }
+    free(cdf); free(scr);
+    return rc ? rc : n;
+}
+
 /* ---- ACSampler encode on a fixed uint64 CDF (arithmetic_coding.py) ---- */
 int lacref_acsampler_encode(const uint64_t *cdf, int64_t V, const int32_t *toks, int64_t n, int prec,
                             uint8_t *bits_out, uint64_t cap_bits, uint64_t *nbits) {

@@ -40,6 +40,9 @@ def lib():
         L.lacref_decode.restype = C.c_int
         L.lacref_decode.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.c_int64, C.c_int64, C.c_void_p,
                                     C.c_uint64, C.c_int, C.c_void_p]
+        L.lacref_decode_bitserial.restype = C.c_int64
+        L.lacref_decode_bitserial.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.c_int64, C.c_int64, C.c_void_p,
+                                              C.c_uint64, C.c_int, C.c_void_p, C.c_int64]
         L.lacref_q1_quantize.restype = C.c_int
         L.lacref_q1_quantize.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.c_int, C.c_void_p]
         L.lacref_q1_k.restype = C.c_int
@@ -120,6 +123,20 @@ def decode(rows, data: bytes, nbits: int, nsym: int, prec: int, static=False):
     if rc:
         raise OracleError(rc)
     return out[:nsym].tolist()
+
+
+def decode_bitserial(rows, data: bytes, nbits: int, prec: int, max_out: int = 1 << 20):
+    """A_from_bin.run(bits, stop=0) (the reference's bit-serial decoder, literal in
+    C): every symbol the bits determine; rows[min(t, len-1)] for step t."""
+    a = _rows_array(rows)
+    V = a.shape[1]
+    buf = np.frombuffer(bytes(data) + b"\0" * 8, dtype=np.uint8).copy()
+    out = np.zeros(max(max_out, 1), dtype=np.int32)
+    n = lib().lacref_decode_bitserial(_ptr(a), a.itemsize, V, a.shape[0], V, _ptr(buf), nbits, prec, _ptr(out),
+                                      max_out)
+    if n < 0:
+        raise OracleError(int(n))
+    return out[:min(n, max_out)].tolist()
 
 
 def acsampler_encode(cdf, tokens, prec=48):

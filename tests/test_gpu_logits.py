@@ -314,3 +314,70 @@ def test_q1_shape_option_range():
     for ok in (0, 19, 20):
         c.set_q1_shape(ok)
     c.close()
+
+
+@pytest.mark.parametrize("hog_s", [0.6, 0.02])
+def test_row_groups_while_another_kernel_holds_cus(hog_s):
+    """Rows over groups of blocks (f32 V = 128256: shape 19, AUTO) need every group
+    member resident.  A kernel on another stream holds all but 8 CUs (tests/native/
+    hog.hip): for 0.6 s the waiting members give up, the launch aborts and the
+    gated tiled launch recomputes every row; for 0.02 s the late members arrive in
+    time.  The hog leaves one CU per XCD free, so the first block of each XCD's
+    first group is resident and its partner is not.  Either way encode bytes and
+    decoded symbols equal a run on an idle GPU."""
+    import ctypes as C
+    import os
+    import time
+    from conftest import REPO
+    from lac_amd import _lib
+    hog = C.CDLL(os.path.join(REPO, "tests", "native", "libhog.so"))
+    hog.hog_launch.argtypes = [C.c_int, C.c_double, C.c_void_p, C.c_void_p]
+    V, B, steps, prec = 128256, 256, 2, 48
+    x = _device_logits(_logits(31, steps, B, V), "f32")
+    c = _coder(V, B, prec, cap=steps * (prec + 2) + 256)
+    q = c.quantize_logits(x)
+    cdf = torch.cumsum(q.view(torch.int32).to(torch.int64) & 0xFFFFFFFF, -1)
+    u = torch.rand((steps, B, 1), generator=torch.Generator(device=DEV).manual_seed(5), device=DEV,
+                   dtype=torch.float64)
+    sym = torch.searchsorted(cdf, (u * cdf[..., -1:].double()).long(), right=True).squeeze(-1).to(torch.int32)
+    sym = torch.clamp(sym, max=V - 1)
+    c.encode_logits_job(x, sym)
+    want, wn = c.to_bytes()
+    ok = torch.zeros(1, dtype=torch.int32, device=DEV)
+    busy = torch.cuda.Stream(device=DEV)
+    mine = torch.cuda.Stream(device=DEV)
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    assert hog.hog_launch(1, 0.001, C.c_void_p(ok.data_ptr()), C.c_void_p(busy.cuda_stream)) == 0   # code loaded
+    torch.cuda.synchronize()
+    ok.zero_()
+    assert hog.hog_launch(cus - 8, hog_s, C.c_void_p(ok.data_ptr()), C.c_void_p(busy.cuda_stream)) == 0
+    time.sleep(min(0.1, hog_s / 4))                               # the hog holds its CUs before we launch
+    t_enc = time.perf_counter()
+    with torch.cuda.stream(mine):
+        c.encode_logits_job(x, sym)
+        mine.synchronize()
+        t_enc = time.perf_counter() - t_enc
+        aborted_enc = C.c_int64()
+        _lib.check(c.lib.lac_q1_group_aborted(c.ctx, C.byref(aborted_enc), c._stream))
+        got, gn = c.to_bytes()
+    torch.cuda.synchronize()
+    assert got == want and (gn == wn).all()
+    assert hog.hog_launch(cus - 8, hog_s, C.c_void_p(ok.data_ptr()), C.c_void_p(busy.cuda_stream)) == 0
+    time.sleep(min(0.1, hog_s / 4))
+    t_dec = time.perf_counter()
+    with torch.cuda.stream(mine):
+        c.decode_open()
+        dec = c.decode_logits(x)
+        mine.synchronize()
+        t_dec = time.perf_counter() - t_dec
+        aborted_dec = C.c_int64()
+        _lib.check(c.lib.lac_q1_group_aborted(c.ctx, C.byref(aborted_dec), c._stream))
+        c.raise_on_error()
+    torch.cuda.synchronize()
+    assert torch.equal(dec, sym)
+    assert int(ok.item()) == 2 * (cus - 8)                        # both hogs ran to their deadline
+    if hog_s > 0.3:
+        # the abort path was taken (which launch meets the missing partner first depends
+        # on how the dispatcher fills the free CUs: tools/contention_probe.py saw both)
+        assert aborted_enc.value or aborted_dec.value, (t_enc, t_dec)
+    c.close()

@@ -223,6 +223,39 @@ def test_headline_shape_softmax_tables():
             assert data[b][-1] & ((1 << (8 - L % 8)) - 1) == 0
 
 
+def test_c2_shape_one_stream_4096_steps():
+    """SURVEY c2 at its own shape: V=32000, ONE stream, 4096 steps of random-softmax
+    u32 tables (seeded, 524 MB).  Bytes == the C oracle; the symbols come back
+    through AUTO and every decode path; the decoder's determined count equals what
+    the reference's bit-serial run(bits, stop=0) emits (the C oracle's literal
+    restatement of it, pinned to the reference's golden counts)."""
+    from oracle import oracle as coracle
+    V, B, steps, prec = 32000, 1, 4096, 48
+    pmf, sym = synth.softmax_tables(steps, B, V, seed=2024, device=DEV)
+    c = _coder(V, B, prec, cap=steps * (prec + 2) + 256)
+    c.encode_job(pmf, sym)
+    data, n = c.to_bytes()
+    host = pmf[:, 0, :].cpu().numpy().view(np.uint32)
+    hsym = sym[:, 0].cpu().numpy()
+    out, nb, status, rc = coracle.encode_batch(host[:, None, :], hsym[:, None], prec, nthreads=1)
+    assert rc == 0 and int(nb[0]) == int(n[0]) and out[0, :(int(nb[0]) + 7) // 8].tobytes() == data[0]
+    for path in ("auto",) + DECODE_PATHS:
+        c.set_decode_path(path)
+        c.decode_open()
+        assert torch.equal(c.decode(pmf), sym), path
+    dec = coracle.decode_bitserial(host, data[0], int(n[0]), prec, max_out=steps + 64)
+    assert dec[:steps] == hsym.tolist()
+    # the decoder's own determined count over the stream and the reference's
+    c.set_decode_path("auto")
+    c.decode_open()
+    extra = len(dec) - steps
+    tail = torch.cat([pmf, pmf[-1:].expand(extra + 1, B, V)]) if extra >= 0 else pmf
+    got = c.decode(tail.contiguous())
+    assert int(c.determined()[0]) == len(dec)
+    assert got[:len(dec), 0].cpu().tolist() == dec
+    c.close()
+
+
 def test_c4_shape_softmax_tables():
     """SURVEY c4 at full size (V=128256 Llama-3 vocab, 4096 streams, u32 rows of
     513 KB): fused and split encoders byte-identical, sampled streams bit-exact

@@ -176,3 +176,19 @@ def test_restated_flush_matches_reference():
         assert got == (c["out"], c["exc"]), (c["src"], c["variant"])
         n += 1
     assert n > 2000
+
+
+def test_c_bitserial_decoder_counts_match_reference():
+    """oracle.decode_bitserial (A_from_bin.run(bits, stop=0) in C) == the reference's
+    decoded symbols, extra determined symbols included, on every small and
+    generator case."""
+    for kind in ("static", "perstep"):
+        for c in SMALL[kind]:
+            got = coracle.decode_bitserial(c["rows"], bytes.fromhex(c["bytes"]), c["L"], c["prec"])
+            assert got == c["syms"] + c["decoded_extra"], c
+    for c in GEN:
+        if "decoded_count" not in c:
+            continue
+        rows = np.stack(_gen_rows(c))
+        got = coracle.decode_bitserial(rows, bytes.fromhex(c["bytes"]), c["L"], c["prec"])
+        assert len(got) == c["decoded_count"] and got[:len(c["syms"])] == c["syms"], c["name"]
