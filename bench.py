@@ -154,8 +154,8 @@ def main():
     if args.block_waves:
         coder.set_block_waves(args.block_waves)
 
-    # N > 1: each job's bitstreams are all-gathered over RCCL into fixed-width slots,
-    # asynchronously (overlapping the next job's encode), double-buffered
+    # N > 1: each job's bitstreams go to rank 0 over RCCL, packed and sized to the
+    # payload, asynchronously (overlapping the next job's encode), double-buffered
     gatherer = BitstreamGatherer(coder) if world > 1 else None
 
     def job():
@@ -195,15 +195,25 @@ def main():
 
     # ---------------- checks, outside the timed region
     gather_ok = None
-    if gatherer:                                           # this rank's slice of the last gather == its bits
-        gb, gn = gatherer.last
-        lo = rank * B
-        mine_b = coder.copy_bits_into(torch.empty_like(gb[lo:lo + B]))
-        mine_n = coder.copy_nbits_into(torch.empty_like(gn[lo:lo + B]))
-        okg = bool(torch.equal(gb[lo:lo + B], mine_b)) and bool(torch.equal(gn[lo:lo + B], mine_n))
+    gather_info = None
+    if gatherer:                                           # the root's last job == every rank's own bits
+        from lac_amd.dist import gather_bitstreams
+        mine_b = coder.bits_tensor()
+        mine_n = coder.nbits_tensor()
+        ref_b, ref_n = gather_bitstreams(mine_b, mine_n)   # a separate, exact-width all-gather
+        okg = True
+        if rank == 0:
+            gb, gn = gatherer.last_unpacked()
+            w = min(gb.shape[1], ref_b.shape[1])
+            okg = bool(torch.equal(gn.to(ref_n.device), ref_n)) and bool(
+                torch.equal(gb[:, :w].to(ref_b.device), ref_b[:, :w]))
         flag = torch.tensor([1 if okg else 0], device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         gather_ok = bool(flag.item())
+        jobs = max(gatherer.jobs, 1)
+        gather_info = {"to_rank": 0, "link_bytes_per_job": gatherer.bytes_sent / jobs,
+                       "payload_bytes_per_job": gatherer.payload_bytes / jobs,
+                       "header_bytes_per_stream": gatherer.hdr}
     rc, err, err_step = coder.status()
     data, nbits = coder.to_bytes() if rc == 0 else ([], None)
     decode = coder.decode_logits if logits_in else coder.decode
@@ -246,6 +256,7 @@ def main():
     parity = {"round_trip_all_streams": round_trip, "stream_status_ok": rc == 0, "decode": decode_info}
     if gatherer:
         parity["gather_ok"] = gather_ok
+        parity["gather"] = gather_info
     if rank == 0:
         from oracle import oracle as coracle
         S = B if (args.cpu_streams <= 0 or args.cpu_streams > B) else args.cpu_streams
@@ -298,7 +309,7 @@ def main():
         cname = workload_name(V, B, world)                      # BASELINE.json configs
         cfg = {"workload": f"{cname}: vocab={V}, {B} streams/GPU, {T} symbols/stream per job, prec={P}, {rows}",
                "vocab": V, "streams": B, "tokens": T, "prec": P, "pmf_bits": args.pmf_bits, "input": args.input,
-               "parallelism": f"streams sharded over {world} GPU(s)" + (f", {'RCCL' if backend == 'nccl' else backend} bitstream all-gather" if world > 1 else "")}
+               "parallelism": f"streams sharded over {world} GPU(s)" + (f", {'RCCL' if backend == 'nccl' else backend} payload-sized bitstream gather to rank 0" if world > 1 else "")}
         value = world * B * T * args.steps / dt
         line = {
             "metric": METRIC if (V, B) == (32000, 4096) else

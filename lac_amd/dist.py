@@ -114,69 +114,201 @@ def _all_gather(out, inp, group, world):
         dist.all_gather(list(out.chunk(world)), inp, group=group)
 
 
+def pack_bitstreams(bits, nbits, hdr_bytes):
+    """Device-side packing, no host synchronisation: a header of every stream's bit
+    count (``hdr_bytes`` = 2 or 4 bytes each, little endian) followed by the
+    streams' bytes back to back (ceil(nbits/8) each).  Returns (payload, L):
+    ``payload`` uint8 of the worst-case size, its first ``L`` (a 0-d device
+    tensor) bytes valid."""
+    import torch
+    B, W = bits.shape
+    dev = bits.device
+    nb = nbits.to(torch.int64)
+    nbytes = (nb + 7) // 8
+    hdr = torch.stack([(nb >> (8 * i)) & 0xFF for i in range(hdr_bytes)], 1).to(torch.uint8).reshape(-1)
+    start = B * hdr_bytes + torch.cumsum(nbytes, 0) - nbytes                 # each stream's first byte
+    cap = B * hdr_bytes + B * W
+    j = torch.arange(W, device=dev)
+    dest = torch.where(j[None, :] < nbytes[:, None], start[:, None] + j[None, :],
+                       torch.full((1, 1), cap, dtype=torch.int64, device=dev))   # the rest: one dump byte
+    payload = torch.zeros(cap + 1, dtype=torch.uint8, device=dev)
+    payload[:B * hdr_bytes] = hdr
+    payload.scatter_(0, dest.reshape(-1), bits.reshape(-1))
+    L = B * hdr_bytes + nbytes.sum()
+    return payload, L
+
+
+def unpack_bitstreams(payload, streams, width, hdr_bytes):
+    """Inverse of pack_bitstreams -> (bits [streams, width] zero padded, nbits int64 [streams])."""
+    import torch
+    dev = payload.device
+    h = payload[:streams * hdr_bytes].reshape(streams, hdr_bytes).to(torch.int64)
+    nb = sum(h[:, i] << (8 * i) for i in range(hdr_bytes))
+    nbytes = (nb + 7) // 8
+    start = streams * hdr_bytes + torch.cumsum(nbytes, 0) - nbytes
+    j = torch.arange(width, device=dev)
+    src = torch.clamp(start[:, None] + j[None, :], max=payload.numel() - 1)
+    out = torch.where(j[None, :] < nbytes[:, None], payload[src], torch.zeros((), dtype=torch.uint8, device=dev))
+    return out, nb
+
+
 class BitstreamGatherer:
-    """Fixed-width, asynchronous, double-buffered bitstream all-gather for
-    back-to-back compression jobs.
+    """Bitstreams of back-to-back compression jobs gathered to one rank, sized to
+    the payload, with no host synchronisation on the GPU's path.
 
-    ``gather_bitstreams`` agrees on the widest stream first (an all-reduce and a
-    host read), which serialises every job behind two collective latencies.  A
-    job's slot width is known up front: no stream can exceed the coder's
-    capacity (``cap_words`` 8-byte words).  So each ``submit()`` copies the
-    packed bits and bit counts into one of ``depth`` slot buffers on the
-    caller's stream and enqueues the all-gathers with ``async_op=True``: RCCL
-    runs them on its own stream while the next job's encode kernel streams its
-    tables, and the caller's stream only waits for a collective when its slot is
-    about to be reused ``depth`` jobs later.  ``drain()`` makes the caller's
-    stream wait for everything still in flight.
+    Per job, on every rank (``submit``): the coder's streams are packed on the
+    device into a header of bit counts (2 bytes per stream when the coder's
+    capacity is below 2^16 bits, else 4) plus the streams' bytes back to back
+    (``pack_bitstreams``), and the packed length -- one int64 -- is all-gathered,
+    asynchronously.  The sizes reach the host through a pinned copy on a side
+    stream, so the host waits only for this job's packing, never for the next
+    job's encode, which it has already enqueued.  At the next ``submit`` (or
+    ``drain``) every rank sends exactly its packed bytes to ``root`` and the root
+    receives them (one grouped send/recv batch: RCCL over xGMI), ordered after the
+    packing only.  xGMI carries the payload, the header and 8 bytes per rank --
+    not a worst-case slot per stream, and not to every rank.
 
-    Under ``gloo`` (CPU tests, one-GPU rehearsals) the gather goes through host
-    tensors synchronously, like ``gather_bitstreams``.
+    On the root, ``last`` is the list of (payload, length) per rank of the last
+    job and ``last_unpacked()`` its streams as (bits [world * B, width], nbits).
+    ``bytes_sent`` / ``payload_bytes`` count what crossed the links and the
+    encoded bytes themselves (bench.py reports both).
+
+    Under ``gloo`` (CPU tests, one-GPU rehearsals) the same exchange runs on host
+    tensors, synchronously.
     """
 
-    def __init__(self, coder, group=None, depth: int = 2):
+    def __init__(self, coder, group=None, depth: int = 2, root: int = 0):
         import torch
         import torch.distributed as dist
-        self.coder, self.group, self.depth = coder, group, max(1, int(depth))
+        self.coder, self.group, self.depth, self.root = coder, group, max(1, int(depth)), int(root)
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.gloo = dist.get_backend(group) == "gloo"
         self.width = coder.bits_stride()                      # cap_words * 8 bytes per stream
+        self.hdr = 2 if self.width * 8 < (1 << 16) else 4
         B, dev = coder.streams, coder.device
+        self.B = B
+        self.cap = B * self.hdr + B * self.width + 1
+        self.io_dev = torch.device("cpu") if self.gloo else torch.device(dev)
         self.slots = [(torch.empty((B, self.width), dtype=torch.uint8, device=dev),
                        torch.empty((B,), dtype=torch.int64, device=dev)) for _ in range(self.depth)]
-        self.outs = [(torch.empty((self.world * B, self.width), dtype=torch.uint8, device=dev),
-                      torch.empty((self.world * B,), dtype=torch.int64, device=dev)) for _ in range(self.depth)]
-        self.pending = [None] * self.depth
+        self.recv = [[torch.empty(self.cap, dtype=torch.uint8, device=self.io_dev) for _ in range(self.world)]
+                     if self.rank == self.root else None for _ in range(self.depth)]
+        self.lens = [torch.empty(self.world, dtype=torch.int64, device=self.io_dev) for _ in range(self.depth)]
+        self.lens_host = [torch.empty(self.world, dtype=torch.int64).pin_memory()
+                          if not self.gloo and torch.cuda.is_available() else torch.empty(self.world, dtype=torch.int64)
+                          for _ in range(self.depth)]
+        self.state = [None] * self.depth                        # per slot: dict of the job in flight
+        self.side = torch.cuda.Stream(device=dev) if not self.gloo else None
         self.k = 0
         self.last = None
+        self.bytes_sent = 0
+        self.payload_bytes = 0
+        self.jobs = 0
 
+    # -- per job
     def submit(self):
-        """Gather the coder's current output; returns the (bits, nbits) output
-        buffers, valid on the caller's stream after ``drain()``."""
+        """Queue the coder's current output for the root; returns the job's slot."""
+        import torch
         import torch.distributed as dist
         i = self.k % self.depth
         self.k += 1
-        self._wait(i)                                           # slot i's previous gather is done
+        self._finish(i)                                         # slot i's previous job, if any
+        self._send_pending()                                    # the jobs queued since: their exact sends
         bits, nbits = self.slots[i]
         self.coder.copy_bits_into(bits)                          # on the caller's stream
         self.coder.copy_nbits_into(nbits)
-        ob, on = self.outs[i]
+        payload, L = pack_bitstreams(bits, nbits, self.hdr)
+        st = {"payload": payload, "nbits": nbits, "job": self.k}
         if self.gloo:
-            _all_gather(ob, bits, self.group, self.world)
-            _all_gather(on, nbits, self.group, self.world)
-        else:
-            self.pending[i] = [dist.all_gather_into_tensor(ob, bits, group=self.group, async_op=True),
-                               dist.all_gather_into_tensor(on, nbits, group=self.group, async_op=True)]
-        self.last = (ob, on)
-        return self.last
+            _all_gather(self.lens[i], L.reshape(1).to(torch.int64).cpu(), self.group, self.world)
+            st["lens"] = self.lens[i].tolist()
+            st["payload"] = payload.cpu()
+            self.state[i] = st
+            self._send(i)
+            self._finish(i)
+            return i
+        ev = torch.cuda.Event()
+        ev.record()                                             # packing done (caller's stream)
+        work = dist.all_gather_into_tensor(self.lens[i], L.reshape(1).to(torch.int64), group=self.group,
+                                           async_op=True)
+        with torch.cuda.stream(self.side):
+            self.side.wait_event(ev)
+            work.wait()                                         # the side stream waits for the sizes
+            self.lens_host[i].copy_(self.lens[i], non_blocking=True)
+            st["lens_ready"] = torch.cuda.Event()
+            st["lens_ready"].record(self.side)
+        st["packed"] = ev
+        self.state[i] = st
+        return i
 
-    def _wait(self, i):
-        if self.pending[i]:
-            for w in self.pending[i]:
-                w.wait()                                        # caller's stream waits; the host does not
-            self.pending[i] = None
+    def _send_pending(self):
+        """Post the sends of every queued job, oldest first (point-to-point order
+        must match between each rank and the root)."""
+        for _, i in sorted((st["job"], i) for i, st in enumerate(self.state) if st is not None):
+            self._send(i)
+
+    def _send(self, i):
+        """Post job i's exact-size send (every rank) / receives (root), once its
+        sizes are on the host."""
+        import torch
+        import torch.distributed as dist
+        st = self.state[i]
+        if st is None or "works" in st:
+            return
+        if "lens" not in st:
+            st["lens_ready"].synchronize()                      # this job's packing + size gather only
+            st["lens"] = self.lens_host[i].tolist()
+        lens = st["lens"]
+        ops = []
+        if self.rank == self.root:
+            for r in range(self.world):
+                if r != self.root:
+                    ops.append(dist.P2POp(dist.irecv, self.recv[i][r][:lens[r]], r, group=self.group))
+        else:
+            ops.append(dist.P2POp(dist.isend, st["payload"][:lens[self.rank]], self.root, group=self.group))
+        ctx = torch.cuda.stream(self.side) if not self.gloo else _nullctx()
+        with ctx:
+            if not self.gloo:
+                self.side.wait_event(st["packed"])
+            st["works"] = dist.batch_isend_irecv(ops) if ops else []
+        if self.rank == self.root:                              # the root's own share: a local copy
+            self.recv[i][self.root][:lens[self.root]].copy_(st["payload"][:lens[self.root]], non_blocking=True)
+        self.bytes_sent += sum(lens) - lens[self.root] + 8 * self.world
+        self.payload_bytes += sum(lens) - self.world * self.B * self.hdr
+        self.jobs += 1
+
+    def _finish(self, i):
+        import torch
+        st = self.state[i]
+        if st is None:
+            return
+        self._send_pending()                                    # older jobs first, then this one
+        for w in st["works"]:
+            w.wait()
+        if not self.gloo:
+            torch.cuda.current_stream().wait_stream(self.side)   # later work sees the received bytes
+        if self.rank == self.root:
+            self.last = [(self.recv[i][r], st["lens"][r]) for r in range(self.world)]
+        self.state[i] = None
 
     def drain(self):
-        for i in range(self.depth):
-            self._wait(i)
+        """Complete every job in flight (the caller's stream waits for them)."""
+        self._send_pending()
+        for _, j in sorted((st["job"], j) for j, st in enumerate(self.state) if st is not None):
+            self._finish(j)
         return self.last
+
+    def last_unpacked(self):
+        """Root: the last job's streams as (bits [world * B, width], nbits [world * B])."""
+        import torch
+        parts = [unpack_bitstreams(p[:n], self.B, self.width, self.hdr) for p, n in self.last]
+        return torch.cat([p[0] for p in parts]), torch.cat([p[1] for p in parts])
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False

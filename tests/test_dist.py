@@ -85,39 +85,68 @@ class _FakeCoder:
         out.copy_(self.nbits)
 
 
-def _gatherer_worker(rank, world, port, q):
+def _gatherer_worker(rank, world, port, q, streams, stride, jobs):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    coder = _FakeCoder(3, 24, seed=100 + rank)
+    coder = _FakeCoder(streams, stride, seed=100 + rank)
     g = BitstreamGatherer(coder, depth=2)
-    jobs = []
-    for _ in range(5):                                  # more jobs than slots: slots are reused
+    out = []
+    for _ in range(jobs):                               # more jobs than slots: slots are reused
         coder.new_job()
-        ob, on = g.submit()
-        jobs.append((coder.bits.clone(), coder.nbits.clone(), ob.clone(), on.clone()))
+        g.submit()
+        got = g.last_unpacked() if rank == 0 else None
+        out.append((coder.bits.tolist(), coder.nbits.tolist(),
+                    None if got is None else (got[0].tolist(), got[1].tolist())))
     g.drain()
-    q.put((rank, [(b.tolist(), n.tolist(), ob.tolist(), on.tolist()) for b, n, ob, on in jobs]))
+    q.put((rank, out, g.bytes_sent, g.payload_bytes, g.jobs, g.hdr))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_bitstream_gatherer_gloo_world2():
+def _run_gatherer(streams, stride, jobs):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_gatherer_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_gatherer_worker, args=(r, 2, port, q, streams, stride, jobs)) for r in range(2)]
     for p in ps:
         p.start()
-    res = dict(q.get(timeout=120) for _ in range(2))
+    res = {r[0]: r[1:] for r in (q.get(timeout=180) for _ in range(2))}
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for j in range(5):
-        b0, n0, ob0, on0 = res[0][j]
-        b1, n1, ob1, on1 = res[1][j]
-        assert ob0 == ob1 == b0 + b1                    # fixed-width slots: every byte travels
-        assert on0 == on1 == n0 + n1
+    return res
+
+
+def _check_root(res, jobs):
+    for j in range(jobs):
+        b0, n0, got = res[0][0][j]
+        b1, n1, _ = res[1][0][j]
+        bits, nbits = got
+        assert nbits == n0 + n1                          # the root holds every stream's bit count
+        for row, want, n in zip(bits, b0 + b1, n0 + n1):
+            nb = (n + 7) // 8
+            assert row[:nb] == want[:nb] and not any(row[nb:])   # exactly the stream's bytes
+
+
+def test_bitstream_gatherer_gloo_world2():
+    """Jobs through the payload-sized gather to rank 0: the root holds every
+    stream's bytes and bit count, exactly; 2-byte headers (capacity < 2^16 bits)."""
+    res = _run_gatherer(3, 24, 5)
+    _check_root(res, 5)
+    assert res[0][4] == 2
+
+
+def test_bitstream_gatherer_long_job_sized_to_payload():
+    """A long job (4096 symbols x 50 bits of capacity per stream): what crosses the
+    links per job stays within 1.2x the encoded bytes, where
+    the fixed-width slots of round 2 moved the whole capacity to every rank."""
+    stride = (4096 * 50 + 256) // 8
+    res = _run_gatherer(6, stride, 3)
+    _check_root(res, 3)
+    sent = res[0][1]                                    # (every rank counts the whole job)
+    payload = res[0][2]
+    assert res[0][4] == 4 and payload > 0 and sent <= 1.2 * payload, (sent, payload)
 
 
 def _scatter_worker(rank, world, port, q):
