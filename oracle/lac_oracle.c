@@ -289,8 +289,8 @@ int lacref_decode(const void *pmf, int elem_bytes, int64_t V, int64_t nsym, int6
 /* A_from_bin.run(bits, stop=0) literally (arith_code.py:264-299, :322-326): per
  * bit receive_bit halves [lb, hb]; while val_to_symbol of both window ends agree,
  * emit_symbol (with its overlap check) and the emit_bit loop over l, h, lb, hb.
- * Rows: step t uses row min(t, nrows-1).  Writes at most max_out symbols and
- * returns how many the bits determine (or a negative status). */
+ * Rows: step t uses row min(t, nrows-1).  Returns how many symbols the bits
+ * determine, at most max_out (or a negative status). */
 int64_t lacref_decode_bitserial(const void *pmf, int elem_bytes, int64_t V, int64_t nrows, int64_t step_stride,
                                 const uint8_t *bytes, uint64_t nbits, int prec, int32_t *syms_out,
                                 int64_t max_out) {
@@ -324,8 +324,8 @@ int64_t lacref_decode_bitserial(const void *pmf, int elem_bytes, int64_t V, int6
             if (region_overlap(l + (int64_t)a, l + (int64_t)b - 1, lb, hb) == 0) { rc = R_E_DECODE_RANGE; break; }
             h = l + (int64_t)b - 1;
             l += (int64_t)a;
-            if (n < max_out) syms_out[n] = (int32_t)ls;
-            n++;
+            if (n >= max_out) break;      /* a one-symbol row determines symbols forever (the reference loops) */
+            syms_out[n++] = (int32_t)ls;
             while (h - l < Hd) {
                 const int64_t d = floordiv(l, Hd);
                 l = l * 2 - d * D;

@@ -147,3 +147,16 @@ def test_cr_ratio_is_pythons_division(core):
         a = max(0, min(a, b))
         want = struct.unpack("<Q", struct.pack("<d", a / b))[0]
         assert core.cc_cr_ratio(a, b) == want, (a, b)
+
+
+def test_host_arithmetic_and_oracle_under_sanitizers():
+    """AddressSanitizer + UndefinedBehaviorSanitizer build of the kernels' host-side
+    arithmetic (lac_core.h via core_check.cpp) and the C oracle, cross-checked on
+    seeded random inputs by tests/native/sanitize_main.cpp (make -C tests/native asan)."""
+    native = os.path.join(REPO, "tests", "native")
+    subprocess.run(["make", "-s", "-C", native, "asan"], check=True)
+    r = subprocess.run([os.path.join(native, "_asan", "sanitize_check")], capture_output=True, text=True, timeout=600)
+    report = r.stdout + r.stderr
+    assert r.returncode == 0, report[-3000:]
+    assert "sanitize_main: ok" in report
+    assert "runtime error" not in report and "AddressSanitizer" not in report
