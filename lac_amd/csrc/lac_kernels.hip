@@ -2350,6 +2350,9 @@ typedef __attribute__((address_space(3))) void lvoid_t;
 // exceeds the CU count (one block per CU: every member is resident), and the wait
 // is bounded: a partner that never posts poisons the row's total (+2^62:
 // LAC_E_TABLE at the coder) instead of hanging the GPU.
+#ifndef LAC_Q1_GROUP_NOWAIT
+#define LAC_Q1_GROUP_NOWAIT 0
+#endif
 constexpr uint32_t kGroupSpinMax = 1u << 17;                 // polls (s_sleep 2 + a device-scope load each): ~0.1 s,
                                                              // far beyond any wait for a resident partner
 
@@ -2383,6 +2386,10 @@ __device__ inline uint32_t group_exchange(uint64_t *xch, uint64_t *abortw, int g
                        __HIP_MEMORY_SCOPE_AGENT);
     uint32_t acc = m;
     bool all = group_ld(abortw) == 0;
+#if LAC_Q1_GROUP_NOWAIT                                          // timing experiment only: wrong tables
+    *ok = true;
+    return acc;
+#endif
 #pragma unroll
     for (int k = 0; k < K; k++) {
         const unsigned pb = (g0 + k) * 8 + xcd;
