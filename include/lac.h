@@ -88,12 +88,14 @@ enum {                       /* lac_set_option */
                                       when the row fits a trimmed last slot, <= 16064 vectors),
                                       16 = 15 with 8 table copies always, 17 / 18 = the same
                                       register + LDS form with 4 rows of <= 4096 / 2 rows of
-                                      <= 8192 vectors per 16-wave block, 19 = one row of
-                                      16385..65536 vectors over a group of 2..4 16-wave blocks
-                                      (one segment each in the form of 15; f32 V = 128256 /
-                                      151936 / 262144, bf16 V = 256000), 20 = 19 with two rows
-                                      of segments of <= 8192 vectors per block (bf16 V =
-                                      151936, f32 V = 65540); identical results, only speed
+                                      <= 8192 vectors per 16-wave block, 19 / 20 / 21 = row
+                                      groups: a row of > 16384 vectors in 2..16 segments, one
+                                      per row slot of 1 / 2 / 4 rows per 16-wave block (the
+                                      forms of 15 / 18 / 17; slots are numbered across the
+                                      blocks of an XCD, so a segment count need not divide
+                                      the blocks); AUTO picks the form that fills its slots
+                                      best (bf16 V = 151936: 5 slots of 4 rows per block,
+                                      f32 V = 128256: 2 of 1); identical results, only speed
                                       differs */
     LAC_OPT_DECODE_FINE = 7,       /* one-wave decode (FUSED path): 1 = one total per 64 vectors of
                                       the row, so only 1 KB is re-read after the search (default,
@@ -257,8 +259,8 @@ int lac_encode_logits(lac_ctx *ctx, const void *logits_dev, int logit_type, int6
 int lac_decode_logits_steps(lac_ctx *ctx, const void *logits_dev, int logit_type, int64_t step_stride,
                             int64_t stream_stride, int64_t steps, int32_t *sym_out_dev, void *stream);
 
-/* Rows longer than a CU holds (LAC_OPT_Q1_SHAPE 19 / 20, AUTO for e.g. f32 V =
- * 128256) are split over groups of 2..4 workgroups that exchange each row's
+/* Rows longer than a CU holds (LAC_OPT_Q1_SHAPE 19 / 20 / 21, AUTO for e.g. f32 V =
+ * 128256) are split over 2..16 row slots of workgroups that exchange each row's
  * maximum, which needs every member resident.  When a member is not (another
  * kernel holds CUs) the waiting ones give up after ~0.1 s, raise the launch's
  * abort flag, and a tiled two-pass launch queued behind it recomputes every row:

@@ -404,7 +404,7 @@ class BatchCoder:
         return out
 
     def set_q1_shape(self, shape: int):
-        """Logits row-stats block shape (0 auto, 1..20 forced, include/lac.h
+        """Logits row-stats block shape (0 auto, 1..21 forced, include/lac.h
         LAC_OPT_Q1_SHAPE; identical results)."""
         check(self.lib.lac_set_option(self.ctx, _lib.LAC_OPT_Q1_SHAPE, int(shape)))
 

@@ -2336,20 +2336,33 @@ typedef __attribute__((address_space(3))) void lvoid_t;
 // IMAX fallback (float max, with its own barrier) is taken by the whole block if
 // any of its rows needs it.
 //
-// KG > 1 ("pairs", groups): rows longer than one CU's registers + LDS hold (f32 V =
+// GROUP (row groups): rows longer than one CU's registers + LDS hold (f32 V =
 // 128256: Llama-3's vocab in f32; bf16 / f32 V = 151936 (Qwen2), 256000 (Gemma))
-// split over a group of KG = 2..4 blocks, each holding one segment of <= 16384
-// vectors exactly as above.  The segments meet twice per row: the row maximum
-// (each block posts its segment's maximum with the row's sequence number into one
-// of two alternating words and polls its partners': the only wait), and the sums
-// (each segment adds its partials -- total, lo, hi, or its 64 chunk partials --
-// into the row's zeroed outputs with relaxed device-scope atomics: no wait, and no
-// fence -- a release/acquire fence here writes back / invalidates the whole L2 and
-// cost ~35 us per row).  A group shares an XCD (blocks slot * 8 + xcd of KG
-// consecutive slots; dispatch is round-robin over the 8 XCDs), the grid never
+// split into kg segments of `split` vectors (the last one the rest), each held by
+// one row slot (NT threads) of some block exactly as above.  Row slots are
+// numbered per XCD -- slot q = (block / 8) * NRB + row-in-block of the blocks
+// b = j * 8 + xcd (dispatch is round-robin over the 8 XCDs) -- and slot q holds
+// segment q % kg of the XCD's row q / kg of the round: rpx rows per XCD per round,
+// slots past rpx * kg idle (no loads).  Segments need not line up with blocks, so
+// kg is free of the block count: with 4 rows of <= 4096 vectors per block a bf16
+// Qwen2 row (18992 vectors) takes 5 slots at 93 % of their capacity, where whole
+// blocks (kg = 2..4 of one or two rows each) held 77 % with 16 of 256 CUs idle.
+// The segments meet twice per row: the row maximum (each slot posts its segment's
+// maximum with its sequence number into one of two alternating words and polls
+// its partners': the only wait; a slot's sequence counts its own exchanges, so a
+// row that needs the float-max fallback exchanges once more without desynchronising
+// the block's other rows), and the sums (each segment adds its partials -- total,
+// lo, hi, or its 64 chunk partials -- into the row's zeroed outputs with relaxed
+// device-scope atomics: no wait, and no fence -- a release/acquire fence here
+// writes back / invalidates the whole L2 and cost ~35 us per row).  The grid never
 // exceeds the CU count (one block per CU: every member is resident), and the wait
 // is bounded: a partner that never posts poisons the row's total (+2^62:
 // LAC_E_TABLE at the coder) instead of hanging the GPU.
+// The exchange's wait costs ~6 points of peak at bf16 Qwen2 (the same kernel without
+// it: 75 vs 69 %, wrong tables; profiles/r03/q1_slots/ab_nrb4).  Neither running the
+// previous row's epilogue between the post and the poll (ab_late) nor per-row LDS
+// barriers with odd rows started half a round late, so that other rows stream while
+// one waits (ab_rowbar, ab_rbo), recovered any of it.
 #ifndef LAC_Q1_GROUP_NOWAIT
 #define LAC_Q1_GROUP_NOWAIT 0
 #endif
@@ -2368,33 +2381,42 @@ __device__ inline uint64_t group_ld(const uint64_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// post this block's 32-bit value (a row maximum; sequence number seq >= 1, one per
-// exchange: a block posts seq + 1 only after reading all its partners' seq, so no
-// partner's word for seq is overwritten unread) and fold in the K - 1 partners'
-// (blocks ((slot / K) * K + k) * 8 + xcd) with op; *ok = false when one never came
-// (NRB rows per block: row g of the block uses word pair b * NRB + g)
+// post this row slot's 32-bit value (a row maximum; sequence number seq >= 1, one
+// per exchange of this slot: a slot posts seq + 1 only after reading all its
+// partners' seq, so no partner's word for seq is overwritten unread) and fold in
+// the kg - 1 partners' (slots q0 .. q0 + kg - 1 of this XCD, q0 = (q / kg) * kg)
+// with op; *ok = false when one never came.  Slot q = (b / 8) * NRB + g of block b
+// uses word pair b * NRB + g.
 // The launch's abort word (after the exchange words, zeroed with them): a block
 // whose partner did not post within kGroupSpinMax polls -- not resident, e.g.
 // while another kernel holds CUs -- sets it; every block then stops waiting at
 // once (its rows are poisoned) and the gated tiled launch queued behind this one
 // (q1_group_kernel) recomputes every row without row groups.
-template <int K, int NRB, typename Op>
-__device__ inline uint32_t group_exchange(uint64_t *xch, uint64_t *abortw, int g, uint32_t seq, uint32_t m, Op op,
-                                          bool *ok) {
-    const unsigned b = blockIdx.x, sl = seq & 1, xcd = b & 7, g0 = ((b >> 3) / K) * K;
-    __hip_atomic_store(&xch[2 * (b * NRB + g) + sl], ((uint64_t)seq << 32) | m, __ATOMIC_RELAXED,
+// Posting (group_post: one lane) and polling (group_poll: a whole wave, the row's
+// first: lane k < kg polls partner slot q0 + k, so the kg - 1 words' L2 round trips
+// overlap instead of queueing one after another; the lanes' values are folded with
+// op, a wave reduction) are separate, so other work can run between them.
+template <int NRB>
+__device__ inline void group_post(uint64_t *xch, int g, uint32_t seq, uint32_t m) {
+    const unsigned b = blockIdx.x;
+    __hip_atomic_store(&xch[2 * (b * NRB + g) + (seq & 1)], ((uint64_t)seq << 32) | m, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
-    uint32_t acc = m;
-    bool all = group_ld(abortw) == 0;
+}
+template <int NRB, typename Op>
+__device__ inline uint32_t group_poll(uint64_t *xch, uint64_t *abortw, int g, int kg, uint32_t seq, uint32_t m,
+                                      Op op, bool *ok) {
+    const unsigned b = blockIdx.x, sl = seq & 1, xcd = b & 7, q = (b >> 3) * NRB + g, q0 = (q / kg) * kg;
+    const unsigned lane = (unsigned)lane_fresh();
 #if LAC_Q1_GROUP_NOWAIT                                          // timing experiment only: wrong tables
     *ok = true;
-    return acc;
+    return m;
 #endif
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-        const unsigned pb = (g0 + k) * 8 + xcd;
-        if (pb == b || !all) continue;
-        const uint64_t *px = &xch[2 * (pb * NRB + g) + sl];
+    const unsigned pq = q0 + lane;
+    uint32_t val = m;                                            // lanes without a partner hold the neutral m
+    bool fine = true;
+    if (lane < (unsigned)kg && pq != q && group_ld(abortw) == 0) {
+        const unsigned pb = (pq / NRB) * 8 + xcd;
+        const uint64_t *px = &xch[2 * (pb * NRB + pq % NRB) + sl];
         uint64_t v = group_ld(px);
         uint32_t n = 0;
         for (; (uint32_t)(v >> 32) != seq && n < kGroupSpinMax; n++) {
@@ -2403,14 +2425,16 @@ __device__ inline uint32_t group_exchange(uint64_t *xch, uint64_t *abortw, int g
             v = group_ld(px);
         }
         if ((uint32_t)(v >> 32) != seq) {
-            all = false;
+            fine = false;
             if (n >= kGroupSpinMax)
                 __hip_atomic_store(abortw, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        acc = op(acc, (uint32_t)v);
+        val = (uint32_t)v;
+    } else if (lane < (unsigned)kg && pq != q) {
+        fine = false;                                            // the launch already gave up
     }
-    *ok = all;
-    return acc;
+    *ok = __ballot(!fine) == 0;
+    return wave_reduce(val, op);
 }
 
 // fmaxf of two segments' maxima (as bits): folded over all, = fmaxf over the whole row
@@ -2423,19 +2447,17 @@ __device__ inline void group_add(uint64_t *p, uint64_t v) {
 }
 constexpr uint64_t kGroupPoison = 1ull << 62;                 // a failed exchange: the row's total is >= 2^62
 
-template <typename LT, bool DEC, int REP = kRLRep, int LASTN = 1024, int NT = 1024, int KG = 1>
+template <typename LT, bool DEC, int REP = kRLRep, int LASTN = 1024, int NT = 1024, bool GROUP = false>
 __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ lg, int64_t step_stride,
                                                          int64_t stream_stride, const int32_t *__restrict__ sym,
                                                          int64_t B, int64_t rows, int64_t V, int64_t t0, uint32_t xsh,
                                                          int64_t G, RowStats *__restrict__ out,
                                                          uint64_t *__restrict__ chunks, float *__restrict__ mrow,
-                                                         uint64_t *__restrict__ xch, int split) {
+                                                         uint64_t *__restrict__ xch, int split, int kg, int rpx) {
     constexpr int N = LogitN<LT>::N, R = 8, L = 8, NW = 16, NRB = 1024 / NT, NWR = NT / 64;
     constexpr int SL = (L - 1) * NT + LASTN;                   // slot vectors per row
     constexpr bool IMAX = LAC_Q1_IMAX && sizeof(LT) == 2;
     static_assert((R + L) * N <= 128, "lane sums must fit 32 bits");
-    constexpr bool GROUP = KG > 1;                              // a row over a group of KG blocks
-    static_assert(!GROUP || NT >= 512, "groups: one or two row segments per block");
     // (not the bf16 8-copy decode forms, which sit at the 128-VGPR cap: two more live
     // registers there add spills)
     constexpr bool DEFER = LAC_Q1_DEFER && !(sizeof(LT) == 2 && REP == kRLRep);
@@ -2456,34 +2478,54 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
     // kernel at its 128-VGPR cap: 2.52 -> 2.70 ms at bf16 V = 128256)
     q1_load_tab_rep<REP>(tabr, xsh);
     const uint32_t loff = (uint32_t)(lane & (REP - 1)) << 2;
-    // GROUP: block b = slot * 8 + xcd holds segment hh = slot % KG of the rows of group
-    // (slot / KG) * 8 + xcd; segments are split vectors long, the last one the rest
-    const int slotb = (int)(blockIdx.x >> 3);
-    const int hh = GROUP ? slotb % KG : 0;
-    const int64_t bix = GROUP ? (int64_t)((slotb / KG) * 8 + (blockIdx.x & 7)) : (int64_t)blockIdx.x;
+    // GROUP: row slot q (of this XCD) holds segment hh = q % kg of the XCD's row q / kg
+    // of each round (rows r = round * 8 * rpx + (q / kg) * 8 + xcd); segments are split
+    // vectors long, the last one the rest; slots past rpx * kg are idle
+    const int sq = (int)(blockIdx.x >> 3) * NRB + g;
+    const int hh = GROUP ? sq % kg : 0;
+    const bool idle = GROUP && sq / kg >= rpx;                  // wave-uniform
     const int vofs = hh * split;                                // vectors of the row before this segment
-    const int nvec = GROUP ? (hh < KG - 1 ? split : (int)(V / N) - (KG - 1) * split) : (int)(V / N);
+    const int nvec = GROUP ? (idle ? 1 : hh < kg - 1 ? split : (int)(V / N) - (kg - 1) * split) : (int)(V / N);
     // TRIM: waves past LASTN have no last slot (their vectors there lie beyond the row)
     const bool noslot = TRIM && wg * 64 >= LASTN;
-    const int64_t stride = (int64_t)(gridDim.x / KG) * NRB;
+    // rows r = base + roff, base = b0, b0 + stride, ... < rows (the same count in every
+    // block of a group launch: partners exchange once per round)
+    const int64_t stride = GROUP ? 8 * (int64_t)rpx : (int64_t)gridDim.x * NRB;
+    const int64_t b0 = GROUP ? 0 : (int64_t)blockIdx.x * NRB;
+    const int64_t roff = GROUP ? (int64_t)(sq / kg) * 8 + (blockIdx.x & 7) : g;
     auto row_of = [&](int64_t r) {
         return lg + (t0 + r / B) * step_stride + (r % B) * stream_stride + (int64_t)vofs * N;
     };
     __shared__ uint32_t sxv[NRB];
     __shared__ int sxok[NRB];
-    uint32_t seq = 0;                                           // GROUP: exchanges done
+    __shared__ int sxact[NRB];
+    uint32_t seq = 0;                                           // GROUP: this row slot's exchanges
     bool pok = true;                                            // GROUP: every exchange of this row came
-    // GROUP: this segment's value for the row, folded with the partners' (block-wide)
-    auto group_combine = [&](uint32_t v, auto op) {
-        seq++;
-        if (tid == g * NT) {                                    // each row's leader
-            bool ok;
-            sxv[g] = group_exchange<KG, NRB>(xch, xch + 2 * NRB * gridDim.x, g, seq, v, op, &ok);
-            sxok[g] = ok;
+    // GROUP: this segment's value v for the row, posted, and then folded with the
+    // partners' (block-wide calls with the same v and act; only rows with act --
+    // row-uniform, and the same in every segment of a row -- exchange, the others
+    // keep v)
+    auto group_post_v = [&](uint32_t v, bool act) {
+        seq += act ? 1 : 0;
+        if (act && tid == g * NT) group_post<NRB>(xch, g, seq, v);
+    };
+    auto group_poll_v = [&](uint32_t v, bool act, auto op) {
+        if (wg == 0) {                                          // each row's first wave (wave-uniform)
+            bool ok = true;
+            const uint32_t res = act ? group_poll<NRB>(xch, xch + 2 * NRB * gridDim.x, g, kg, seq, v, op, &ok) : v;
+            if (tid == g * NT) {
+                sxv[g] = res;
+                sxok[g] = ok;
+                sxact[g] = act;
+            }
         }
         __syncthreads();
         pok = pok && sxok[g] != 0;
         return sxv[g];
+    };
+    auto group_combine = [&](uint32_t v, bool act, auto op) {
+        group_post_v(v, act);
+        return group_poll_v(v, act, op);
     };
     int64_t pend_r = -1;                                        // DEC, LAC_Q1_DEFER: a row's chunk totals
     uint64_t pend = 0;                                          //   (lane ln: chunk ln) not yet stored
@@ -2508,7 +2550,7 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
     // vmcnt(0) before pass 1 reads any slot, lgkmcnt(0) before a slot is refilled.
     const uint32_t slot_base = (uint32_t)(uintptr_t)(lvoid_t *)&slots[g * SL + wg * 64];   // wave-uniform
     auto ld_lds = [&](const LT *rw, int k) {
-        if (k == L - 1 && noslot) return;                      // wave-uniform
+        if ((k == L - 1 && noslot) || idle) return;            // wave-uniform
         const u32x4 *src = reinterpret_cast<const u32x4 *>(rw) + vidx(R + k);
         uint32_t keep;
         asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
@@ -2516,23 +2558,63 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
                      : "v"(src), "s"(slot_base + (uint32_t)(k * NT * 16))
                      : "memory");
     };
+    // a row's epilogue, after the barrier that follows its pass 2: its partials (wave
+    // sums, the symbol's entry, DEC: group totals) into the outputs
+    auto epilogue = [&](int64_t er, bool eok) {
+        if constexpr (DEC) {
+            if (wg == 0 && er >= 0) {
+                // chunk c = groups [c G, (c + 1) G) of the row's ngrp groups
+                // GROUP: this segment's groups are the row's [gofs, gofs + ngrp) (split is a multiple of 64)
+                const int ngrp = (nvec + 63) / 64, ln = lane_fresh(), gofs = vofs / 64;
+                const int g0 = ln * (int)G, ga = g0 > gofs ? g0 : gofs;
+                const int gb = g0 + (int)G < gofs + ngrp ? g0 + (int)G : gofs + ngrp;
+                uint64_t ct = 0;
+                for (int gi = ga; gi < gb; gi++) ct += gtot[g * NWR * (R + L) + gi - gofs];
+                pend = ct + (GROUP && !eok ? kGroupPoison : 0);
+                pend_r = er;
+                if (!DEFER) flush_chunks();
+            }
+        } else if (gti() == 0) {
+            const uint64_t ps = sps[g];
+            if (er < 0) return;
+            uint64_t T = 0, Ls = 0;
+#pragma unroll
+            for (int i = 0; i < NWR; i++) { T += ssum[g * NWR + i][0]; Ls += ssum[g * NWR + i][1]; }
+            if constexpr (GROUP) {                              // the segments' partials add up
+                RowStats *o = out + er;                        // (zeroed; inv_tot 0: the coder divides)
+                group_add(&o->tot, T + (eok ? 0 : kGroupPoison));
+                group_add(&o->lo, Ls);
+                group_add(&o->hi, Ls + ps);
+                if (hh == 0) __hip_atomic_store(&o->minp, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                RowStats st;
+                st.lo = Ls;
+                st.hi = Ls + ps;
+                st.tot = T;
+                st.minp = 1;
+                st.inv_tot = 1.0 / (double)T;
+                st.pad = 0;
+                out[er] = st;
+            }
+        }
+    };
     u32x4 x[R];
     {                                                          // the block's first rows
-        const int64_t r0 = bix * NRB + g;
+        const int64_t r0 = b0 + roff;
         const LT *rw = r0 < rows ? row_of(r0) : lg;
-        const RowSrc<true, sizeof(LT)> src(rw, true, nvec);
+        const RowSrc<true, sizeof(LT)> src(rw, true, idle ? 0 : nvec);   // idle: no loads (out of range: 0)
 #pragma unroll
         for (int k = 0; k < L; k++) ld_lds(rw, k);
 #pragma unroll
         for (int j = 0; j < R; j++) x[j] = ld_reg(src, j);
     }
-    for (int64_t rb = bix * NRB; rb < rows; rb += stride) {
+    for (int64_t rb = b0; rb < rows; rb += stride) {
         // tid opaque per row: the per-load addresses derived from it are recomputed
         // next to each load, not hoisted out of the loop and spilled (a spill reload
         // is a VM load: its vmcnt(0) would drain the prefetches)
         asm volatile("" : "+v"(tid));
-        const int64_t r = rb + g;
-        const bool valid = r < rows;
+        const int64_t r = rb + roff;
+        const bool valid = !idle && r < rows;
         const int64_t rn = r + stride;
         const LT *nrow = rn < rows ? row_of(rn) : lg;
         // pass 1: the row maximum over registers and slots (everything has landed)
@@ -2575,13 +2657,16 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
                 all_ok = all_ok && bm >= 0 && bm <= 0x7F80;
                 bi = gg == g ? bm : bi;
             }
+            bool my_ok = true;                                 // GROUP: this row's combined int max usable
             if constexpr (GROUP) {                              // one row: the int max of all segments
-                bi = (int)group_combine((uint32_t)bi, [](uint32_t a, uint32_t b) {
+                bi = (int)group_combine((uint32_t)bi, valid, [](uint32_t a, uint32_t b) {
                     return (int)a > (int)b ? a : b;
                 });
-                all_ok = true;                                 // (block-uniform: every row's combined max)
+                my_ok = !valid || (bi >= 0 && bi <= 0x7F80);
+                all_ok = true;                                 // (block-uniform: every exchanging row's combined max)
 #pragma unroll
-                for (int gg = 0; gg < NRB; gg++) all_ok = all_ok && (int)sxv[gg] >= 0 && (int)sxv[gg] <= 0x7F80;
+                for (int gg = 0; gg < NRB; gg++)
+                    all_ok = all_ok && (!sxact[gg] || ((int)sxv[gg] >= 0 && (int)sxv[gg] <= 0x7F80));
             }
             if (all_ok) {                                      // (see k_q1_stats)
                 m = __uint_as_float((uint32_t)bi << 16);
@@ -2603,7 +2688,11 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
                 m = smax[g * NWR];
 #pragma unroll
                 for (int i = 1; i < NWR; i++) m = fmaxf(m, smax[g * NWR + i]);
-                if constexpr (GROUP) m = __uint_as_float(group_combine(__float_as_uint(m), [](uint32_t a, uint32_t b) { return f32_max_bits(a, b); }));
+                if constexpr (GROUP) {                          // only the rows whose int max failed exchange again
+                    const float mf = __uint_as_float(group_combine(
+                        __float_as_uint(m), valid && !my_ok, [](uint32_t a, uint32_t b) { return f32_max_bits(a, b); }));
+                    m = my_ok ? __uint_as_float((uint32_t)bi << 16) : mf;
+                }
             }
         } else {
             float mx = -INFINITY;
@@ -2624,7 +2713,9 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
             m = smax[g * NWR];
 #pragma unroll
             for (int i = 1; i < NWR; i++) m = fmaxf(m, smax[g * NWR + i]);
-            if constexpr (GROUP) m = __uint_as_float(group_combine(__float_as_uint(m), [](uint32_t a, uint32_t b) { return f32_max_bits(a, b); }));
+            if constexpr (GROUP)
+                m = __uint_as_float(group_combine(__float_as_uint(m), valid,
+                                                  [](uint32_t a, uint32_t b) { return f32_max_bits(a, b); }));
         }
         if (DEC && valid && gti() == 0 && hh == 0) mrow[r] = m;   // now: m is not held over pass 2
         if constexpr (DEC) flush_chunks();                    // the previous row's (LAC_Q1_DEFER)
@@ -2668,7 +2759,7 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
             }
             (void)v;
         };
-        const RowSrc<true, sizeof(LT)> nsrc(nrow, true, nvec);
+        const RowSrc<true, sizeof(LT)> nsrc(nrow, true, idle ? 0 : nvec);
         // DEC: the 64-vector group totals of one half (vectors j0 .. j0+7) into the bins,
         // by wave_multi_sum32<8>'s butterfly run as the sums appear: vectors are taken in
         // the order 0 4 2 6 1 5 3 7 and each halving step runs once both of its inputs
@@ -2723,40 +2814,7 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
             if (lane == 0) { ssum[w][0] = t64; ssum[w][1] = l64; }
         }
         __syncthreads();
-        if (DEC) {
-            if (wg == 0 && valid) {
-                // chunk c = groups [c G, (c + 1) G) of the row's ngrp groups
-                // GROUP: this segment's groups are the row's [gofs, gofs + ngrp) (split is a multiple of 64)
-                const int ngrp = (nvec + 63) / 64, ln = lane_fresh(), gofs = vofs / 64;
-                const int g0 = ln * (int)G, ga = g0 > gofs ? g0 : gofs;
-                const int gb = g0 + (int)G < gofs + ngrp ? g0 + (int)G : gofs + ngrp;
-                uint64_t ct = 0;
-                for (int gi = ga; gi < gb; gi++) ct += gtot[g * NWR * (R + L) + gi - gofs];
-                pend = ct + (GROUP && !pok ? kGroupPoison : 0);
-                pend_r = r;
-                if (!DEFER) flush_chunks();
-            }
-        } else if (gti() == 0 && valid) {
-            uint64_t T = 0, Ls = 0, ps = sps[g];
-#pragma unroll
-            for (int i = 0; i < NWR; i++) { T += ssum[g * NWR + i][0]; Ls += ssum[g * NWR + i][1]; }
-            if constexpr (GROUP) {                              // the segments' partials add up
-                RowStats *o = out + r;                         // (zeroed; inv_tot 0: the coder divides)
-                group_add(&o->tot, T + (pok ? 0 : kGroupPoison));
-                group_add(&o->lo, Ls);
-                group_add(&o->hi, Ls + ps);
-                if (hh == 0) __hip_atomic_store(&o->minp, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                continue;
-            }
-            RowStats st;
-            st.lo = Ls;
-            st.hi = Ls + ps;
-            st.tot = T;
-            st.minp = 1;
-            st.inv_tot = 1.0 / (double)T;
-            st.pad = 0;
-            out[r] = st;
-        }
+        epilogue(valid ? r : -1, pok);
     }
     if constexpr (DEC) flush_chunks();
     __builtin_amdgcn_s_waitcnt(0);                             // no LDS-DMA outlives the block
@@ -3295,48 +3353,78 @@ static int q1_rl_kernel(lac_ctx *c, const Q1Args &a, hipStream_t st) {
     ProfScope ps(c, KID_Q1_STATS, st);
     k_q1_stats_rl<LT, DEC, REP, LASTN, NT><<<grid, 1024, 0, st>>>(
         (const LT *)a.lg, a.ss, a.bs, a.sym, c->B, a.rows, c->V, a.t0, a.xsh, q1_groups_per_chunk(nvec), c->stats,
-        c->q1chunks, c->q1m, nullptr, 0);
+        c->q1chunks, c->q1m, nullptr, 0, 1, 0);
     CHECK_LAUNCH();
     return LAC_OK;
 }
 
-// Grouped row stats (shape 19): a row over K = 2..4 blocks, segments of `split`
-// vectors (a multiple of 64), the last one the rest; every segment must fit one
-// block's registers + slots -- the 16-copy form (<= 16064 vectors) with the fewest
-// blocks if any K allows it, else the 8-copy form (<= 16384).
-// Shape 20: the same with two rows per block (8 waves each), segments of <= 7999
-// vectors (16-copy form) else <= 8192.
+// Grouped row stats (shapes 19 / 20 / 21): a row in kg segments of `split` vectors
+// (a multiple of 64; the last one the rest), one per row slot of the rl kernel
+// with NRB = 1 / 2 / 4 rows per block; every segment must fit its slot -- the
+// 16-copy form (16064 / 8000 / 4032 vectors) or the 8-copy form (16384 / 8192 /
+// 4096).  Decode has no 16-copy form at NRB = 4 (LDS: its group totals).
+constexpr int kQ1MaxSeg = 16;                    // segments per row (lanes polling partners)
 struct Q1Group {
-    int k = 0, split = 0;
+    int k = 0, split = 0, nrb = 1;
     bool rep16 = false;
+    double score = 0;
 };
-static bool q1_group(lac_ctx *c, int64_t nvec, Q1Group *g, bool two = false) {
-    if (nvec <= (two ? 8192 : 16384)) return false;
-    const int64_t ngrp = (nvec + 63) / 64;
-    for (int pass = 0; pass < 2; pass++) {
-        const int64_t lim = two ? (pass ? 8192 : 15 * 512 + 320) : (pass ? 16384 : kRLTrimMaxVec);
-        for (int k = 2; k <= 4 && 8 * k <= c->cus; k++) {
-            const int64_t sp = 64 * ((ngrp + k - 1) / k), last = nvec - (k - 1) * sp;
-            if (last > 0 && sp <= lim && last <= lim) {
-                g->k = k;
-                g->split = (int)sp;
-                g->rep16 = pass == 0;
-                return true;
-            }
+static int64_t q1_slot_cap(int nrb, bool rep16) {
+    if (nrb == 1) return rep16 ? kRLTrimMaxVec : 16384;
+    if (nrb == 2) return rep16 ? 15 * 512 + 320 : 8192;
+    return rep16 ? 15 * 256 + 192 : 4096;
+}
+// the fewest segments of this form; score = the row's share of its slots' capacity
+// (the bytes a CU keeps in flight) x the share of the XCD's slots in use
+static bool q1_group_form(lac_ctx *c, int64_t nvec, int nrb, bool rep16, Q1Group *g) {
+    const int64_t ngrp = (nvec + 63) / 64, lim = q1_slot_cap(nrb, rep16), spx = (int64_t)(c->cus / 8) * nrb;
+    for (int k = 2; k <= kQ1MaxSeg && k <= spx; k++) {
+        const int64_t sp = 64 * ((ngrp + k - 1) / k), last = nvec - (k - 1) * sp;
+        if (last > 0 && sp <= lim && last <= lim) {
+            g->k = k;
+            g->split = (int)sp;
+            g->nrb = nrb;
+            g->rep16 = rep16;
+            g->score = (double)nvec / (k * (16384.0 / nrb)) * (double)((spx / k) * k) / (double)spx;
+            return true;
         }
     }
     return false;
 }
+// nrb = 0: the best-scoring form (ties: the first, i.e. fewer rows per block and the
+// 16-copy form); decode's 8-copy forms score 5 % lower (q1_rl_rep16: its lookups
+// are the bound there; encode measured the same either way), and bf16 encode's
+// 25 % lower: with the group logic they spill 29-32 VGPRs at the 128 cap (the
+// 16-copy ones none), and the round-2 pair form at V = 262144 ran at 59 % of peak
+// against 78 % for V = 256000's 16-copy halves
+static bool q1_group(lac_ctx *c, int64_t nvec, bool dec, bool bf16, int nrb, Q1Group *best) {
+    bool any = false;
+    for (int n : {1, 2, 4}) {
+        if (nrb && n != nrb) continue;
+        for (int rep16 = 1; rep16 >= 0; rep16--) {
+            if (dec && n == 4 && rep16) continue;
+            Q1Group g;
+            if (!q1_group_form(c, nvec, n, rep16 != 0, &g)) continue;
+            if (!rep16) g.score *= dec ? 0.95 : bf16 ? 0.75 : 1.0;
+            if (!any || g.score > best->score + 1e-9) *best = g;
+            any = true;
+        }
+    }
+    return any;
+}
 
-template <typename LT, bool DEC, int REP, int LASTN, int K, int NT = 1024>
-static int q1_group_kernel(lac_ctx *c, const Q1Args &a, hipStream_t st, int split) {
+template <typename LT, bool DEC, int REP, int LASTN, int NT>
+static int q1_group_kernel(lac_ctx *c, const Q1Args &a, hipStream_t st, const Q1Group &g) {
     constexpr int NRB = 1024 / NT;
     const int64_t nvec = c->V / LogitN<LT>::N;
-    if (!c->pxch) HIPCHK(hipMalloc(&c->pxch, sizeof(uint64_t) * (4 * c->cus + 1)));   // (<= 2 rows per block) + abort
-    // groups of K blocks in runs of 8 K (one per XCD each); never more blocks than CUs
-    // (one per CU: every member of every group resident at once)
-    const int64_t need = 8 * K * ((a.rows + 8 * NRB - 1) / (8 * NRB)), cap = (int64_t)(c->cus / (8 * K)) * (8 * K);
-    const unsigned grid = (unsigned)(need < cap ? need : cap);
+    // (<= 4 rows per block) + the abort word
+    if (!c->pxch) HIPCHK(hipMalloc(&c->pxch, sizeof(uint64_t) * (8 * (int64_t)c->cus + 1)));
+    // rpx rows per XCD per round (all of the XCD's slots' worth, or all rows in one
+    // round), on the fewest blocks that hold rpx * k slots; never more blocks than
+    // CUs (one per CU: every partner resident at once)
+    const int64_t spx = (int64_t)(c->cus / 8) * NRB, rcap = spx / g.k, rneed = (a.rows + 7) / 8;
+    const int64_t rpx = rneed < rcap ? rneed : rcap;
+    const unsigned grid = (unsigned)(8 * ((rpx * g.k + NRB - 1) / NRB));
     HIPCHK(hipMemsetAsync(c->pxch, 0, sizeof(uint64_t) * (2 * NRB * grid + 1), st));   // no stale sequence numbers,
                                                                                       // abort word clear
     // the segments add into zeroed outputs
@@ -3344,9 +3432,9 @@ static int q1_group_kernel(lac_ctx *c, const Q1Args &a, hipStream_t st, int spli
     else HIPCHK(hipMemsetAsync(c->stats, 0, sizeof(RowStats) * a.rows, st));
     {
         ProfScope ps(c, KID_Q1_STATS, st);
-        k_q1_stats_rl<LT, DEC, REP, LASTN, NT, K><<<grid, 1024, 0, st>>>(
+        k_q1_stats_rl<LT, DEC, REP, LASTN, NT, true><<<grid, 1024, 0, st>>>(
             (const LT *)a.lg, a.ss, a.bs, a.sym, c->B, a.rows, c->V, a.t0, a.xsh, q1_groups_per_chunk(nvec), c->stats,
-            c->q1chunks, c->q1m, c->pxch, split);
+            c->q1chunks, c->q1m, c->pxch, g.split, g.k, (int)rpx);
         CHECK_LAUNCH();
     }
     // repair: the tiled two-pass shape over the same rows, gated on the abort word
@@ -3358,21 +3446,19 @@ static int q1_group_kernel(lac_ctx *c, const Q1Args &a, hipStream_t st, int spli
     return q1_stats_launch<LT, 8, 8, DEC, true, false>(c, a, st, gate);                            // shape 8
 }
 
-template <typename LT, bool DEC, int REP, int LASTN, int NT>
-static int q1_group_k(lac_ctx *c, const Q1Args &a, hipStream_t st, const Q1Group &g) {
-    if (g.k == 2) return q1_group_kernel<LT, DEC, REP, LASTN, 2, NT>(c, a, st, g.split);
-    if (g.k == 3) return q1_group_kernel<LT, DEC, REP, LASTN, 3, NT>(c, a, st, g.split);
-    return q1_group_kernel<LT, DEC, REP, LASTN, 4, NT>(c, a, st, g.split);
-}
-
 template <typename LT, bool DEC>
-static int q1_stats_group_launch(lac_ctx *c, const Q1Args &a, hipStream_t st, const Q1Group &g, bool two = false) {
-    if (two) {
-        if (g.rep16) return q1_group_k<LT, DEC, 16, 320, 512>(c, a, st, g);
-        return q1_group_k<LT, DEC, kRLRep, 512, 512>(c, a, st, g);
+static int q1_stats_group_launch(lac_ctx *c, const Q1Args &a, hipStream_t st, const Q1Group &g) {
+    if (g.nrb == 4) {
+        if constexpr (!DEC)
+            if (g.rep16) return q1_group_kernel<LT, DEC, 16, 192, 256>(c, a, st, g);
+        return q1_group_kernel<LT, DEC, kRLRep, 256, 256>(c, a, st, g);
     }
-    if (g.rep16) return q1_group_k<LT, DEC, 16, kRLLastTrim, 1024>(c, a, st, g);
-    return q1_group_k<LT, DEC, kRLRep, 1024, 1024>(c, a, st, g);
+    if (g.nrb == 2) {
+        if (g.rep16) return q1_group_kernel<LT, DEC, 16, 320, 512>(c, a, st, g);
+        return q1_group_kernel<LT, DEC, kRLRep, 512, 512>(c, a, st, g);
+    }
+    if (g.rep16) return q1_group_kernel<LT, DEC, 16, kRLLastTrim, 1024>(c, a, st, g);
+    return q1_group_kernel<LT, DEC, kRLRep, 1024, 1024>(c, a, st, g);
 }
 
 // The register + LDS-slot shapes (k_q1_stats_rl), by rows per block:
@@ -3437,17 +3523,14 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
         // spills were removed (streamed butterfly, per-group LDS totals, fresh lane index),
         // 220 -> 210 us per step of 4096 rows vs shape 9, profiles/r02/q1_rl_dec/)
         if (sh == 0 && nvec <= 16384) sh = 15;
-        // longer rows that two blocks' registers + slots hold: one half per block (shape 19)
-        // (bf16: V = 256000 encode 4.36 -> 2.68 ms, 48 -> 78 % of peak; profiles/r02/q1_pair_bf16/)
-        // two rows per block (shape 20) where shape 19's segments would be small (<= 11000
-        // vectors: the per-row exchange is then amortised over two rows): bf16 V = 131080
-        // 50 -> 58 %, 151936 (Qwen2) 57 -> 65 %, f32 65540 60 -> 66 %; at 12500-vector
-        // segments 19 stays ahead (bf16 200000 70 vs 66 %, f32 100000 77 vs 73 %;
-        // profiles/r02/q1_groups2/)
-        Q1Group g0, g1;
-        // (and only in shape 20's 16-copy form, the one measured)
-        if (sh == 0 && q1_group(c, nvec, &g0))
-            sh = g0.split <= 11000 && q1_group(c, nvec, &g1, true) && g1.rep16 ? 20 : 19;
+        // longer rows: row groups (shapes 19 / 20 / 21: segments in row slots of 1 / 2 / 4
+        // rows per block), the form that keeps the most bytes in flight (q1_group).
+        // Round 2 had whole blocks per segment (kg = 2..4 blocks of 1 or 2 rows): bf16
+        // V = 256000 48 -> 78 % of peak (profiles/r02/q1_pair_bf16/), Qwen2 bf16 57 -> 65 %
+        // (profiles/r02/q1_groups2/); row slots at any kg: profiles/r03/q1_slots/
+        Q1Group grp;
+        if (sh == 0 && nvec > 16384 && q1_group(c, nvec, DEC, sizeof(LT) == 2, 0, &grp))
+            return q1_stats_group_launch<LT, DEC>(c, a, st, grp);
         // measured at V = 128256 f32: encode tiles of (16,8) with the tile-rolling
         // prefetch 1.98 ms vs 2.18 for tiles of (8,8) (shape 13, its (8,8) form: 2.20)
         if (sh == 0) sh = nvec <= 64 * 16 * 16 ? 9 : (DEC ? 10 : (sizeof(LT) == 4 ? 14 : 8));
@@ -3464,8 +3547,8 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
     if (sh == 17 && nvec <= 4096) return q1_stats_rl_launch<LT, DEC>(c, a, st, 17);
     if (sh == 18 && nvec <= 8192) return q1_stats_rl_launch<LT, DEC>(c, a, st, 18);
     Q1Group grp;
-    if (sh == 19 && q1_group(c, nvec, &grp)) return q1_stats_group_launch<LT, DEC>(c, a, st, grp);
-    if (sh == 20 && q1_group(c, nvec, &grp, true)) return q1_stats_group_launch<LT, DEC>(c, a, st, grp, true);
+    if (sh >= 19 && sh <= 21 && q1_group(c, nvec, DEC, sizeof(LT) == 2, sh == 19 ? 1 : sh == 20 ? 2 : 4, &grp))
+        return q1_stats_group_launch<LT, DEC>(c, a, st, grp);
     if (sh == 13) return q1_stats_launch<LT, 8, 8, DEC, true, true>(c, a, st);         // tiles of (8,8,y)
     if (sh == 14) return q1_stats_launch<LT, 16, 8, DEC, true, true, 16>(c, a, st);    // tiles of (16,8,y)
     if (sh == 8) return q1_stats_launch<LT, 8, 8, DEC, true, false>(c, a, st);      // tiles of 4096 vectors
@@ -3665,7 +3748,7 @@ int lac_set_option(lac_ctx *c, int option, int64_t value) {
         c->fine_decode = (int)value;
         return LAC_OK;
     case LAC_OPT_Q1_SHAPE:
-        if (value < 0 || value > 20) return fail(LAC_E_ARG, "bad q1 shape");
+        if (value < 0 || value > 21) return fail(LAC_E_ARG, "bad q1 shape");
         c->q1_shape = (int)value;
         return LAC_OK;
     case LAC_OPT_MAPPING:

@@ -80,7 +80,8 @@ CASES = [
     (1000, 40, 30, 40, "bf16"),
     (128256, 8, 4, 48, "bf16"),            # 16-wave single-pass row stats
     (128256, 4, 5, 48, "f32"),             # rows split over a pair of blocks (shape 19)
-    (131080, 6, 5, 48, "bf16"),            # bf16 pairs: the int16 max exchanged, float fallback rows
+    (131080, 6, 5, 48, "bf16"),            # bf16 row groups: the int16 max exchanged, float fallback rows
+    (151936, 12, 4, 48, "bf16"),           # Qwen2: 5 row slots of 4-row blocks, fallback rows among them
     (65536, 6, 3, 48, "bf16"),             # (8,16) shape
     (24, 5, 50, 24, "f32"),
     (4096, 2048, 3, 48, "bf16"),
@@ -242,10 +243,11 @@ def test_every_q1_shape_gives_the_same_bits(dtype, V):
     cannot hold the row are refused with LAC_E_ARG.  V = 128256 bf16 and 65536
     f32 fill the register + LDS shape (15) exactly up to its 16384 vectors; bf16
     128512 / 128520 sit on either side of its 16-copy form's 16064-vector limit.
-    Rows past 16384 vectors take groups of 2..4 blocks (19): pairs at f32 65540 ..
-    128520 and bf16 131080 .. 151936 (halves on either side of the same limit),
-    three blocks at f32 151936 (Qwen2) and bf16 262144, four at f32 256000 and,
-    in the 8-copy form, f32 262144 (Gemma 3)."""
+    Rows past 16384 vectors take row groups (19 / 20 / 21: segments in row slots
+    of 1 / 2 / 4 rows per block; forced, they also split shorter rows): 2 slots at
+    f32 65540 .. 128520 in the 1-row form, 5 slots of the 4-row form at bf16
+    131080 / 151936 and f32 65540, 5 of the 2-row form at f32 151936, 9 at bf16
+    262144, 2 / 4 of the 8-copy 1-row form at f32 256000 / 262144 (Gemma 3)."""
     from lac_amd._lib import LacError
     B, steps, prec = 12, 3, 48
     x = _logits(777, steps, B, V, specials=True)
@@ -256,7 +258,7 @@ def test_every_q1_shape_gives_the_same_bits(dtype, V):
     c.encode_logits_job(dl, sym)
     want, wn = c.to_bytes()
     ran = 0
-    for sh in range(1, 21):
+    for sh in range(1, 22):
         c.set_q1_shape(sh)
         try:
             c.encode_logits_job(dl, sym)
@@ -273,12 +275,14 @@ def test_every_q1_shape_gives_the_same_bits(dtype, V):
 
 @pytest.mark.parametrize("dtype,V,B,steps", [("f32", 65540, 300, 70), ("f32", 128256, 520, 3),
                                              ("bf16", 256000, 300, 3), ("bf16", 262144, 64, 3),
-                                             ("f32", 151936, 256, 3), ("f32", 262144, 128, 3)])
+                                             ("f32", 151936, 256, 3), ("f32", 262144, 128, 3),
+                                             ("bf16", 151936, 300, 3), ("bf16", 131080, 333, 3)])
 def test_paired_row_stats_many_rows(dtype, V, B, steps):
-    """Rows split over a group of blocks (shape 19) with many rows per group and, at
-    70 steps, two launches per job (the per-row arrival counts rearm, the maximum
-    words are cleared): logits path bytes == quantise + pmf path, decode round trip,
-    and == the tiled shape's bytes."""
+    """Rows split into row groups with many rounds per launch and, at 70 steps, two
+    launches per job (the sequence numbers and maximum words are cleared): logits
+    path bytes == quantise + pmf path, decode round trip, and == the tiled shape's
+    and every forced group form's bytes (rounds with a partial last one: 333 x 3
+    rows over 25 rows per XCD per round)."""
     g = torch.Generator(device=DEV).manual_seed(V + B)
     dl = torch.randn((steps, B, V), device=DEV, generator=g) * 3
     if dtype == "bf16":
@@ -288,9 +292,10 @@ def test_paired_row_stats_many_rows(dtype, V, B, steps):
     sym = torch.randint(0, V, (steps, B), device=DEV, generator=g, dtype=torch.int32)
     c.encode_logits_job(dl, sym)
     a, na = c.to_bytes()
-    c.set_q1_shape(14)
-    c.encode_logits_job(dl, sym)
-    assert c.to_bytes()[0] == a
+    for sh in (14, 19, 20, 21):
+        c.set_q1_shape(sh)
+        c.encode_logits_job(dl, sym)
+        assert c.to_bytes()[0] == a, sh
     c.set_q1_shape(0)
     pmf = c.quantize_logits(dl)
     c2 = _coder(V, B, prec, cap=steps * (prec + 2) + 256)
@@ -304,14 +309,14 @@ def test_paired_row_stats_many_rows(dtype, V, B, steps):
 
 
 def test_q1_shape_option_range():
-    """LAC_OPT_Q1_SHAPE takes 0 (AUTO) .. 20; anything else is refused with LAC_E_ARG."""
+    """LAC_OPT_Q1_SHAPE takes 0 (AUTO) .. 21; anything else is refused with LAC_E_ARG."""
     from lac_amd._lib import LacError, LAC_E_ARG
     c = _coder(1024, 4, 40)
-    for bad in (-1, 21, 99):
+    for bad in (-1, 22, 99):
         with pytest.raises(LacError) as e:
             c.set_q1_shape(bad)
         assert e.value.code == LAC_E_ARG
-    for ok in (0, 19, 20):
+    for ok in (0, 19, 20, 21):
         c.set_q1_shape(ok)
     c.close()
 
