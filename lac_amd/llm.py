@@ -8,11 +8,11 @@ re-evaluates them; ``calc_dist`` turns the last logits into an integer CDF
 duck type works as ``llm``: ``reset()``, ``eval(tokens)``, ``n_ctx()`` and
 ``_scores`` (2-D, last row = next-token logits).
 
-``TorchLLM`` provides that duck type for a PyTorch causal LM on the GPU
-(``module(tokens[1, t]) -> logits[1, t, V]``), so a ROCm model drops in where
-llama.cpp was.  It re-runs the window on every ``eval`` -- the same op sequence
-on the encode and the decode side, which is what makes the quantised tables,
-and therefore the bitstream, reproducible.
+``TorchLLM`` provides that duck type for a PyTorch causal LM on the GPU, so a
+ROCm model drops in where llama.cpp was: one cached step per evaluated token
+for a module with a key/value cache (TinyCausalLM), else the window re-run on
+every ``eval`` -- the same op sequence on the encode and the decode side either
+way, which is what makes the quantised tables, and the bitstream, reproducible.
 
 Coding goes through lac_amd.coder (GPU); this module only produces tables.
 """
@@ -81,15 +81,25 @@ class Llama_AC(ProbPredictor):
 
 
 class TorchLLM:
-    """llama_cpp.Llama's duck type over a torch causal LM on a HIP device."""
+    """llama_cpp.Llama's duck type over a torch causal LM on a HIP device.
+
+    A module with ``init_cache(B, T)`` / ``step(tokens[B], cache, t)`` (as
+    TinyCausalLM) is run incrementally: each evaluated token is one step against
+    a key/value cache, so a sequence costs O(T) steps as with llama.cpp's own KV
+    cache.  Past ``n_ctx`` tokens the window slides and is re-evaluated from an
+    empty cache (Llama_AC resets before that happens).  Any other module
+    (``module(tokens[1, t]) -> logits[1, t, V]``) re-runs the window on every
+    ``eval``.  Either way the encode and decode sides issue the same sequence of
+    calls, which is what makes the logits -- and the tables and bitstream --
+    reproducible."""
 
     def __init__(self, module, n_ctx=512, device="cuda"):
         import torch
         self.module = module.to(device).eval()
         self.device = torch.device(device)
         self._n_ctx = n_ctx
-        self.tokens = []
-        self._scores = None
+        self.incremental = hasattr(module, "step") and hasattr(module, "init_cache")
+        self.reset()
 
     def n_ctx(self):
         return self._n_ctx
@@ -97,24 +107,70 @@ class TorchLLM:
     def reset(self):
         self.tokens = []
         self._scores = None
+        self._cache = None
+        self._pos = 0
 
     def eval(self, tokens):
         import torch
-        self.tokens.extend(int(t) for t in tokens)
-        window = self.tokens[-self._n_ctx:]
+        new = [int(t) for t in tokens]
+        self.tokens.extend(new)
         with torch.no_grad():
-            x = torch.tensor([window], dtype=torch.long, device=self.device)
-            logits = self.module(x)[0, -1].float()
+            if self.incremental:
+                if self._cache is None or len(self.tokens) > self._n_ctx:
+                    self._cache = self.module.init_cache(1, self._n_ctx)
+                    self._pos = 0
+                    new = self.tokens[-self._n_ctx:]
+                for t in new:
+                    x = torch.tensor([t], dtype=torch.long, device=self.device)
+                    logits = self.module.step(x, self._cache, self._pos)[0].float()
+                    self._pos += 1
+            else:
+                window = self.tokens[-self._n_ctx:]
+                x = torch.tensor([window], dtype=torch.long, device=self.device)
+                logits = self.module(x)[0, -1].float()
         self._scores = logits.cpu().numpy()[None, :]
 
 
 class TinyCausalLM:
-    """A small random-init causal transformer (torch) for tests and demos -- a
-    stand-in for a real checkpoint, which cannot be fetched offline."""
+    """A small random-init GPT-style causal transformer (torch) for tests and demos
+    -- a stand-in for a real checkpoint, which cannot be fetched offline.  Pre-LN
+    blocks (attention + 4d MLP); ``forward(tokens[B, T]) -> logits[B, T, V]``
+    teacher-forced, and ``init_cache`` / ``step`` for incremental decoding with a
+    key/value cache: every step has the same shapes (the cache is T long and
+    masked past position t), so a step runs the same kernels whoever calls it."""
 
     def __new__(cls, vocab=32000, d=64, layers=2, heads=4, max_len=512, seed=0):
+        import math
+
         import torch
         import torch.nn as nn
+
+        class _Block(nn.Module):
+            def __init__(self):
+                super().__init__()
+                self.ln1, self.ln2 = nn.LayerNorm(d), nn.LayerNorm(d)
+                self.qkv, self.proj = nn.Linear(d, 3 * d), nn.Linear(d, d)
+                self.fc1, self.fc2 = nn.Linear(d, 4 * d), nn.Linear(4 * d, d)
+
+            def _heads(self, z):                                  # [B, t, d] -> [B, H, t, dh]
+                return z.view(z.shape[0], z.shape[1], heads, d // heads).transpose(1, 2)
+
+            def attend(self, q, k, v, mask):
+                a = torch.softmax((q @ k.transpose(-1, -2)) / math.sqrt(d // heads) + mask, dim=-1) @ v
+                return a.transpose(1, 2).reshape(q.shape[0], q.shape[2], d)
+
+            def mlp(self, h):
+                return h + self.fc2(torch.nn.functional.gelu(self.fc1(self.ln2(h))))
+
+            def forward(self, h, mask):
+                q, k, v = (self._heads(z) for z in self.qkv(self.ln1(h)).split(d, dim=-1))
+                return self.mlp(h + self.proj(self.attend(q, k, v, mask)))
+
+            def step(self, h, kv, t, mask):                      # h [B, 1, d]; kv: this block's (K, V) [B, H, T, dh]
+                q, k, v = (self._heads(z) for z in self.qkv(self.ln1(h)).split(d, dim=-1))
+                kv[0][:, :, t:t + 1] = k
+                kv[1][:, :, t:t + 1] = v
+                return self.mlp(h + self.proj(self.attend(q, kv[0], kv[1], mask)))
 
         class _M(nn.Module):
             def __init__(self):
@@ -122,18 +178,37 @@ class TinyCausalLM:
                 g = torch.Generator().manual_seed(seed)
                 self.emb = nn.Embedding(vocab, d)
                 self.pos = nn.Embedding(max_len, d)
-                layer = nn.TransformerEncoderLayer(d, heads, 4 * d, dropout=0.0, batch_first=True)
-                self.body = nn.TransformerEncoder(layer, layers)
+                self.blocks = nn.ModuleList(_Block() for _ in range(layers))
+                self.ln = nn.LayerNorm(d)
                 self.head = nn.Linear(d, vocab)
                 with torch.no_grad():
-                    for p in self.parameters():
+                    for name, p in self.named_parameters():
+                        if ".ln" in name or name.startswith("ln"):
+                            continue                              # LayerNorm: weight 1, bias 0
                         p.copy_(torch.randn(p.shape, generator=g) * 0.5)
 
             def forward(self, x):
                 t = x.shape[1]
                 mask = torch.triu(torch.full((t, t), float("-inf"), device=x.device), 1)
                 h = self.emb(x) + self.pos(torch.arange(t, device=x.device))[None]
-                return self.head(self.body(h, mask=mask, is_causal=True))
+                for blk in self.blocks:
+                    h = blk(h, mask)
+                return self.head(self.ln(h))
+
+            def init_cache(self, B, T):
+                p = self.head.weight
+                return [(p.new_zeros((B, heads, T, d // heads)), p.new_zeros((B, heads, T, d // heads)))
+                        for _ in self.blocks]
+
+            def step(self, tok, cache, t):
+                """Logits [B, V] of the next token after tok[B] at position t."""
+                T = cache[0][0].shape[2]
+                mask = torch.full((T,), float("-inf"), device=tok.device)
+                mask[:t + 1] = 0
+                h = self.emb(tok[:, None]) + self.pos.weight[t][None, None]
+                for blk, kv in zip(self.blocks, cache):
+                    h = blk.step(h, kv, t, mask)
+                return self.head(self.ln(h))[:, 0]
 
         return _M()
 
@@ -141,19 +216,20 @@ class TinyCausalLM:
 class LogitsCompressor:
     """Batched LLM compression on the GPU through the logits path (SURVEY §8(f) 1 + 3).
 
-    ``compress(tokens[B, T])`` runs the causal LM once, teacher-forced on
-    ``[BOS] + tokens[:, :-1]`` (llama_compress.py primes with BOS = 1, :20-23),
-    and hands its logits -- cast to ``logits_dtype``, still [B, T, V] in HBM --
-    straight to ``BatchCoder.encode_logits_job`` as a strided [T, B, V] view: the
-    q1 tables are computed in-kernel and no pmf is ever written.
+    Step t codes token t with the model's logits after ``[BOS] + tokens[:, :t]``
+    (llama_compress.py primes with BOS = 1, :20-23), handed -- cast to
+    ``logits_dtype``, in HBM -- straight to the coder's logits entry points: the q1
+    tables are computed in-kernel and no pmf is ever written.  Decoding must see
+    bit-identical logits, so both sides produce them the same way:
 
-    ``decompress`` must see bit-identical logits.  It re-runs the *same*
-    fixed-shape forward ([B, T], not-yet-decoded positions filled with 0) before
-    each step: under the causal mask position t never depends on later positions,
-    and equal shapes select the same kernels, so row t is computed by the
-    identical op sequence as in ``compress``.  (An incremental KV-cache decode
-    would change shapes and kernels, and with them the low bits of the logits.)
-    O(T) forwards: a demonstration driver, not a serving loop.
+    * incremental (a module with ``init_cache`` / ``step``, e.g. TinyCausalLM):
+      one cached step per position on both sides (``encode_logits`` /
+      ``decode_logits`` per step) -- O(T) steps each way, as a serving loop;
+    * otherwise (``module(tokens[B, T]) -> logits[B, T, V]`` only): compress runs
+      one teacher-forced forward, and decompress re-runs the *same* fixed-shape
+      [B, T] forward (not-yet-decoded positions 0) before each step -- under the
+      causal mask position t never depends on later ones, and equal shapes select
+      the same kernels.  O(T) full forwards: for modules without a cache.
     """
 
     def __init__(self, module, vocab, prec=48, bos=1, logits_dtype=None, device="cuda"):
@@ -163,6 +239,7 @@ class LogitsCompressor:
         self.vocab, self.prec, self.bos = int(vocab), int(prec), int(bos)
         self.dtype = logits_dtype or torch.bfloat16
         self.device = torch.device(device)
+        self.incremental = hasattr(module, "step") and hasattr(module, "init_cache")
         # the logits kernels read rows as 16-B vectors: a vocab that is not a multiple
         # of 8 (bf16) / 4 (f32) -- GPT-2's 50257, say -- is coded over rows padded
         # with -inf (pad entries get the q1 minimum weight, 1 unit; compress and
@@ -170,13 +247,37 @@ class LogitsCompressor:
         m = logits_row_multiple(self.dtype)
         self.vcode = (self.vocab + m - 1) // m * m
 
+    def _fit(self, lg):
+        if self.vcode != lg.shape[-1]:
+            lg = __import__("torch").nn.functional.pad(lg, (0, self.vcode - lg.shape[-1]), value=float("-inf"))
+        return lg.contiguous()
+
     def _logits(self, ctx):
         import torch
         with torch.no_grad():
-            lg = self.module(ctx).to(self.dtype)
-            if self.vcode != lg.shape[-1]:
-                lg = torch.nn.functional.pad(lg, (0, self.vcode - lg.shape[-1]), value=float("-inf"))
-            return lg.contiguous()
+            return self._fit(self.module(ctx).to(self.dtype))
+
+    def _steps(self, B, T, feed):
+        """Incremental: yields (t, logits [1, B, vcode]) for t < T; feed(t) -> the tokens [B]
+        at position t + 1's input (the coded / decoded token t)."""
+        import torch
+        cache = self.module.init_cache(B, T)
+        tok = torch.full((B,), self.bos, dtype=torch.long, device=self.device)
+        for t in range(T):
+            with torch.no_grad():
+                lg = self._fit(self.module.step(tok, cache, t).to(self.dtype))[None]
+            yield t, lg
+            tok = feed(t)
+
+    def logits(self, tokens):
+        """The [B, T, vcode] logits compress codes tokens[B, T] with (for checking)."""
+        import torch
+        tokens = tokens.to(self.device, torch.long)
+        B, T = tokens.shape
+        if not self.incremental:
+            ctx = torch.cat([torch.full((B, 1), self.bos, dtype=torch.long, device=self.device), tokens[:, :-1]], 1)
+            return self._logits(ctx)
+        return torch.cat([lg for _, lg in self._steps(B, T, lambda t: tokens[:, t])], 0).transpose(0, 1)
 
     def _coder(self, B, T):
         from .batch import BatchCoder
@@ -188,10 +289,15 @@ class LogitsCompressor:
         import torch
         tokens = tokens.to(self.device, torch.long)
         B, T = tokens.shape
-        ctx = torch.cat([torch.full((B, 1), self.bos, dtype=torch.long, device=self.device), tokens[:, :-1]], 1)
-        lg = self._logits(ctx)                                   # [B, T, V]
         coder = self._coder(B, T)
-        coder.encode_logits_job(lg.transpose(0, 1), tokens.t().contiguous().to(torch.int32))
+        if self.incremental:
+            sym = tokens.t().contiguous().to(torch.int32)          # [T, B]
+            coder.reset()
+            for t, lg in self._steps(B, T, lambda t: tokens[:, t]):
+                coder.encode_logits(lg, sym[t:t + 1])
+            coder.finish()
+        else:
+            coder.encode_logits_job(self.logits(tokens).transpose(0, 1), tokens.t().contiguous().to(torch.int32))
         out = coder.to_bytes()
         coder.close()
         return out
@@ -208,15 +314,19 @@ class LogitsCompressor:
         bits = torch.from_numpy(buf).to(self.device)
         nb = torch.as_tensor(np.asarray(nbits, dtype=np.int64), device=self.device)
         coder.decode_open(bits, nb)
-        ctx = torch.zeros((B, T), dtype=torch.long, device=self.device)
-        ctx[:, 0] = self.bos
         out = torch.empty((B, T), dtype=torch.long, device=self.device)
-        for t in range(T):
-            lg = self._logits(ctx)[:, t:t + 1, :]                # [B, 1, V]
-            s = coder.decode_logits(lg.transpose(0, 1))[0].to(torch.long)
-            out[:, t] = s
-            if t + 1 < T:
-                ctx[:, t + 1] = s
+        if self.incremental:
+            for t, lg in self._steps(B, T, lambda t: out[:, t]):
+                out[:, t] = coder.decode_logits(lg)[0].to(torch.long)
+        else:
+            ctx = torch.zeros((B, T), dtype=torch.long, device=self.device)
+            ctx[:, 0] = self.bos
+            for t in range(T):
+                lg = self._logits(ctx)[:, t:t + 1, :]            # [B, 1, V]
+                s = coder.decode_logits(lg.transpose(0, 1))[0].to(torch.long)
+                out[:, t] = s
+                if t + 1 < T:
+                    ctx[:, t + 1] = s
         coder.raise_on_error()
         coder.close()
         return out

@@ -287,19 +287,31 @@ def test_llama_ac_adapter_with_torch_model_roundtrip():
     assert list(ac.from_bin.run(bits, stop=0, n=len(toks))) == toks
 
 
-def test_logits_compressor_roundtrip_and_oracle():
-    """LLM compression through the logits path: one teacher-forced forward, bf16
-    logits straight into the coder; bytes == q1 oracle + encode oracle on the same
-    logits; the fixed-shape decode loop reproduces the tokens."""
+@pytest.mark.parametrize("incremental", [True, False])
+def test_logits_compressor_roundtrip_and_oracle(incremental):
+    """LLM compression through the logits path, bf16 logits straight into the coder:
+    incremental (TinyCausalLM's key/value-cache steps on both sides, O(T)) and, for a
+    module with only forward(), one teacher-forced forward + fixed-shape decode
+    forwards.  Bytes == q1 oracle + encode oracle on the logits compress coded with;
+    decompress reproduces the tokens."""
     from lac_amd.llm import LogitsCompressor, TinyCausalLM
     from oracle import oracle as coracle
     V, B, T, prec = 1024, 4, 24, 48
     model = TinyCausalLM(vocab=V, d=32, layers=1, heads=2, max_len=64)
+    if not incremental:
+        class Plain(torch.nn.Module):                          # forward() only: no cache
+            def __init__(self):
+                super().__init__()
+                self.m = model
+
+            def forward(self, x):
+                return self.m(x)
+        model = Plain()
     lc = LogitsCompressor(model, V, prec=prec, device="cuda:0")
+    assert lc.incremental == incremental
     toks = torch.from_numpy(np.random.default_rng(5).integers(0, V, (B, T))).to("cuda:0")
     data, nbits = lc.compress(toks)
-    ctx = torch.cat([torch.ones((B, 1), dtype=torch.long, device="cuda:0"), toks[:, :-1]], 1)
-    lg = lc._logits(ctx)                                        # [B, T, V] bf16, as compress saw it
+    lg = lc.logits(toks)                                        # [B, T, V] bf16, as compress saw it
     host = lg.transpose(0, 1).contiguous().view(torch.int16).cpu().numpy().view(np.uint16)
     pmf = coracle.q1_quantize(host, prec)
     out, nb, status, rc = coracle.encode_batch(pmf, toks.t().contiguous().cpu().numpy().astype(np.int32), prec)
@@ -325,8 +337,7 @@ def test_logits_compressor_vocab_not_a_multiple_of_8():
         lc = LogitsCompressor(model, V, prec=prec, logits_dtype=dt, device="cuda:0")
         assert lc.vcode == (1008 if dt == torch.bfloat16 else 1004)
         data, nbits = lc.compress(toks)
-        ctx = torch.cat([torch.ones((B, 1), dtype=torch.long, device="cuda:0"), toks[:, :-1]], 1)
-        lg = lc._logits(ctx)
+        lg = lc.logits(toks)
         assert lg.shape[-1] == lc.vcode and torch.isinf(lg[..., V:]).all()
         h = lg.transpose(0, 1).contiguous()
         host = h.view(torch.int16).cpu().numpy().view(np.uint16) if dt == torch.bfloat16 else h.cpu().numpy()

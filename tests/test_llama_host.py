@@ -51,3 +51,34 @@ def test_oracle_exact_bits_on_reference_tables(case):
         p.accept(t)
     data, L = restate.encode_bytes(rows, case["tokens"], case["prec"])
     assert L == case["exact_L"] and data.hex() == case["exact_bytes"]
+
+
+def test_tiny_lm_cached_steps_match_forward():
+    """TinyCausalLM's key/value-cache steps (what LogitsCompressor and TorchLLM run,
+    O(1) model work per token) compute the teacher-forced forward's logits, and
+    TorchLLM's incremental eval matches re-running the window -- across the
+    sliding-window rebuild past n_ctx (CPU, float32)."""
+    torch = pytest.importorskip("torch")
+    from lac_amd.llm import TinyCausalLM, TorchLLM
+    m = TinyCausalLM(vocab=300, d=32, layers=2, heads=2, max_len=64, seed=3).eval()
+    x = torch.from_numpy(np.random.default_rng(1).integers(0, 300, (3, 20)))
+    with torch.no_grad():
+        full = m(x)
+        cache = m.init_cache(3, 20)
+        steps = torch.stack([m.step(x[:, t], cache, t) for t in range(20)], 1)
+    assert torch.allclose(full, steps, atol=1e-4, rtol=1e-4)
+
+    class Plain(torch.nn.Module):                              # forward() only: the window re-run
+        def forward(self, z):
+            return m(z)
+    inc, win = TorchLLM(m, n_ctx=12, device="cpu"), TorchLLM(Plain(), n_ctx=12, device="cpu")
+    assert inc.incremental and not win.incremental
+    for t in range(1, 30):
+        inc.eval([t])
+        win.eval([t])
+        assert np.allclose(inc._scores, win._scores, atol=1e-4), t
+    inc.reset()
+    inc.eval([1, 2, 3])
+    win.reset()
+    win.eval([1, 2, 3])
+    assert np.allclose(inc._scores, win._scores, atol=1e-4)
