@@ -1798,6 +1798,17 @@ __constant__ uint32_t c_q1_tab[LAC_Q1_TAB_SIZE] = LAC_Q1_TAB_INIT;
 #ifndef LAC_Q1_NT
 #define LAC_Q1_NT 1              // logits rows are read once: nontemporal loads
 #endif
+// the LDS-DMA loads of the register + slot shapes with the nt policy too: a DMA
+// stream without it read at 76.5 % of peak, with it 86 % = the register loads'
+// (tools/hbm_probe3.hip, profiles/r03/hbm_probe3.txt)
+#ifndef LAC_Q1_DMA_NT
+#define LAC_Q1_DMA_NT LAC_Q1_NT
+#endif
+#if LAC_Q1_DMA_NT
+#define LAC_Q1_DMA_POLICY " nt"
+#else
+#define LAC_Q1_DMA_POLICY ""
+#endif
 #ifndef LAC_Q1_SCHED
 #define LAC_Q1_SCHED 0           // scheduling fence between vectors in k_q1_stats
 #endif
@@ -2553,7 +2564,7 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
         if ((k == L - 1 && noslot) || idle) return;            // wave-uniform
         const u32x4 *src = reinterpret_cast<const u32x4 *>(rw) + vidx(R + k);
         uint32_t keep;
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" LAC_Q1_DMA_POLICY "\n\ts_mov_b32 m0, %0"
                      : "=&s"(keep)
                      : "v"(src), "s"(slot_base + (uint32_t)(k * NT * 16))
                      : "memory");
