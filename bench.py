@@ -254,6 +254,19 @@ def main():
 
     cpu = None
     parity = {"round_trip_all_streams": round_trip, "stream_status_ok": rc == 0, "decode": decode_info}
+    if not logits_in:
+        # rows that can take fudged_dist at all: T > w * minp (arith_code.py:84) for some
+        # interval width w > 2^(prec-1) (every width the renormalisation leaves)
+        nf = 0
+        for t in range(T):
+            r = pmf[t].to(torch.int64)
+            if args.pmf_bits == 32:
+                r = r & 0xFFFFFFFF
+            mn = torch.where(r > 0, r, torch.full_like(r, 1 << 62)).amin(dim=1)
+            tot = r.sum(dim=1, dtype=torch.float64)                    # order of magnitude is enough here
+            nf += int((tot > mn.to(torch.float64) * float(1 << (P - 1))).sum())
+            del r
+        parity["rows_that_can_fudge"] = nf / (T * B)
     if gatherer:
         parity["gather_ok"] = gather_ok
         parity["gather"] = gather_info

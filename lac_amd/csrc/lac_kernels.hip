@@ -1418,7 +1418,8 @@ __global__ __launch_bounds__(64 * LAC_STREAM_WG, LAC_DECF_MINW) void k_decode_wa
 #pragma unroll
         for (int r = 0; r < NR; r++) mine[r] = 0;
         uint32_t mn = ~0u;                                    // min over min_key (0 -> max)
-        uint64_t hh = 0;                                      // u64 rows: sum of the high words
+        uint32_t hh = 0;                                      // u64 rows: sum of the high words, saturating
+                                                              // (a lane at 2^32 - 1 already means T >= 2^64)
         uint32_t ovf = 0;                                     // (unused: totals wrap, see u64_total_overflows)
         const int nfull = nvec / 512;                         // groups of 8 whole iterations
         auto group = [&](int g, bool full) {
@@ -1451,8 +1452,14 @@ __global__ __launch_bounds__(64 * LAC_STREAM_WG, LAC_DECF_MINW) void k_decode_wa
                 for (int j = 0; j < VEC; j++) {
                     const E e = vget<E, VEC>(x[u], j);
                     a += (uint64_t)e;                         // wraps only if T >= 2^64 (detected below)
-                    if constexpr (W) hh += (uint64_t)e >> 32;
-                    mn = min(mn, min_key<E>(e));
+                    // one clamped v_add_u32 (a 64-bit sum took a move and a 64-bit add)
+                    if constexpr (W) hh = __builtin_elementwise_add_sat(hh, (uint32_t)((uint64_t)e >> 32));
+                }
+                if constexpr (W) {                            // VEC = 2: both keys in one v_min3_u32
+                    mn = min(mn, min(min_key<E>(vget<E, VEC>(x[u], 0)), min_key<E>(vget<E, VEC>(x[u], 1))));
+                } else {
+#pragma unroll
+                    for (int j = 0; j < VEC; j++) mn = min(mn, min_key<E>(vget<E, VEC>(x[u], j)));
                 }
                 s[u] = a;
             }
@@ -1484,7 +1491,7 @@ __global__ __launch_bounds__(64 * LAC_STREAM_WG, LAC_DECF_MINW) void k_decode_wa
         const uint64_t T = base;
         int err = 0;
         if (T == 0) err = LAC_E_TABLE;
-        if constexpr (W) { if (u64_total_overflows(T, wave_sum_u64(hh))) err = LAC_E_TABLE; }
+        if constexpr (W) { if (u64_total_overflows(T, wave_sum_u64((uint64_t)hh))) err = LAC_E_TABLE; }
         const uint64_t minp = err ? 1 : row_minp<E>(row, V, wave_min_u32(mn), T, (uint64_t)(st.h - st.l + 1));
         int64_t s = -1;
         if (!err) {
@@ -2832,6 +2839,300 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
     asm volatile("" ::: "memory");
 }
 
+// k_q1_stats_wide (shape 22): one row per CU held entirely in registers by an
+// 8-wave block at 2 waves per SIMD (256 VGPRs per lane): thread t holds vectors
+// t + 512 j, j < R, of its row -- R = 40: rows of <= 20480 16-B vectors (bf16
+// V <= 163840: Qwen2's 151936; f32 V <= 81920).  The 16-wave shapes hold only 8
+// vectors per thread in registers (128-VGPR cap, most of it working registers),
+// so such rows had to be split over row slots of several blocks with a maximum
+// exchange between them (§5b item 14); with 8 waves the register file is mostly
+// row, no exchange.  All R loads of a row are issued at once, so a CU alternates a
+// load phase and a compute phase (~4 VALU ops per logit); the CUs drift apart, so
+// the chip's HBM stream stays busy while some of them compute.  LDS: the 32-copy
+// table only (no bank conflicts).  Same outputs as k_q1_stats.
+//
+// GROUP (shape 23): rows longer than one block holds (bf16 Gemma 256000 / 262144,
+// f32 Llama-3 / Qwen2 / Gemma) in kg segments of `split` vectors (the last one the
+// rest), one per block, exactly as the row slots of k_q1_stats_rl's GROUP form
+// with one row per block: slot q = block / 8 of the block's XCD holds segment
+// q % kg of the XCD's row q / kg of each round (rpx rows per XCD per round, grid =
+// 8 rpx kg <= the CU count: every member resident), the segments exchange the row
+// maximum through group_post / group_poll and add their partials into the zeroed
+// outputs with relaxed atomics; a partner that never posts sets the launch's abort
+// word and poisons the row, and the gated repair launch recomputes every row.
+template <typename LT, int R, bool DEC, bool GROUP = false>
+__global__ __launch_bounds__(512, 2) void k_q1_stats_wide(const LT *__restrict__ lg, int64_t step_stride,
+                                                          int64_t stream_stride, const int32_t *__restrict__ sym,
+                                                          int64_t B, int64_t rows, int64_t V, int64_t t0, uint32_t xsh,
+                                                          int64_t G, RowStats *__restrict__ out,
+                                                          uint64_t *__restrict__ chunks, float *__restrict__ mrow,
+                                                          uint64_t *__restrict__ xch, int split, int kg, int rpx) {
+    constexpr int N = LogitN<LT>::N, NT = 512, NW = 8;
+    constexpr bool IMAX = LAC_Q1_IMAX && sizeof(LT) == 2;
+    static_assert(R % 8 == 0, "group totals in batches of 8 vectors");
+    __shared__ uint32_t tabr[LAC_Q1_TAB_SIZE * kQ1Rep];
+    __shared__ float smax[NW];
+    __shared__ int smaxi[NW];
+    __shared__ uint64_t ssum[NW][2];
+    __shared__ uint32_t sps;
+    __shared__ unsigned long long bins[DEC ? 64 : 1];
+    __shared__ uint32_t sxv;
+    __shared__ int sxok;
+    const int tid = threadIdx.x, lane = tid & 63, w = wave_in_block();
+    // GROUP: this block's segment of its rows (slot sq of its XCD)
+    const int sq = (int)(blockIdx.x >> 3), hh = GROUP ? sq % kg : 0;
+    const int vofs = hh * split;                               // vectors of the row before the segment
+    const int nrow = (int)(V / N);
+    const int nvec = GROUP ? (hh < kg - 1 ? split : nrow - (kg - 1) * split) : nrow;
+    const int64_t stride = GROUP ? 8 * (int64_t)rpx : (int64_t)gridDim.x;
+    const int64_t r0 = GROUP ? (int64_t)(sq / kg) * 8 + (blockIdx.x & 7) : (int64_t)blockIdx.x;
+    auto row_of = [&](int64_t r) {
+        return lg + (t0 + r / B) * step_stride + (r % B) * stream_stride + (int64_t)vofs * N;
+    };
+    // one buffer resource per row (SGPRs) sized to the row: vector tid + 512 j at
+    // voffset tid * 16 + soffset j * 8192, one offset VGPR for all R loads; loads past
+    // the row return 0 without touching memory, and pass 1 masks those vectors
+    auto rsrc = [&](int64_t r) {                               // no row (r >= rows): 0 bytes, loads return 0
+        return __builtin_amdgcn_make_buffer_rsrc(const_cast<LT *>(r < rows ? row_of(r) : lg), 0,
+                                                 r < rows ? nvec * 16 : 0, 0x00020000);
+    };
+    // GROUP: post this segment's value for the row and fold in the partners' (block-wide)
+    uint32_t seq = 0;
+    bool pok = true;                                           // every exchange of this row came
+    auto group_combine = [&](uint32_t v, auto op) {
+        seq++;
+        if (tid == 0) group_post<1>(xch, 0, seq, v);
+        if (w == 0) {
+            bool ok = true;
+            const uint32_t res = group_poll<1>(xch, xch + 2 * gridDim.x, 0, kg, seq, v, op, &ok);
+            if (lane == 0) {
+                sxv = res;
+                sxok = ok;
+            }
+        }
+        __syncthreads();
+        pok = pok && sxok != 0;
+        return sxv;
+    };
+    auto load_vec = [&](const __amdgpu_buffer_rsrc_t &rs, int j) {
+        // soffset materialised next to its load (asm): 40 hoisted constants spilled SGPRs
+        uint32_t so;
+        asm volatile("s_mov_b32 %0, %1" : "=s"(so) : "i"(j * NT * 16));
+        return __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)tid * 16u, so, LAC_Q1_NT ? 2 : 0);
+    };
+    u32x4 x[R];
+    {                                                          // the first row, in flight during the table fill
+        const __amdgpu_buffer_rsrc_t rs = rsrc(r0);
+#pragma unroll
+        for (int j = 0; j < R; j++) x[j] = load_vec(rs, j);
+    }
+    if (DEC && w == 0) bins[lane] = 0;
+    q1_fill_tab_rep<kQ1Rep, NT>(tabr, xsh);
+    const uint32_t loff = (uint32_t)(lane & (kQ1Rep - 1)) << 2;
+    // the q1 weight of a -inf logit (index 0) -- what every vector past the row adds in
+    // pass 2 once pass 1 has made it -inf; subtracted from the totals instead of masking
+    // each vector (per-vector masks are loop-invariant: hoisted, they spilled)
+    const uint32_t tab0 = q1_entry(0, xsh);
+    for (int64_t r = r0; r < rows; r += stride) {          // (GROUP: a group's members share r)
+        // (the row was loaded during the previous row's pass 2: rolling prefetch)
+        pok = true;
+        // tid and nvec opaque per row: what is derived from them is recomputed where it
+        // is used instead of hoisted out of the row loop into live registers
+        int ti = tid, nv = nvec;
+        asm volatile("" : "+v"(ti), "+s"(nv));
+        // vectors past the row read as 0: -inf for the maximum (vectors j >= nv / NT only)
+        const int nfull = nv / NT;
+#pragma unroll
+        for (int j = 0; j < R; j++)
+            if (j >= nfull) x[j] = ti + NT * j < nv ? x[j] : neg_inf16(sizeof(LT));
+        float m;
+        if constexpr (IMAX) {                                  // (see k_q1_stats)
+            s16x2 pm = {(short)-32768, (short)-32768};
+#pragma unroll
+            for (int j = 0; j < R; j++) {
+                pm = __builtin_elementwise_max(pm, as_s16x2(x[j].x));
+                pm = __builtin_elementwise_max(pm, as_s16x2(x[j].y));
+                pm = __builtin_elementwise_max(pm, as_s16x2(x[j].z));
+                pm = __builtin_elementwise_max(pm, as_s16x2(x[j].w));
+            }
+            const int li = pm.x > pm.y ? (int)pm.x : (int)pm.y;
+            const int wi = (int)wave_reduce((uint32_t)li, [](uint32_t a, uint32_t b) {
+                return (uint32_t)((int)a > (int)b ? (int)a : (int)b);
+            });
+            if (lane == 0) smaxi[w] = wi;
+            if (!DEC && tid == 0) sps = 0;
+            __syncthreads();
+            int bi = smaxi[0];
+#pragma unroll
+            for (int i = 1; i < NW; i++) bi = smaxi[i] > bi ? smaxi[i] : bi;
+            if constexpr (GROUP)                               // the int max of all segments
+                bi = (int)group_combine((uint32_t)bi, [](uint32_t a, uint32_t b) { return (int)a > (int)b ? a : b; });
+            if (bi >= 0 && bi <= 0x7F80) {                    // block-uniform (GROUP: the same in every segment)
+                m = __uint_as_float((uint32_t)bi << 16);
+            } else {
+                float mx = -INFINITY;
+#pragma unroll
+                for (int j = 0; j < R; j++)
+#pragma unroll
+                    for (int e = 0; e < N; e++) mx = fmaxf(mx, logit_at<LT>(x[j], e));
+                mx = wave_max_f32(mx);
+                if (lane == 0) smax[w] = mx;
+                __syncthreads();
+                m = smax[0];
+#pragma unroll
+                for (int i = 1; i < NW; i++) m = fmaxf(m, smax[i]);
+                if constexpr (GROUP)
+                    m = __uint_as_float(group_combine(__float_as_uint(m), [](uint32_t a, uint32_t b) { return f32_max_bits(a, b); }));
+            }
+        } else {
+            float mx = -INFINITY;
+#pragma unroll
+            for (int j = 0; j < R; j++)
+#pragma unroll
+                for (int e = 0; e < N; e++) mx = fmaxf(mx, logit_at<LT>(x[j], e));
+            mx = wave_max_f32(mx);
+            if (lane == 0) smax[w] = mx;
+            if (!DEC && tid == 0) sps = 0;
+            __syncthreads();
+            m = smax[0];
+#pragma unroll
+            for (int i = 1; i < NW; i++) m = fmaxf(m, smax[i]);
+            if constexpr (GROUP)
+                m = __uint_as_float(group_combine(__float_as_uint(m), [](uint32_t a, uint32_t b) { return f32_max_bits(a, b); }));
+        }
+        const bool fast = q1_fast_row(m);
+        const float c = q1_c(m);
+        uint64_t tot = 0, lo = 0;
+        int jl = 0;
+        if (!DEC) {
+            const int64_t s = sym[(t0 + r / B) * B + r % B];
+            const int sc = (int)(s < 0 ? 0 : (s > V ? V : s));
+            int sfull = sc / N;
+            const int sr = sc - sfull * N;
+            sfull -= vofs;                                     // GROUP: < 0 / >= nv: another segment's
+            const int sfc = sfull < 0 ? 0 : (sfull > nv ? nv : sfull);
+            const int js = sfull / NT, so = sfull - js * NT;  // vector js of thread so holds s
+            jl = sfc > ti ? (sfc - ti + NT - 1) / NT : 0;      // this thread's vectors below it: j < jl
+            if (sfull >= 0 && sfull < nv && w == so / 64 && js < R) {   // that thread's wave (uniform): split the
+                u32x4 v = x[0];                                // vector once, before pass 2
+#pragma unroll
+                for (int j = 1; j < R; j++)
+                    if (j == js) v = x[j];                     // (js uniform: scalar branches)
+                uint32_t pl = 0, ps = 0;
+#pragma unroll
+                for (int e = 0; e < N; e++) {
+                    const uint32_t q = q1_rep_at(tabr, q1_j(logit_at<LT>(v, e), c), loff);
+                    pl += e < sr ? q : 0;
+                    ps += e == sr ? q : 0;
+                }
+                const bool own = ti == so;
+                lo = own ? pl : 0;
+                if (own) sps = ps;
+            }
+        }
+        if (sizeof(LT) == 2) {                                 // re-unpack in pass 2 (see k_q1_stats)
+#pragma unroll
+            for (int j = 0; j < R; j++) asm volatile("" : "+v"(x[j]));
+        }
+        // pass 2: lane sums of 8 vectors at a time in 32 bits (entries <= 2^24, at most 64
+        // of them), folded into 64 bits per batch; DEC: the batch's 8 group totals.
+        // Vectors past the row are summed too (tab0 each logit) and taken off after.
+        // rolling prefetch: once vector j is summed its registers load vector j of the
+        // block's next row, so that row streams in while this one is quantised (without
+        // it a CU alternated a load phase and a compute phase: 61 vs 71 % of peak at bf16
+        // Qwen2, profiles/r03/wide1/)
+        const __amdgpu_buffer_rsrc_t rsn = rsrc(r + stride);
+        // The fast / capped choice is a branch per batch around the sums only, with the
+        // loads after it: with the whole pass 2 duplicated per branch, the next row's
+        // registers met from two paths and the allocator spilled them (134-208 VGPRs).
+        // Batches wholly past the row (NT j0 >= nv, uniform) skip their sums; their loads
+        // are still issued (past the row they touch no memory) so that the registers
+        // never meet from two paths.
+        auto batch = [&](int j0) {
+            uint32_t sv[8];
+            const bool live = NT * j0 < nv;
+            if (live && fast) {
+#pragma unroll
+                for (int u = 0; u < 8; u++) sv[u] = q1_vec_sum<LT>(x[j0 + u], c, true, tabr, loff);
+            } else if (live) {
+#pragma unroll
+                for (int u = 0; u < 8; u++) sv[u] = q1_vec_sum<LT>(x[j0 + u], c, false, tabr, loff);
+            } else {
+#pragma unroll
+                for (int u = 0; u < 8; u++) sv[u] = 0;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < 8; u++) x[j0 + u] = load_vec(rsn, j0 + u);
+            if (!live) return;
+            if constexpr (DEC) {
+                // group (w + 8 j) = vectors [64 (w + 8 j), +64): wave w's vector j
+                uint64_t gsum = wave_multi_sum32<8>(sv);        // lane l < 8: vector j0 + q_index<8>(l)
+                if (lane < 8) {
+                    const int grp = w + NW * (j0 + q_index<8>(lane)), past = (grp + 1) * 64 - nv;
+                    if (past > 0 && past < 64) gsum -= (uint64_t)past * N * tab0;   // the row's last group
+                    // (GROUP: segment group grp is the row's group vofs / 64 + grp; split is a multiple of 64)
+                    if (grp * 64 < nv) atomicAdd(&bins[(vofs / 64 + grp) / (int)G], (unsigned long long)gsum);
+                }
+            } else {
+                uint32_t bt = 0, bl = 0;
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    bt += sv[u];
+                    bl += j0 + u < jl ? sv[u] : 0;
+                }
+                asm volatile("" : "+v"(bt), "+v"(bl));          // folded here, not sunk to the row's end
+                tot += bt;
+                lo += bl;
+            }
+        };
+#pragma unroll
+        for (int j0 = 0; j0 < R; j0 += 8) { batch(j0); __builtin_amdgcn_sched_barrier(0); }
+        if (!DEC) {
+            const uint64_t t64 = wave_sum_u64(tot), l64 = wave_sum_u64(lo);
+            if (lane == 0) { ssum[w][0] = t64; ssum[w][1] = l64; }
+        }
+        __syncthreads();
+        if (DEC) {
+            if (w == 0) {
+                if constexpr (GROUP) {                         // into the zeroed chunk totals
+                    const uint64_t v = bins[lane] + (pok ? 0 : kGroupPoison);
+                    if (v) group_add(&chunks[r * 64 + lane], v);
+                    if (lane == 0 && hh == 0) mrow[r] = m;
+                } else {
+                    chunks[r * 64 + lane] = bins[lane];
+                    if (lane == 0) mrow[r] = m;
+                }
+                bins[lane] = 0;
+            }
+        } else if (tid == 0) {
+            uint64_t T = 0, L = 0;
+#pragma unroll
+            for (int i = 0; i < NW; i++) { T += ssum[i][0]; L += ssum[i][1]; }
+            const int nsum = 8 * NT * ((nv + 8 * NT - 1) / (8 * NT));   // vectors of the live batches
+            T -= (uint64_t)(nsum - nv) * N * tab0;             // those past the row
+            if constexpr (GROUP) {                              // the segments' partials add up
+                RowStats *o = out + r;                         // (zeroed; inv_tot 0: the coder divides)
+                group_add(&o->tot, T + (pok ? 0 : kGroupPoison));
+                group_add(&o->lo, L);
+                group_add(&o->hi, L + sps);
+                if (hh == 0) __hip_atomic_store(&o->minp, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                RowStats st;
+                st.lo = L;
+                st.hi = L + sps;
+                st.tot = T;
+                st.minp = 1;
+                st.inv_tot = 1.0 / (double)T;
+                st.pad = 0;
+                out[r] = st;
+            }
+        }
+    }
+}
+constexpr int kQ1WideR = 40;
+constexpr int kQ1WideMaxVec = 512 * kQ1WideR;
+
 // k_q1_decode: one wave per stream, sequential over a chunk of steps, from the
 // chunk totals of k_q1_stats: per step it finds the chunk holding
 // floor((x-l)*T/w), re-quantises only that chunk's logits and scans them to the
@@ -3355,6 +3656,19 @@ static int q1_stats_launch(lac_ctx *c, const Q1Args &a, hipStream_t st, const ui
     return LAC_OK;
 }
 
+template <typename LT, bool DEC>
+static int q1_wide_launch(lac_ctx *c, const Q1Args &a, hipStream_t st) {
+    const int64_t cap = (int64_t)c->cus;                         // one 8-wave block per CU
+    const unsigned grid = (unsigned)(a.rows < cap ? a.rows : cap);
+    const int64_t nvec = c->V / LogitN<LT>::N;
+    ProfScope ps(c, KID_Q1_STATS, st);
+    k_q1_stats_wide<LT, kQ1WideR, DEC><<<grid, 512, 0, st>>>(
+        (const LT *)a.lg, a.ss, a.bs, a.sym, c->B, a.rows, c->V, a.t0, a.xsh, q1_groups_per_chunk(nvec), c->stats,
+        c->q1chunks, c->q1m, nullptr, 0, 1, 0);
+    CHECK_LAUNCH();
+    return LAC_OK;
+}
+
 template <typename LT, bool DEC, int REP, int LASTN, int NT>
 static int q1_rl_kernel(lac_ctx *c, const Q1Args &a, hipStream_t st) {
     constexpr int NRB = 1024 / NT;
@@ -3472,6 +3786,49 @@ static int q1_stats_group_launch(lac_ctx *c, const Q1Args &a, hipStream_t st, co
     return q1_group_kernel<LT, DEC, kRLRep, 1024, 1024>(c, a, st, g);
 }
 
+// Shape 23: rows of > 20480 vectors in kg = ceil(vectors / 20480) segments of one
+// 8-wave block each (k_q1_stats_wide's GROUP form); false when the row would need
+// more segments than an XCD's CUs.
+static bool q1_wide_group(lac_ctx *c, int64_t nvec, Q1Group *g) {
+    const int64_t ngrp = (nvec + 63) / 64, spx = c->cus / 8;
+    for (int k = (int)((nvec + kQ1WideMaxVec - 1) / kQ1WideMaxVec); k <= kQ1MaxSeg && k <= spx; k++) {
+        const int64_t sp = 64 * ((ngrp + k - 1) / k), last = nvec - (k - 1) * sp;
+        if (k >= 2 && last > 0 && sp <= kQ1WideMaxVec && last <= kQ1WideMaxVec) {
+            g->k = k;
+            g->split = (int)sp;
+            g->nrb = 1;
+            return true;
+        }
+    }
+    return false;
+}
+
+template <typename LT, bool DEC>
+static int q1_wide_group_kernel(lac_ctx *c, const Q1Args &a, hipStream_t st, const Q1Group &g) {
+    const int64_t nvec = c->V / LogitN<LT>::N;
+    if (!c->pxch) HIPCHK(hipMalloc(&c->pxch, sizeof(uint64_t) * (8 * (int64_t)c->cus + 1)));
+    // rpx rows per XCD per round on rpx * k blocks of the XCD (one per CU: every member resident)
+    const int64_t spx = (int64_t)(c->cus / 8), rcap = spx / g.k, rneed = (a.rows + 7) / 8;
+    const int64_t rpx = rneed < rcap ? rneed : rcap;
+    const unsigned grid = (unsigned)(8 * rpx * g.k);
+    HIPCHK(hipMemsetAsync(c->pxch, 0, sizeof(uint64_t) * (2 * (int64_t)grid + 1), st));
+    if (DEC) HIPCHK(hipMemsetAsync(c->q1chunks, 0, sizeof(uint64_t) * 64 * a.rows, st));
+    else HIPCHK(hipMemsetAsync(c->stats, 0, sizeof(RowStats) * a.rows, st));
+    {
+        ProfScope ps(c, KID_Q1_STATS, st);
+        k_q1_stats_wide<LT, kQ1WideR, DEC, true><<<grid, 512, 0, st>>>(
+            (const LT *)a.lg, a.ss, a.bs, a.sym, c->B, a.rows, c->V, a.t0, a.xsh, q1_groups_per_chunk(nvec), c->stats,
+            c->q1chunks, c->q1m, c->pxch, g.split, g.k, (int)rpx);
+        CHECK_LAUNCH();
+    }
+    // repair: the tiled two-pass shape, gated on the abort word (as q1_group_kernel)
+    const uint64_t *gate = c->pxch + 2 * (int64_t)grid;
+    c->xch_abort = 2 * (int64_t)grid;
+    if (DEC) return q1_stats_launch<LT, 16, 16, DEC, true, false, 16>(c, a, st, gate);            // shape 10
+    if (sizeof(LT) == 4) return q1_stats_launch<LT, 16, 8, DEC, true, true, 16>(c, a, st, gate);  // shape 14
+    return q1_stats_launch<LT, 8, 8, DEC, true, false>(c, a, st, gate);                            // shape 8
+}
+
 // The register + LDS-slot shapes (k_q1_stats_rl), by rows per block:
 //   15 = one row of <= 16384 vectors (16 table copies when <= 16064: trimmed last slot), 16 = the same with 8
 //   copies always, 17 = four rows of <= 4096 vectors (4 waves each), 18 = two rows of <= 8192 (8 waves each).
@@ -3534,14 +3891,28 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
         // spills were removed (streamed butterfly, per-group LDS totals, fresh lane index),
         // 220 -> 210 us per step of 4096 rows vs shape 9, profiles/r02/q1_rl_dec/)
         if (sh == 0 && nvec <= 16384) sh = 15;
+        // rows of 16385..20480 vectors: one row per CU in the registers of an 8-wave
+        // block with a rolling prefetch (shape 22; same-box vs row groups,
+        // profiles/r03/wide/prefetch/: bf16 V = 151936 (Qwen2) 70.8 -> 85.6 % of peak,
+        // decode stats 270 -> 184-216 us per step; bf16 131080 63 -> 73 %; f32 65540
+        // 71.7 -> 80.5 %)
+        if (sh == 0 && nvec <= kQ1WideMaxVec) sh = 22;
         // longer rows: row groups (shapes 19 / 20 / 21: segments in row slots of 1 / 2 / 4
         // rows per block), the form that keeps the most bytes in flight (q1_group).
         // Round 2 had whole blocks per segment (kg = 2..4 blocks of 1 or 2 rows): bf16
         // V = 256000 48 -> 78 % of peak (profiles/r02/q1_pair_bf16/), Qwen2 bf16 57 -> 65 %
         // (profiles/r02/q1_groups2/); row slots at any kg: profiles/r03/q1_slots/
         Q1Group grp;
-        if (sh == 0 && nvec > 16384 && q1_group(c, nvec, DEC, sizeof(LT) == 2, 0, &grp))
+        if (sh == 0 && nvec > 16384 && q1_group(c, nvec, DEC, sizeof(LT) == 2, 0, &grp)) {
+            // where the best slot form has several rows per block, rows go to groups of
+            // 8-wave blocks instead (shape 23; same box, profiles/r03/wide/group/: bf16
+            // V = 262144 68.6 -> 80.1 % of peak (slots of the 4-row form before), f32
+            // 151936 79.6 -> 85.2 % (2-row form); one-row forms stay: bf16 256000 79.3 vs
+            // 77.8 %, f32 128256 83.7 vs 82.5 %, f32 262144 82.2 vs 82.1 %)
+            Q1Group wg;
+            if (grp.nrb > 1 && q1_wide_group(c, nvec, &wg)) return q1_wide_group_kernel<LT, DEC>(c, a, st, wg);
             return q1_stats_group_launch<LT, DEC>(c, a, st, grp);
+        }
         // measured at V = 128256 f32: encode tiles of (16,8) with the tile-rolling
         // prefetch 1.98 ms vs 2.18 for tiles of (8,8) (shape 13, its (8,8) form: 2.20)
         if (sh == 0) sh = nvec <= 64 * 16 * 16 ? 9 : (DEC ? 10 : (sizeof(LT) == 4 ? 14 : 8));
@@ -3560,6 +3931,8 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
     Q1Group grp;
     if (sh >= 19 && sh <= 21 && q1_group(c, nvec, DEC, sizeof(LT) == 2, sh == 19 ? 1 : sh == 20 ? 2 : 4, &grp))
         return q1_stats_group_launch<LT, DEC>(c, a, st, grp);
+    if (sh == 22 && nvec <= kQ1WideMaxVec) return q1_wide_launch<LT, DEC>(c, a, st);
+    if (sh == 23 && q1_wide_group(c, nvec, &grp)) return q1_wide_group_kernel<LT, DEC>(c, a, st, grp);
     if (sh == 13) return q1_stats_launch<LT, 8, 8, DEC, true, true>(c, a, st);         // tiles of (8,8,y)
     if (sh == 14) return q1_stats_launch<LT, 16, 8, DEC, true, true, 16>(c, a, st);    // tiles of (16,8,y)
     if (sh == 8) return q1_stats_launch<LT, 8, 8, DEC, true, false>(c, a, st);      // tiles of 4096 vectors
@@ -3759,7 +4132,7 @@ int lac_set_option(lac_ctx *c, int option, int64_t value) {
         c->fine_decode = (int)value;
         return LAC_OK;
     case LAC_OPT_Q1_SHAPE:
-        if (value < 0 || value > 21) return fail(LAC_E_ARG, "bad q1 shape");
+        if (value < 0 || value > 23) return fail(LAC_E_ARG, "bad q1 shape");
         c->q1_shape = (int)value;
         return LAC_OK;
     case LAC_OPT_MAPPING:

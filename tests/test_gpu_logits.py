@@ -258,7 +258,7 @@ def test_every_q1_shape_gives_the_same_bits(dtype, V):
     c.encode_logits_job(dl, sym)
     want, wn = c.to_bytes()
     ran = 0
-    for sh in range(1, 22):
+    for sh in range(1, 24):
         c.set_q1_shape(sh)
         try:
             c.encode_logits_job(dl, sym)
@@ -292,7 +292,7 @@ def test_paired_row_stats_many_rows(dtype, V, B, steps):
     sym = torch.randint(0, V, (steps, B), device=DEV, generator=g, dtype=torch.int32)
     c.encode_logits_job(dl, sym)
     a, na = c.to_bytes()
-    for sh in (14, 19, 20, 21):
+    for sh in (14, 19, 20, 21, 23) + ((22,) if V // (8 if dtype == "bf16" else 4) <= 20480 else ()):
         c.set_q1_shape(sh)
         c.encode_logits_job(dl, sym)
         assert c.to_bytes()[0] == a, sh
@@ -309,14 +309,14 @@ def test_paired_row_stats_many_rows(dtype, V, B, steps):
 
 
 def test_q1_shape_option_range():
-    """LAC_OPT_Q1_SHAPE takes 0 (AUTO) .. 21; anything else is refused with LAC_E_ARG."""
+    """LAC_OPT_Q1_SHAPE takes 0 (AUTO) .. 23; anything else is refused with LAC_E_ARG."""
     from lac_amd._lib import LacError, LAC_E_ARG
     c = _coder(1024, 4, 40)
-    for bad in (-1, 22, 99):
+    for bad in (-1, 24, 99):
         with pytest.raises(LacError) as e:
             c.set_q1_shape(bad)
         assert e.value.code == LAC_E_ARG
-    for ok in (0, 19, 20, 21):
+    for ok in (0, 19, 20, 21, 22, 23):
         c.set_q1_shape(ok)
     c.close()
 
