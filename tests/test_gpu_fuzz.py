@@ -74,6 +74,9 @@ def _logits_case(i):
     sizes += [128256, 128512, 128520, 131072] if dtype == "bf16" else [65536 - 8]
     # rows over groups of 2..4 blocks (shape 19)
     sizes += [131080, 151936, 262144, 300000] if dtype == "bf16" else [65540, 128256, 151936, 200000, 262144]
+    # a whole row per 8-wave block (shape 22: <= 20480 vectors) and either side of its
+    # limit (shape 23 past it)
+    sizes += [147464, 163840, 163848] if dtype == "bf16" else [73732, 81920, 81924]
     V = int(rng.choice(sizes))
     lo = max(int(np.ceil(np.log2(V))) + 2, 8)
     prec = int(rng.integers(lo, 62))
@@ -82,7 +85,7 @@ def _logits_case(i):
     while B * steps * V > 2_000_000 and B > 1:
         B //= 2
     scale = float(rng.choice([0.25, 3.0, 12.0]))
-    shape = int(rng.choice([0, 0, 0] + list(range(1, 21))))
+    shape = int(rng.choice([0, 0, 0] + list(range(1, 24))))
     return dtype, V, prec, B, steps, scale, shape
 
 

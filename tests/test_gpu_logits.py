@@ -236,7 +236,8 @@ def test_incremental_logits_encode_mixes_with_pmf_steps():
 @pytest.mark.parametrize("dtype,V", [("bf16", 32000), ("f32", 32000), ("bf16", 128256), ("f32", 65536),
                                      ("bf16", 128512), ("bf16", 128520), ("f32", 65540), ("f32", 128256),
                                      ("f32", 128512), ("f32", 128520), ("bf16", 131080), ("bf16", 151936),
-                                     ("f32", 151936), ("bf16", 262144), ("f32", 256000), ("f32", 262144)])
+                                     ("f32", 151936), ("bf16", 262144), ("f32", 256000), ("f32", 262144),
+                                     ("bf16", 163840), ("bf16", 163848), ("f32", 81920), ("f32", 81924)])
 def test_every_q1_shape_gives_the_same_bits(dtype, V):
     """Every forced row-stats shape (8/16-wave blocks, tiles, rolling prefetch,
     registers + LDS slots) yields the AUTO shape's bytes and decodes; shapes that
@@ -247,7 +248,11 @@ def test_every_q1_shape_gives_the_same_bits(dtype, V):
     of 1 / 2 / 4 rows per block; forced, they also split shorter rows): 2 slots at
     f32 65540 .. 128520 in the 1-row form, 5 slots of the 4-row form at bf16
     131080 / 151936 and f32 65540, 5 of the 2-row form at f32 151936, 9 at bf16
-    262144, 2 / 4 of the 8-copy 1-row form at f32 256000 / 262144 (Gemma 3)."""
+    262144, 2 / 4 of the 8-copy 1-row form at f32 256000 / 262144 (Gemma 3).
+    Rows of 16385..20480 vectors take one 8-wave block each (22: bf16 131080 /
+    151936 / 163840, f32 65540 / 81920), longer ones where the slot form would
+    put several rows in a block take groups of such blocks (23: bf16 163848 /
+    262144, f32 81924 / 151936); forced, 23 also splits shorter rows."""
     from lac_amd._lib import LacError
     B, steps, prec = 12, 3, 48
     x = _logits(777, steps, B, V, specials=True)
