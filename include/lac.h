@@ -94,8 +94,13 @@ enum {                       /* lac_set_option */
                                       forms of 15 / 18 / 17; slots are numbered across the
                                       blocks of an XCD, so a segment count need not divide
                                       the blocks); AUTO picks the form that fills its slots
-                                      best (bf16 V = 151936: 5 slots of 4 rows per block,
-                                      f32 V = 128256: 2 of 1); identical results, only speed
+                                      best (f32 V = 128256: 2 slots of 1 row per block),
+                                      22 = one row of <= 20480 vectors per 8-wave block,
+                                      whole in registers (AUTO for 16385..20480 vectors:
+                                      bf16 V = 151936), 23 = groups of such blocks (AUTO
+                                      where the slot form has several rows per block:
+                                      bf16 V = 262144, f32 V = 151936); identical results,
+                                      only speed
                                       differs */
     LAC_OPT_DECODE_FINE = 7,       /* one-wave decode (FUSED path): 1 = one total per 64 vectors of
                                       the row, so only 1 KB is re-read after the search (default,
@@ -259,7 +264,7 @@ int lac_encode_logits(lac_ctx *ctx, const void *logits_dev, int logit_type, int6
 int lac_decode_logits_steps(lac_ctx *ctx, const void *logits_dev, int logit_type, int64_t step_stride,
                             int64_t stream_stride, int64_t steps, int32_t *sym_out_dev, void *stream);
 
-/* Rows longer than a CU holds (LAC_OPT_Q1_SHAPE 19 / 20 / 21, AUTO for e.g. f32 V =
+/* Rows longer than a CU holds (LAC_OPT_Q1_SHAPE 19 / 20 / 21 / 23, AUTO for e.g. f32 V =
  * 128256) are split over 2..16 row slots of workgroups that exchange each row's
  * maximum, which needs every member resident.  When a member is not (another
  * kernel holds CUs) the waiting ones give up after ~0.1 s, raise the launch's

@@ -101,6 +101,10 @@ __device__ inline int lane_fresh() {
 // compiler cannot tell threadIdx.x >> 6 is uniform, so everything derived from
 // it (stream index, row pointers, coder state) would otherwise occupy VGPRs.
 __device__ inline int wave_in_block() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
+__device__ inline uint64_t rfl_u64(uint64_t x) {          // a wave-uniform value into SGPRs
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(x >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+}
 
 __device__ inline uint64_t shfl_u64(uint64_t v, int src) {
     const uint32_t lo = __shfl((int)(uint32_t)v, src), hi = __shfl((int)(uint32_t)(v >> 32), src);
@@ -519,18 +523,27 @@ __device__ inline void frac_pair(uint64_t f0, uint64_t f1, uint64_t c0, uint64_t
     *q1 = readlane_u64(q, 1);
 }
 
-template <typename E>
+// UNI: every argument and register is wave-uniform (k_encode keeps them in SGPRs),
+// so the chain runs on the scalar unit -- the two quotients one after the other
+// (a 64 x 64 -> 128-bit product is ~8 s_mul on the SALU, against four quarter-rate
+// v_mad_u64_u32 plus readlanes per lane-split pair) and the fudge test as one
+// compare against the row's precomputed threshold fthr = ceil(T / minp) (T > w minp
+// iff w < ceil(T / minp)).
+template <typename E, bool UNI = false>
 __device__ inline bool coder_step(EncState &st, int64_t &l, int64_t &h, uint64_t lo, uint64_t hi, uint64_t T,
                                   uint64_t minp, int64_t s, const E *row, int64_t V, int prec, uint64_t *pa,
                                   uint64_t *pc, uint64_t cap_words, uint64_t *trace_slot, int lane, int mapping,
                                   double inv_T = 0.0, bool allow_fudge = true, uint64_t flo = kNoFrac,
-                                  uint64_t fhi = kNoFrac) {
+                                  uint64_t fhi = kNoFrac, uint64_t fthr = 0) {
     if (s < 0 || s >= V) { st.err = LAC_E_SYMBOL_RANGE; return false; }   // arith_code.py:100-101
     if (T == 0) { st.err = LAC_E_TABLE; return false; }
     const uint64_t w = (uint64_t)(h - l + 1);
     uint64_t a, bb;
-    if (mapping == LAC_MAP_FLOOR || !is_fudged(T, w, minp)) {  // floor: Predictor/ACSampler; else ceil
-        if (flo != kNoFrac)
+    if (mapping == LAC_MAP_FLOOR || !(UNI ? w < fthr : is_fudged(T, w, minp))) {  // floor: Predictor/ACSampler; else ceil
+        if (UNI && flo != kNoFrac) {
+            a = frac_mul_div(flo, lo, w, T, mapping != LAC_MAP_FLOOR);
+            bb = frac_mul_div(fhi, hi, w, T, mapping != LAC_MAP_FLOOR);
+        } else if (flo != kNoFrac)
             frac_pair(flo, fhi, lo, hi, w, T, mapping != LAC_MAP_FLOOR, &a, &bb);
         else
             div_pair(lo, hi, w, mapping == LAC_MAP_FLOOR ? 0 : T - 1, T, inv_T != 0.0 ? inv_T : recip(T), &a, &bb);
@@ -540,6 +553,10 @@ __device__ inline bool coder_step(EncState &st, int64_t &l, int64_t &h, uint64_t
         const i128 xs = fudge_x(hi, s, w, T);
         a = s > 0 ? fudge_f(s - 1, xprev, T, w, V) : 0;
         bb = fudge_f(s, xs > xprev ? xs : xprev, T, w, V);
+    }
+    if (UNI) {                      // (the fudged branch's wave reductions leave them in VGPRs:
+        a = rfl_u64(a);             //  uniform again here, or l and h -- and the chain -- would
+        bb = rfl_u64(bb);           //  move to the vector unit)
     }
     if (a >= bb) { st.err = LAC_E_ZERO_WIDTH; return false; }   // the reference hangs here
     h = l + (int64_t)bb - 1;
@@ -671,7 +688,13 @@ __global__ __launch_bounds__(256) void k_encode(const RowStats *__restrict__ sta
         return;
     }
     uint64_t *pa = planeA + (uint64_t)b * cap_words, *pc = planeC + (uint64_t)b * cap_words;
-    int64_t l = st.l, h = st.h;
+    // the registers and plane words wave-uniform (SGPRs): the serial chain then runs on
+    // the scalar unit (coder_step<E, true>)
+    int64_t l = (int64_t)rfl_u64((uint64_t)st.l), h = (int64_t)rfl_u64((uint64_t)st.h);
+    st.L = rfl_u64(st.L);
+    st.wa = rfl_u64(st.wa);
+    st.wc = rfl_u64(st.wc);
+    st.nsym = (int64_t)rfl_u64((uint64_t)st.nsym);
     bool ok = true;
     for (int64_t g0 = 0; g0 < nsteps && ok; g0 += 64) {
         const int n = (int)((nsteps - g0) < 64 ? (nsteps - g0) : 64);
@@ -681,20 +704,22 @@ __global__ __launch_bounds__(256) void k_encode(const RowStats *__restrict__ sta
             my = stats[(g0 + lane) * B + b];
             mys = sym[(t0 + g0 + lane) * B + b];
         }
-        // the 64 steps' row fractions at once, one lane each: off the serial chain
+        // the 64 steps' row fractions and fudge thresholds at once, one lane each: off
+        // the serial chain
         const uint64_t flo = lane < n ? row_frac(my.lo, my.tot) : kNoFrac;
         const uint64_t fhi = lane < n ? row_frac(my.hi, my.tot) : kNoFrac;
+        const uint64_t fthr = lane < n && my.minp ? div_floor((u128)my.tot + (my.minp - 1), my.minp) : 0;
         for (int i = 0; i < n; i++) {
             const uint64_t lo = readlane_u64(my.lo, i), hi = readlane_u64(my.hi, i);
             const uint64_t T = readlane_u64(my.tot, i), minp = readlane_u64(my.minp, i);
             const uint64_t invb = readlane_u64(__builtin_bit_cast(uint64_t, my.inv_tot), i);
-            const uint64_t fl = readlane_u64(flo, i), fh = readlane_u64(fhi, i);
+            const uint64_t fl = readlane_u64(flo, i), fh = readlane_u64(fhi, i), ft = readlane_u64(fthr, i);
             const int64_t s = __builtin_amdgcn_readlane(mys, i);
             const int64_t t = t0 + g0 + i;
             const E *row = pmf + t * step_stride + b * stream_stride;
-            if (!coder_step<E>(st, l, h, lo, hi, T, minp, s, row, V, prec, pa, pc, cap_words,
-                               trace ? trace + 2 * (t * B + b) : nullptr, lane, mapping,
-                               __builtin_bit_cast(double, invb), allow_fudge, fl, fh)) {
+            if (!coder_step<E, true>(st, l, h, lo, hi, T, minp, s, row, V, prec, pa, pc, cap_words,
+                                     trace ? trace + 2 * (t * B + b) : nullptr, lane, mapping,
+                                     __builtin_bit_cast(double, invb), allow_fudge, fl, fh, ft)) {
                 ok = false;
                 break;
             }
@@ -1399,12 +1424,22 @@ __global__ __launch_bounds__(64 * LAC_STREAM_WG, LAC_DECF_MINW) void k_decode_wa
     const uint64_t mynbits = nbits[b];
     const int nvec = (int)(V / VEC), nit = (nvec + 63) / 64, ngrp = (nit + 7) / 8;
 #if LAC_DEC_XPF
-    typename VecT<E, VEC>::type xb[8];
+    // XD = 2: two groups in flight (g + 1 and g + 2) while group g is summed, and the
+    // next row's groups 0 and 1 over the step's tail; rows of <= 128 iterations (u64:
+    // <= 256) only (240-250 VGPRs; longer u32 rows' second buffer spilled)
+    constexpr int XD = (LAC_DEC_XPF >= 2 && (NR <= 2 || (W && NR <= 4))) ? 2 : 1;
+    typename VecT<E, VEC>::type xb[8], xb2[8];
     if (nsteps > 0) {
         const E *row0 = pmf + b * stream_stride;
 #pragma unroll
         for (int u = 0; u < 8; u++)
             xb[u] = nvec >= 512 ? load_vec<E, VEC>(row0, u * 64 + lane) : load_vec_or0<E, VEC>(row0, u * 64 + lane, nvec);
+        if (XD == 2 && ngrp > 1) {
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                xb2[u] = nvec >= 1024 ? load_vec<E, VEC>(row0, (8 + u) * 64 + lane)
+                                      : load_vec_or0<E, VEC>(row0, (8 + u) * 64 + lane, nvec);
+        }
     }
 #endif
     for (int64_t t = 0; t < nsteps; t++) {
@@ -1428,12 +1463,17 @@ __global__ __launch_bounds__(64 * LAC_STREAM_WG, LAC_DECF_MINW) void k_decode_wa
             typename VecT<E, VEC>::type x[8];
 #pragma unroll
             for (int u = 0; u < 8; u++) x[u] = xb[u];
-            if (g + 1 < ngrp) {
-                const bool nf = g + 1 < nfull;
+            if constexpr (XD == 2) {
+#pragma unroll
+                for (int u = 0; u < 8; u++) xb[u] = xb2[u];
+            }
+            auto &nb = XD == 2 ? xb2 : xb;                    // group g + XD into the freed buffer
+            if (g + XD < ngrp) {
+                const bool nf = g + XD < nfull;
 #pragma unroll
                 for (int u = 0; u < 8; u++) {
-                    const int vi = ((g + 1) * 8 + u) * 64 + lane;
-                    xb[u] = nf ? load_vec<E, VEC>(row, vi) : load_vec_or0<E, VEC>(row, vi, nvec);
+                    const int vi = ((g + XD) * 8 + u) * 64 + lane;
+                    nb[u] = nf ? load_vec<E, VEC>(row, vi) : load_vec_or0<E, VEC>(row, vi, nvec);
                 }
             }
 #else
@@ -1478,6 +1518,13 @@ __global__ __launch_bounds__(64 * LAC_STREAM_WG, LAC_DECF_MINW) void k_decode_wa
             for (int u = 0; u < 8; u++) {
                 const int vi = u * 64 + lane;
                 xb[u] = nfull > 0 ? load_vec<E, VEC>(nrow, vi) : load_vec_or0<E, VEC>(nrow, vi, nvec);
+            }
+            if (XD == 2 && ngrp > 1) {                        // and its group 1
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const int vi = (8 + u) * 64 + lane;
+                    xb2[u] = nfull > 1 ? load_vec<E, VEC>(nrow, vi) : load_vec_or0<E, VEC>(nrow, vi, nvec);
+                }
             }
         }
 #endif
