@@ -2907,7 +2907,7 @@ __global__ __launch_bounds__(1024, 4) void k_q1_stats_rl(const LT *__restrict__ 
 // maximum through group_post / group_poll and add their partials into the zeroed
 // outputs with relaxed atomics; a partner that never posts sets the launch's abort
 // word and poisons the row, and the gated repair launch recomputes every row.
-template <typename LT, int R, bool DEC, bool GROUP = false>
+template <typename LT, int R, bool DEC, bool GROUP = false, int L = 0>
 __global__ __launch_bounds__(512, 2) void k_q1_stats_wide(const LT *__restrict__ lg, int64_t step_stride,
                                                           int64_t stream_stride, const int32_t *__restrict__ sym,
                                                           int64_t B, int64_t rows, int64_t V, int64_t t0, uint32_t xsh,
@@ -2925,6 +2925,9 @@ __global__ __launch_bounds__(512, 2) void k_q1_stats_wide(const LT *__restrict__
     __shared__ unsigned long long bins[DEC ? 64 : 1];
     __shared__ uint32_t sxv;
     __shared__ int sxok;
+    // L > 0: vectors j = R .. R + L - 1 of each thread in LDS slots (slot k of thread t
+    // at slots[k NT + t], filled by LDS-DMA), for rows of NT R < vectors <= NT (R + L)
+    __shared__ u32x4 slots[L > 0 ? L * NT : 1];
     const int tid = threadIdx.x, lane = tid & 63, w = wave_in_block();
     // GROUP: this block's segment of its rows (slot sq of its XCD)
     const int sq = (int)(blockIdx.x >> 3), hh = GROUP ? sq % kg : 0;
@@ -2967,11 +2970,28 @@ __global__ __launch_bounds__(512, 2) void k_q1_stats_wide(const LT *__restrict__
         asm volatile("s_mov_b32 %0, %1" : "=s"(so) : "i"(j * NT * 16));
         return __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)tid * 16u, so, LAC_Q1_NT ? 2 : 0);
     };
+    // LDS-DMA as asm (see k_q1_stats_rl: untracked by the compiler's wait counting, so
+    // pass 1 waits vmcnt(0) itself and a slot is refilled after lgkmcnt(0)); lanes past
+    // the row load its last vector (masked when read)
+    const uint32_t slot_base = (uint32_t)(uintptr_t)(lvoid_t *)&slots[w * 64];   // wave-uniform
+    auto ld_slot = [&](const LT *rw, int k) {
+        const int vi = tid + NT * (R + k);
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(rw) + (vi < nvec ? vi : nvec - 1);
+        uint32_t keep;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" LAC_Q1_DMA_POLICY "\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(src), "s"(slot_base + (uint32_t)(k * NT * 16))
+                     : "memory");
+    };
     u32x4 x[R];
     {                                                          // the first row, in flight during the table fill
         const __amdgpu_buffer_rsrc_t rs = rsrc(r0);
 #pragma unroll
         for (int j = 0; j < R; j++) x[j] = load_vec(rs, j);
+        if (L > 0 && r0 < rows) {
+#pragma unroll
+            for (int kk = 0; kk < L; kk++) ld_slot(row_of(r0), kk);
+        }
     }
     if (DEC && w == 0) bins[lane] = 0;
     q1_fill_tab_rep<kQ1Rep, NT>(tabr, xsh);
@@ -2992,6 +3012,15 @@ __global__ __launch_bounds__(512, 2) void k_q1_stats_wide(const LT *__restrict__
 #pragma unroll
         for (int j = 0; j < R; j++)
             if (j >= nfull) x[j] = ti + NT * j < nv ? x[j] : neg_inf16(sizeof(LT));
+        if constexpr (L > 0) {                                 // this wave's LDS-DMA writes (asm: untracked)
+            __builtin_amdgcn_s_waitcnt(0);
+            asm volatile("" ::: "memory");
+        }
+        // slot vector k, read where used (past the row: -inf)
+        auto slot = [&](int kk) {
+            const u32x4 v = slots[kk * NT + ti];
+            return ti + NT * (R + kk) < nv ? v : neg_inf16(sizeof(LT));
+        };
         float m;
         if constexpr (IMAX) {                                  // (see k_q1_stats)
             s16x2 pm = {(short)-32768, (short)-32768};
@@ -3001,6 +3030,14 @@ __global__ __launch_bounds__(512, 2) void k_q1_stats_wide(const LT *__restrict__
                 pm = __builtin_elementwise_max(pm, as_s16x2(x[j].y));
                 pm = __builtin_elementwise_max(pm, as_s16x2(x[j].z));
                 pm = __builtin_elementwise_max(pm, as_s16x2(x[j].w));
+            }
+#pragma unroll
+            for (int kk = 0; kk < L; kk++) {
+                const u32x4 v = slot(kk);
+                pm = __builtin_elementwise_max(pm, as_s16x2(v.x));
+                pm = __builtin_elementwise_max(pm, as_s16x2(v.y));
+                pm = __builtin_elementwise_max(pm, as_s16x2(v.z));
+                pm = __builtin_elementwise_max(pm, as_s16x2(v.w));
             }
             const int li = pm.x > pm.y ? (int)pm.x : (int)pm.y;
             const int wi = (int)wave_reduce((uint32_t)li, [](uint32_t a, uint32_t b) {
@@ -3022,6 +3059,12 @@ __global__ __launch_bounds__(512, 2) void k_q1_stats_wide(const LT *__restrict__
                 for (int j = 0; j < R; j++)
 #pragma unroll
                     for (int e = 0; e < N; e++) mx = fmaxf(mx, logit_at<LT>(x[j], e));
+#pragma unroll
+                for (int kk = 0; kk < L; kk++) {
+                    const u32x4 v = slot(kk);
+#pragma unroll
+                    for (int e = 0; e < N; e++) mx = fmaxf(mx, logit_at<LT>(v, e));
+                }
                 mx = wave_max_f32(mx);
                 if (lane == 0) smax[w] = mx;
                 __syncthreads();
@@ -3037,6 +3080,12 @@ __global__ __launch_bounds__(512, 2) void k_q1_stats_wide(const LT *__restrict__
             for (int j = 0; j < R; j++)
 #pragma unroll
                 for (int e = 0; e < N; e++) mx = fmaxf(mx, logit_at<LT>(x[j], e));
+#pragma unroll
+            for (int kk = 0; kk < L; kk++) {
+                const u32x4 v = slot(kk);
+#pragma unroll
+                for (int e = 0; e < N; e++) mx = fmaxf(mx, logit_at<LT>(v, e));
+            }
             mx = wave_max_f32(mx);
             if (lane == 0) smax[w] = mx;
             if (!DEC && tid == 0) sps = 0;
@@ -3060,11 +3109,12 @@ __global__ __launch_bounds__(512, 2) void k_q1_stats_wide(const LT *__restrict__
             const int sfc = sfull < 0 ? 0 : (sfull > nv ? nv : sfull);
             const int js = sfull / NT, so = sfull - js * NT;  // vector js of thread so holds s
             jl = sfc > ti ? (sfc - ti + NT - 1) / NT : 0;      // this thread's vectors below it: j < jl
-            if (sfull >= 0 && sfull < nv && w == so / 64 && js < R) {   // that thread's wave (uniform): split the
+            if (sfull >= 0 && sfull < nv && w == so / 64 && js < R + L) {   // that thread's wave (uniform): split the
                 u32x4 v = x[0];                                // vector once, before pass 2
 #pragma unroll
                 for (int j = 1; j < R; j++)
                     if (j == js) v = x[j];                     // (js uniform: scalar branches)
+                if (L > 0 && js >= R) v = slot(js - R);
                 uint32_t pl = 0, ps = 0;
 #pragma unroll
                 for (int e = 0; e < N; e++) {
@@ -3135,6 +3185,49 @@ __global__ __launch_bounds__(512, 2) void k_q1_stats_wide(const LT *__restrict__
         };
 #pragma unroll
         for (int j0 = 0; j0 < R; j0 += 8) { batch(j0); __builtin_amdgcn_sched_barrier(0); }
+        // the slot vectors, 8 at a time; each slot refilled with the next row's vector once
+        // this wave's reads of it are done
+        if constexpr (L > 0) {
+            const bool nxt = r + stride < rows;                // uniform
+            const LT *nrw = nxt ? row_of(r + stride) : lg;
+#pragma unroll
+            for (int k0 = 0; k0 < L; k0 += 8) {
+                uint32_t sv[8];
+                if (fast) {
+#pragma unroll
+                    for (int u = 0; u < 8; u++) sv[u] = k0 + u < L ? q1_vec_sum<LT>(slot(k0 + u), c, true, tabr, loff) : 0;
+                } else {
+#pragma unroll
+                    for (int u = 0; u < 8; u++) sv[u] = k0 + u < L ? q1_vec_sum<LT>(slot(k0 + u), c, false, tabr, loff) : 0;
+                }
+                __builtin_amdgcn_s_waitcnt(0xc07f);            // lgkmcnt(0): the slot reads are done
+                if (nxt) {
+#pragma unroll
+                    for (int u = 0; u < 8; u++)
+                        if (k0 + u < L) ld_slot(nrw, k0 + u);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                const int j0 = R + k0;
+                if constexpr (DEC) {
+                    uint64_t gsum = wave_multi_sum32<8>(sv);
+                    if (lane < 8) {
+                        const int grp = w + NW * (j0 + q_index<8>(lane)), past = (grp + 1) * 64 - nv;
+                        if (past > 0 && past < 64) gsum -= (uint64_t)past * N * tab0;
+                        if (grp * 64 < nv) atomicAdd(&bins[(vofs / 64 + grp) / (int)G], (unsigned long long)gsum);
+                    }
+                } else {
+                    uint32_t bt = 0, bl = 0;
+#pragma unroll
+                    for (int u = 0; u < 8; u++) {
+                        bt += sv[u];
+                        bl += j0 + u < jl ? sv[u] : 0;
+                    }
+                    asm volatile("" : "+v"(bt), "+v"(bl));
+                    tot += bt;
+                    lo += bl;
+                }
+            }
+        }
         if (!DEC) {
             const uint64_t t64 = wave_sum_u64(tot), l64 = wave_sum_u64(lo);
             if (lane == 0) { ssum[w][0] = t64; ssum[w][1] = l64; }
@@ -3153,21 +3246,22 @@ __global__ __launch_bounds__(512, 2) void k_q1_stats_wide(const LT *__restrict__
                 bins[lane] = 0;
             }
         } else if (tid == 0) {
-            uint64_t T = 0, L = 0;
+            uint64_t T = 0, Ls = 0;
 #pragma unroll
-            for (int i = 0; i < NW; i++) { T += ssum[i][0]; L += ssum[i][1]; }
-            const int nsum = 8 * NT * ((nv + 8 * NT - 1) / (8 * NT));   // vectors of the live batches
+            for (int i = 0; i < NW; i++) { T += ssum[i][0]; Ls += ssum[i][1]; }
+            // vectors of the live batches (L > 0: rows past the registers, every batch live)
+            const int nsum = L > 0 ? NT * (R + L) : 8 * NT * ((nv + 8 * NT - 1) / (8 * NT));
             T -= (uint64_t)(nsum - nv) * N * tab0;             // those past the row
             if constexpr (GROUP) {                              // the segments' partials add up
                 RowStats *o = out + r;                         // (zeroed; inv_tot 0: the coder divides)
                 group_add(&o->tot, T + (pok ? 0 : kGroupPoison));
-                group_add(&o->lo, L);
-                group_add(&o->hi, L + sps);
+                group_add(&o->lo, Ls);
+                group_add(&o->hi, Ls + sps);
                 if (hh == 0) __hip_atomic_store(&o->minp, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } else {
                 RowStats st;
-                st.lo = L;
-                st.hi = L + sps;
+                st.lo = Ls;
+                st.hi = Ls + sps;
                 st.tot = T;
                 st.minp = 1;
                 st.inv_tot = 1.0 / (double)T;
@@ -3176,9 +3270,15 @@ __global__ __launch_bounds__(512, 2) void k_q1_stats_wide(const LT *__restrict__
             }
         }
     }
+    if constexpr (L > 0) {
+        __builtin_amdgcn_s_waitcnt(0);                         // no LDS-DMA outlives the block
+        asm volatile("" ::: "memory");
+    }
 }
 constexpr int kQ1WideR = 40;
-constexpr int kQ1WideMaxVec = 512 * kQ1WideR;
+constexpr int kQ1WideMaxVec = 512 * kQ1WideR;                  // registers only
+constexpr int kQ1WideL = 11;                                   // + LDS slots (the 32-copy table beside them)
+constexpr int kQ1WideSlotMaxVec = 512 * (kQ1WideR + kQ1WideL);
 
 // k_q1_decode: one wave per stream, sequential over a chunk of steps, from the
 // chunk totals of k_q1_stats: per step it finds the chunk holding
@@ -3709,9 +3809,14 @@ static int q1_wide_launch(lac_ctx *c, const Q1Args &a, hipStream_t st) {
     const unsigned grid = (unsigned)(a.rows < cap ? a.rows : cap);
     const int64_t nvec = c->V / LogitN<LT>::N;
     ProfScope ps(c, KID_Q1_STATS, st);
-    k_q1_stats_wide<LT, kQ1WideR, DEC><<<grid, 512, 0, st>>>(
-        (const LT *)a.lg, a.ss, a.bs, a.sym, c->B, a.rows, c->V, a.t0, a.xsh, q1_groups_per_chunk(nvec), c->stats,
-        c->q1chunks, c->q1m, nullptr, 0, 1, 0);
+    if (nvec <= kQ1WideMaxVec)
+        k_q1_stats_wide<LT, kQ1WideR, DEC><<<grid, 512, 0, st>>>(
+            (const LT *)a.lg, a.ss, a.bs, a.sym, c->B, a.rows, c->V, a.t0, a.xsh, q1_groups_per_chunk(nvec), c->stats,
+            c->q1chunks, c->q1m, nullptr, 0, 1, 0);
+    else                                                         // rows past the registers: + LDS slots
+        k_q1_stats_wide<LT, kQ1WideR, DEC, false, kQ1WideL><<<grid, 512, 0, st>>>(
+            (const LT *)a.lg, a.ss, a.bs, a.sym, c->B, a.rows, c->V, a.t0, a.xsh, q1_groups_per_chunk(nvec), c->stats,
+            c->q1chunks, c->q1m, nullptr, 0, 1, 0);
     CHECK_LAUNCH();
     return LAC_OK;
 }
@@ -3943,7 +4048,12 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
         // profiles/r03/wide/prefetch/: bf16 V = 151936 (Qwen2) 70.8 -> 85.6 % of peak,
         // decode stats 270 -> 184-216 us per step; bf16 131080 63 -> 73 %; f32 65540
         // 71.7 -> 80.5 %)
-        if (sh == 0 && nvec <= kQ1WideMaxVec) sh = 22;
+        // Rows of 20481..26112 vectors add 11 vectors per thread in LDS slots (same box,
+        // profiles/r03/vocabs/: bf16 V = 202048 (Llama-4) 66.9 -> 81.1 %, bf16 200024
+        // (o200k) 65.8 -> 76.0 %, f32 100280 (cl100k) 72.4 -> 80.4 %, f32 102400
+        // (DeepSeek) 78.5 -> 86.7 %; f32 decode stats 8-11 % faster); not the bf16
+        // decode form, which spills 21 VGPRs there (368 vs 306 us per step at 202048)
+        if (sh == 0 && nvec <= kQ1WideSlotMaxVec && !(DEC && sizeof(LT) == 2 && nvec > kQ1WideMaxVec)) sh = 22;
         // longer rows: row groups (shapes 19 / 20 / 21: segments in row slots of 1 / 2 / 4
         // rows per block), the form that keeps the most bytes in flight (q1_group).
         // Round 2 had whole blocks per segment (kg = 2..4 blocks of 1 or 2 rows): bf16
@@ -3956,8 +4066,12 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
             // V = 262144 68.6 -> 80.1 % of peak (slots of the 4-row form before), f32
             // 151936 79.6 -> 85.2 % (2-row form); one-row forms stay: bf16 256000 79.3 vs
             // 77.8 %, f32 128256 83.7 vs 82.5 %, f32 262144 82.2 vs 82.1 %)
+            // ... and only where those blocks are well filled: segments of ~12500 vectors
+            // (f32 V = 100280 / 102400, bf16 200024 / 202048: 61-63 % of a block) ran at
+            // 58-70 % against 66-79 % in the slot forms (profiles/r03/vocabs/)
             Q1Group wg;
-            if (grp.nrb > 1 && q1_wide_group(c, nvec, &wg)) return q1_wide_group_kernel<LT, DEC>(c, a, st, wg);
+            if (grp.nrb > 1 && q1_wide_group(c, nvec, &wg) && nvec >= 0.75 * wg.k * kQ1WideMaxVec)
+                return q1_wide_group_kernel<LT, DEC>(c, a, st, wg);
             return q1_stats_group_launch<LT, DEC>(c, a, st, grp);
         }
         // measured at V = 128256 f32: encode tiles of (16,8) with the tile-rolling
@@ -3978,7 +4092,7 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
     Q1Group grp;
     if (sh >= 19 && sh <= 21 && q1_group(c, nvec, DEC, sizeof(LT) == 2, sh == 19 ? 1 : sh == 20 ? 2 : 4, &grp))
         return q1_stats_group_launch<LT, DEC>(c, a, st, grp);
-    if (sh == 22 && nvec <= kQ1WideMaxVec) return q1_wide_launch<LT, DEC>(c, a, st);
+    if (sh == 22 && nvec <= kQ1WideSlotMaxVec) return q1_wide_launch<LT, DEC>(c, a, st);
     if (sh == 23 && q1_wide_group(c, nvec, &grp)) return q1_wide_group_kernel<LT, DEC>(c, a, st, grp);
     if (sh == 13) return q1_stats_launch<LT, 8, 8, DEC, true, true>(c, a, st);         // tiles of (8,8,y)
     if (sh == 14) return q1_stats_launch<LT, 16, 8, DEC, true, true, 16>(c, a, st);    // tiles of (16,8,y)

@@ -76,7 +76,7 @@ def _logits_case(i):
     sizes += [131080, 151936, 262144, 300000] if dtype == "bf16" else [65540, 128256, 151936, 200000, 262144]
     # a whole row per 8-wave block (shape 22: <= 20480 vectors) and either side of its
     # limit (shape 23 past it)
-    sizes += [147464, 163840, 163848] if dtype == "bf16" else [73732, 81920, 81924]
+    sizes += [147464, 163840, 163848, 202048, 208904] if dtype == "bf16" else [73732, 81920, 81924, 100280, 104456]
     V = int(rng.choice(sizes))
     lo = max(int(np.ceil(np.log2(V))) + 2, 8)
     prec = int(rng.integers(lo, 62))

@@ -237,7 +237,8 @@ def test_incremental_logits_encode_mixes_with_pmf_steps():
                                      ("bf16", 128512), ("bf16", 128520), ("f32", 65540), ("f32", 128256),
                                      ("f32", 128512), ("f32", 128520), ("bf16", 131080), ("bf16", 151936),
                                      ("f32", 151936), ("bf16", 262144), ("f32", 256000), ("f32", 262144),
-                                     ("bf16", 163840), ("bf16", 163848), ("f32", 81920), ("f32", 81924)])
+                                     ("bf16", 163840), ("bf16", 163848), ("f32", 81920), ("f32", 81924),
+                                     ("bf16", 202048), ("bf16", 208896), ("bf16", 208904), ("f32", 102400)])
 def test_every_q1_shape_gives_the_same_bits(dtype, V):
     """Every forced row-stats shape (8/16-wave blocks, tiles, rolling prefetch,
     registers + LDS slots) yields the AUTO shape's bytes and decodes; shapes that
@@ -249,10 +250,12 @@ def test_every_q1_shape_gives_the_same_bits(dtype, V):
     f32 65540 .. 128520 in the 1-row form, 5 slots of the 4-row form at bf16
     131080 / 151936 and f32 65540, 5 of the 2-row form at f32 151936, 9 at bf16
     262144, 2 / 4 of the 8-copy 1-row form at f32 256000 / 262144 (Gemma 3).
-    Rows of 16385..20480 vectors take one 8-wave block each (22: bf16 131080 /
-    151936 / 163840, f32 65540 / 81920), longer ones where the slot form would
-    put several rows in a block take groups of such blocks (23: bf16 163848 /
-    262144, f32 81924 / 151936); forced, 23 also splits shorter rows."""
+    Rows of 16385..20480 vectors take one 8-wave block each, in registers (22: bf16
+    131080 / 151936 / 163840, f32 65540 / 81920), up to 26112 with 11 more vectors
+    per thread in LDS slots (22: bf16 163848 / 202048 / 208896, f32 81924 /
+    102400); longer ones where the slot form would put several rows in a block and
+    the blocks fill well take groups of such blocks (23: bf16 262144, f32 151936);
+    forced, 23 also splits shorter rows."""
     from lac_amd._lib import LacError
     B, steps, prec = 12, 3, 48
     x = _logits(777, steps, B, V, specials=True)
@@ -297,7 +300,7 @@ def test_paired_row_stats_many_rows(dtype, V, B, steps):
     sym = torch.randint(0, V, (steps, B), device=DEV, generator=g, dtype=torch.int32)
     c.encode_logits_job(dl, sym)
     a, na = c.to_bytes()
-    for sh in (14, 19, 20, 21, 23) + ((22,) if V // (8 if dtype == "bf16" else 4) <= 20480 else ()):
+    for sh in (14, 19, 20, 21, 23) + ((22,) if V // (8 if dtype == "bf16" else 4) <= 26112 else ()):
         c.set_q1_shape(sh)
         c.encode_logits_job(dl, sym)
         assert c.to_bytes()[0] == a, sh
