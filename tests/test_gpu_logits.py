@@ -329,9 +329,10 @@ def test_q1_shape_option_range():
     c.close()
 
 
-@pytest.mark.parametrize("hog_s", [0.6, 0.02])
-def test_row_groups_while_another_kernel_holds_cus(hog_s):
-    """Rows over groups of blocks (f32 V = 128256: shape 19, AUTO) need every group
+@pytest.mark.parametrize("hog_s,shape", [(0.6, 0), (0.02, 0), (0.6, 23)])
+def test_row_groups_while_another_kernel_holds_cus(hog_s, shape):
+    """Rows over groups of blocks (f32 V = 128256: shape 19, AUTO; or forced 23,
+    groups of 8-wave blocks) need every group
     member resident.  A kernel on another stream holds all but 8 CUs (tests/native/
     hog.hip): for 0.6 s the waiting members give up, the launch aborts and the
     gated tiled launch recomputes every row; for 0.02 s the late members arrive in
@@ -356,6 +357,7 @@ def test_row_groups_while_another_kernel_holds_cus(hog_s):
     sym = torch.clamp(sym, max=V - 1)
     c.encode_logits_job(x, sym)
     want, wn = c.to_bytes()
+    c.set_q1_shape(shape)
     ok = torch.zeros(1, dtype=torch.int32, device=DEV)
     busy = torch.cuda.Stream(device=DEV)
     mine = torch.cuda.Stream(device=DEV)
