@@ -96,6 +96,9 @@ def main():
     ap.add_argument("--q1-shape", type=int, default=0, help="logits row-stats block shape (tuning)")
     ap.add_argument("--decode-path", default="auto", choices=("auto", "split", "fused", "fused_chunk", "stats", "block"))
     ap.add_argument("--block-waves", type=int, default=0, help="block decode path: waves per stream (tuning)")
+    ap.add_argument("--gather", action="store_true",
+                    help="run the bitstream gather (lac_amd.dist.BitstreamGatherer) even on one rank: a "
+                         "one-rank RCCL group, the gather inside the timed region, parity.gather_ok")
     ap.add_argument("--input", default="pmf", choices=("pmf", "logits-bf16", "logits-f32"),
                     help="pmf rows (BASELINE c3, default) or raw logits quantised in-kernel (q1, SURVEY §8(f)1)")
     args = ap.parse_args()
@@ -122,6 +125,10 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
+    elif args.gather:                                      # a one-rank group: no launcher, no rendezvous
+        import torch.distributed as dist
+        dist.init_process_group(backend, store=dist.HashStore(), rank=0, world_size=1,
+                                **({"device_id": dev} if backend == "nccl" else {}))
 
     from lac_amd import synth
     from lac_amd.batch import BatchCoder
@@ -156,7 +163,7 @@ def main():
 
     # N > 1: each job's bitstreams go to rank 0 over RCCL, packed and sized to the
     # payload, asynchronously (overlapping the next job's encode), double-buffered
-    gatherer = BitstreamGatherer(coder) if world > 1 else None
+    gatherer = BitstreamGatherer(coder) if (world > 1 or args.gather) else None
 
     def job():
         if logits_in:
@@ -322,7 +329,9 @@ def main():
         cname = workload_name(V, B, world)                      # BASELINE.json configs
         cfg = {"workload": f"{cname}: vocab={V}, {B} streams/GPU, {T} symbols/stream per job, prec={P}, {rows}",
                "vocab": V, "streams": B, "tokens": T, "prec": P, "pmf_bits": args.pmf_bits, "input": args.input,
-               "parallelism": f"streams sharded over {world} GPU(s)" + (f", {'RCCL' if backend == 'nccl' else backend} payload-sized bitstream gather to rank 0" if world > 1 else "")}
+               "parallelism": f"streams sharded over {world} GPU(s)" + (
+                   f", {'RCCL' if backend == 'nccl' else backend} payload-sized bitstream gather to rank 0"
+                   if gatherer else "")}
         value = world * B * T * args.steps / dt
         line = {
             "metric": METRIC if (V, B) == (32000, 4096) else

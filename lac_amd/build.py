@@ -1,6 +1,7 @@
 """Build liblac.so in-tree for gfx950:  python -m lac_amd.build"""
 from __future__ import annotations
 
+import glob
 import os
 import subprocess
 import sys
@@ -8,7 +9,9 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "lac_kernels.hip")
-DEPS = [SRC, os.path.join(HERE, "csrc", "lac_core.h"), os.path.join(REPO, "include", "lac.h")]
+# every header the kernels can #include: csrc/*.h and include/*.h (lac_tail.h,
+# lac_q1_table.h, ...), so a header edit always rebuilds
+DEPS = [SRC, *sorted(glob.glob(os.path.join(HERE, "csrc", "*.h"))), *sorted(glob.glob(os.path.join(REPO, "include", "*.h")))]
 OUT = os.path.join(HERE, "liblac.so")
 ARCH = os.environ.get("LAC_OFFLOAD_ARCH", "gfx950")
 

@@ -147,23 +147,51 @@ ternary = Predictor(3)
 
 
 # ------------------------------------------------------------------ tables
+def _cdf_array(d):
+    """An integer CDF as a 1-D int64/uint64 numpy array, or None when it needs exact
+    Python ints (object or float arrays, values beyond 64 bits).  Lists go
+    through np.fromiter -- never np.asarray, which turns [1, 2**63] into float64."""
+    if isinstance(d, np.ndarray):
+        return d if d.ndim == 1 and d.dtype.kind in "iu" else None
+    for dt in (np.int64, np.uint64):
+        try:
+            return np.fromiter(d, dtype=dt, count=len(d))
+        except (OverflowError, TypeError, ValueError):
+            continue
+    return None
+
+
 def _row_of(predictor):
-    """The predictor's current integer pmf row (numpy uint64) from its CDF."""
+    """(pmf, T): the predictor's current integer pmf row (numpy uint64) from its
+    CDF, and the row total as a Python int.  Integer CDFs convert in one
+    vectorised pass; anything else through exact Python ints."""
     fast = getattr(predictor, "pmf_row", None)
     if fast is not None:
-        return np.asarray(fast(), dtype=np.uint64)
+        r = np.asarray(fast(), dtype=np.uint64)
+        return r, int(r.sum(dtype=object)) if r.size else 0
     d = getattr(predictor, "dist", None)
     if d is None:
         raise TypeError(f"{type(predictor).__name__} exposes no probability table (.dist); the GPU coder "
                         "needs CDFPredictor/ProbPredictor-style predictors")
-    cdf = np.asarray([int(x) for x in d], dtype=object) if not isinstance(d, np.ndarray) or d.dtype == object \
-        else d.astype(object)
+    a = _cdf_array(d)
+    if a is not None and a.size:
+        if a.dtype.kind == "i" and a[0] < 0:
+            raise ValueError("dist is not monotone non-decreasing")
+        a = a.astype(np.uint64, copy=False)
+        if a.size > 1 and bool((a[1:] < a[:-1]).any()):
+            raise ValueError("dist is not monotone non-decreasing")
+        pmf = np.empty(a.size, dtype=np.uint64)
+        pmf[0] = a[0]
+        np.subtract(a[1:], a[:-1], out=pmf[1:])
+        return pmf, int(a[-1])
+    cdf = np.asarray([int(x) for x in d], dtype=object)
     pmf = np.empty(len(cdf), dtype=object)
-    pmf[0] = int(cdf[0])
-    pmf[1:] = cdf[1:] - cdf[:-1]
+    if len(cdf):
+        pmf[0] = int(cdf[0])
+        pmf[1:] = cdf[1:] - cdf[:-1]
     if any(int(x) < 0 for x in pmf):
         raise ValueError("dist is not monotone non-decreasing")
-    return np.array([int(x) for x in pmf], dtype=np.uint64)
+    return np.array([int(x) for x in pmf], dtype=np.uint64), int(cdf[-1]) if len(cdf) else 0
 
 
 _REF_MODULES = ("lac_amd.coder", "arith_code")          # this module and the reference's own
@@ -224,37 +252,132 @@ def _raise_for(code, sym=None):
     raise _lib.LacError(code, "coder error")
 
 
-class _Tables:
-    """Per-step rows from a predictor.  A uniform Predictor(n) becomes a row of n
-    ones coded with the floor mapping (Predictor.symbol_to_range, :69-70)."""
+def _is_static(predictor):
+    """A table predictor whose accept is the base no-op (Predictor.accept,
+    arith_code.py:71-72): its table never changes while it codes -- a static
+    model, coded with one stride-0 row (the reference's CDFPredictor fast case,
+    fudged_dist returning self.dist, :84-85)."""
+    return _impl(predictor, "accept") in (("Predictor.accept", mod) for mod in _REF_MODULES)
 
-    def __init__(self, predictor):
+
+def _declared_minp(predictor):
+    """The minp the reference's fudge test reads (arith_code.py:84), or None when
+    it is by definition the table's smallest positive entry: the base
+    ProbPredictor property (:129-131), an O(V) Python scan, is never called."""
+    prop = getattr(type(predictor), "minp", None)
+    if isinstance(prop, property):
+        f = prop.fget
+        if getattr(f, "__qualname__", None) == "ProbPredictor.minp" and getattr(f, "__module__", None) in _REF_MODULES:
+            return None
+    return getattr(predictor, "minp", None)
+
+
+def fudge_decisions_agree(T, minp, min_pos, prec):
+    """Whether fudged_dist's test ``T > w*minp`` (arith_code.py:84) with the
+    predictor's ``minp`` and with the table's smallest positive entry
+    ``min_pos`` (what the kernels use) agree for every width the coder can
+    pass, w in (2^(prec-1), 2^prec].  They differ exactly for the w with
+    w*lo < T <= w*hi (lo, hi the two minima in order): refuse only when that
+    range meets the coder's.  A minp of 0 (the reference's Llama_AC on rows with
+    zero CDF steps, llama_compress.py:43-45) always fudges, and so do the
+    kernels when T > 2^prec * min_pos."""
+    minp, min_pos = int(minp), int(min_pos)
+    if minp == min_pos:
+        return True
+    lo, hi = min(minp, min_pos), max(minp, min_pos)
+    wmin, wmax = (1 << (prec - 1)) + 1, 1 << prec
+    first = max(wmin, -(-T // hi))                     # smallest w with T <= w*hi
+    last = wmax if lo <= 0 else min(wmax, -(-T // lo) - 1)   # largest w with w*lo < T
+    return first > last
+
+
+class _Tables:
+    """Per-step rows from a predictor, converted once per table: a row is cached
+    until the coder calls ``accept`` (through :meth:`accept`); a static model
+    (``_is_static``) keeps its row -- and its device copy -- for as long as its
+    ``dist`` object and ``minp`` stay the same.  A uniform Predictor(n) becomes
+    a row of n ones coded with the floor mapping (Predictor.symbol_to_range,
+    :69-70)."""
+
+    def __init__(self, predictor, prec=None):
         self.p = predictor
+        self.prec = prec
         self.uniform = _is_uniform(predictor)
         self.mapping = "floor" if self.uniform else "ceil"
+        self.static = self.uniform or _is_static(predictor)
+        self._row = None
+        self._key = None
+        self._dev = None
+
+    def _static_key(self):
+        if self.uniform:
+            return (int(self.p.n),)
+        return (self.p.dist, getattr(self.p, "minp", None))
+
+    def begin(self):
+        """Start of a coder call: rows of adaptive predictors are re-read (the
+        caller may have driven the predictor in between)."""
+        if not self.static:
+            self._row = None
 
     def row(self):
+        if self._row is not None:
+            if not self.static:
+                return self._row
+            k = self._static_key()
+            if k[0] is self._key[0] and k[1:] == self._key[1:]:
+                return self._row
+        self._row = self._build()
+        self._dev = None
+        if self.static:
+            self._key = self._static_key()
+        return self._row
+
+    def _build(self):
         if self.uniform:
             return np.ones(int(self.p.n), dtype=np.uint64)
-        r = _row_of(self.p)
+        r, T = _row_of(self.p)
         # fudged_dist decides with the predictor's own minp (arith_code.py:84); the
-        # kernels take the row's smallest positive entry (:79-82): refuse a predictor
-        # whose minp says otherwise (a stale attribute, Llama_AC's zero-including
-        # minp on a row with zeros) instead of coding a different table
-        m = getattr(self.p, "minp", None)
-        if m is not None:
+        # kernels with the row's smallest positive entry (:79-82): a predictor whose
+        # minp could change that decision at some width (a stale attribute) is
+        # refused instead of being coded with another table
+        m = _declared_minp(self.p)
+        if m is not None and r.size:
             pos = r[r > 0]
-            if pos.size and int(m) != int(pos.min()):
+            if pos.size and int(m) != int(pos.min()) and (
+                    self.prec is None or not fudge_decisions_agree(T, m, int(pos.min()), self.prec)):
                 raise ValueError(f"{type(self.p).__name__}.minp = {int(m)} but its table's smallest positive "
-                                 f"entry is {int(pos.min())}: the GPU coder derives minp from the table")
+                                 f"entry is {int(pos.min())}, which changes fudged_dist's decision at some "
+                                 f"width: the GPU coder derives minp from the table")
         return r
+
+    def row_dev(self, device):
+        """The current row on ``device`` (int64 view of the uint64 entries, 1-D)."""
+        import torch
+        r = self.row()
+        if self._dev is None or self._dev.device != device:
+            self._dev = torch.from_numpy(r.view(np.int64)).to(device)
+        return self._dev
+
+    def accept(self, symbol):
+        self.p.accept(symbol)
+        if not self.static:
+            self._row = None
 
 
 # ------------------------------------------------------------------ encoder
 class A_to_bin:
     """Encoder (arith_code.py:156-246) backed by liblac.so (one stream).  A
     predictor with its own mapping (mapping_of == 'mapped') gets the
-    lac_amd.mapped encoder instead."""
+    lac_amd.mapped encoder instead.
+
+    A static model (a CDFPredictor whose accept is the base no-op) is coded as
+    one stride-0 row: ``run`` / ``encode`` / ``bits`` are one launch over the
+    whole symbol sequence, and ``encode`` / ``bits`` of a fresh coder take the
+    packed output straight from the device (no per-symbol digit trace).
+    Adaptive predictors are streamed in chunks of rows (``_CHUNK_BYTES``)."""
+
+    _CHUNK_BYTES = 32 << 20
 
     def __new__(cls, predictor=ternary, prec=16):
         if cls is A_to_bin and mapping_of(predictor) == "mapped":
@@ -270,8 +393,17 @@ class A_to_bin:
         self.debug_log = None
         self._coder = None
         self._V = None
+        self._tab = None
         self._plane_bits = 0          # output bits held in the device planes since the last reset
         self._nsym = 0                # symbols coded since the last reset
+
+    def _tables(self, begin=True):
+        t = self._tab
+        if t is None or t.p is not self.predictor:
+            t = self._tab = _Tables(self.predictor, self.precision)
+        if begin:
+            t.begin()
+        return t
 
     # -- device plumbing
     # Digits reach the caller through the per-symbol trace, so the device's own
@@ -281,33 +413,36 @@ class A_to_bin:
     # fits a fixed capacity.
     _SLACK = 256                      # flush digits + the word a rebase keeps
 
+    def _fresh(self):
+        """Registers at l = 0, h = 2^prec - 1 with nothing coded since (a symbol of
+        p > 1/2 narrows l, h without emitting a digit, so empty planes alone do
+        not mean fresh registers)."""
+        return self._coder is None or (self._plane_bits == 0 and self._nsym == 0)
+
     def _ensure(self, V, steps):
         per = self.precision + 1      # one symbol emits at most prec digits (renorm)
         need = (steps + 2) * per + self._SLACK
+        if self._coder is not None and self._V == V and self._fresh() and self._coder.capacity_bits < need:
+            self._coder.close()       # fresh: reallocate at the new size
+            self._coder = None
         if self._coder is not None and self._V == V:
             return
-        if self._coder is not None and (self._plane_bits or self._nsym):
+        if self._coder is not None and not self._fresh():
             raise RuntimeError(f"table size changed mid-stream ({self._V} -> {V} symbols); flush() first")
         if self._coder is not None:
             self._coder.close()
         self._coder = BatchCoder(V, 1, prec=self.precision, pmf_bits=64, capacity_bits=max(need * 2, 1 << 12))
-        self._coder.set_mapping(_Tables(self.predictor).mapping)
+        self._coder.set_mapping(self._tables(begin=False).mapping)
         self._V = V
         self._plane_bits = 0
         self._nsym = 0
 
     def _encode_rows(self, rows, syms):
-        """Encode rows/syms (chunked to the coder's capacity); -> (digit lists, (rc, n_ok))."""
+        """Encode syms with ``rows`` -- a [steps, V] array, or one 1-D row for every
+        step (a static model, stride 0) -- chunked to the coder's capacity;
+        -> (digit lists, (rc, n_ok))."""
         steps = len(syms)
-        V = len(rows[0])
-        if self._coder is not None and self._V == V and self._plane_bits == 0 and self._nsym == 0:
-            # a fresh coder (nothing coded since the last reset: a symbol of p > 1/2
-            # narrows l, h without emitting a digit, so empty planes alone do not
-            # mean fresh registers): reallocate at the new size
-            per = self.precision + 1
-            if self._coder.capacity_bits < (steps + 2) * per + self._SLACK:
-                self._coder.close()
-                self._coder = None
+        V = rows.shape[-1]
         self._ensure(V, steps)
         per = self.precision + 1
         out = []
@@ -319,42 +454,53 @@ class A_to_bin:
                 self._plane_bits = 64
                 continue
             n = min(room, steps - i)
-            digs, rc, n_ok = self._encode_chunk(rows[i:i + n], syms[i:i + n])
+            digs, rc, n_ok = self._encode_chunk(rows if rows.ndim == 1 else rows[i:i + n], syms[i:i + n])
             out.extend(digs)
             if rc:
                 return out, (rc, i + n_ok)
             i += n
         return out, (0, steps)
 
+    def _sym_tensor(self, syms):
+        """int32 [steps, 1] device symbols; values outside int32 become -1 (the
+        kernels report LAC_E_SYMBOL_RANGE for them as for any symbol >= V)."""
+        import torch
+        if isinstance(syms, np.ndarray):
+            a = np.where((syms >= 0) & (syms < 2 ** 31), syms, -1).astype(np.int32)
+        else:
+            a = np.fromiter((int(s) if 0 <= int(s) < 2 ** 31 else -1 for s in syms), dtype=np.int32,
+                            count=len(syms))
+        return torch.from_numpy(a).view(len(syms), 1).to(self._coder.device)
+
     def _encode_chunk(self, rows, syms):
         import torch
         steps = len(syms)
-        V = len(rows[0])
         dev = self._coder.device
-        pmf = torch.from_numpy(np.stack(rows).astype(np.uint64).view(np.int64).reshape(steps, 1, V)).to(dev)
-        sym = torch.tensor([int(s) if 0 <= int(s) < 2 ** 31 else -1 for s in syms], dtype=torch.int32,
-                           device=dev).view(steps, 1)
+        if rows.ndim == 1:
+            pmf = self._tab.row_dev(dev)                          # stride 0: one row for every step
+        else:
+            pmf = torch.from_numpy(np.ascontiguousarray(rows).view(np.int64).reshape(steps, 1, -1)).to(dev)
         tr = torch.zeros((steps, 1, 2), dtype=torch.int64, device=dev)
-        self._coder.encode(pmf, sym, trace=tr)
+        self._coder.encode(pmf, self._sym_tensor(syms), trace=tr)
         rc, err, step = self._coder.status()
         t = tr.cpu().numpy()
         # err_step counts symbols since the last reset: the failing one's index in this chunk
         n_ok = steps if rc == 0 else min(max(int(step[0]) - self._nsym, 0), steps)
         self._nsym += n_ok
         digs = [digits_of(int(E), int(k)) for E, k in t[:n_ok, 0]]
-        for d in digs:
-            self.emitted_bits += len(d)
-            self._plane_bits += len(d)
+        nd = int(t[:n_ok, 0, 1].sum()) if n_ok else 0
+        self.emitted_bits += nd
+        self._plane_bits += nd
         return digs, rc, n_ok
 
     # -- registers (reference attributes)
     @property
     def l(self):
-        return int(self._coder.registers()[0][0]) if self._coder else 0
+        return int(self._coder.registers()[0][0]) if not self._fresh() else 0
 
     @property
     def h(self):
-        return int(self._coder.registers()[1][0]) if self._coder else self.denom - 1
+        return int(self._coder.registers()[1][0]) if not self._fresh() else self.denom - 1
 
     def __repr__(self):
         sl = bin(self.l + (self.denom << 1))[3:]
@@ -363,16 +509,16 @@ class A_to_bin:
 
     # -- reference API
     def step(self, symbol):
-        tab = _Tables(self.predictor)
+        tab = self._tables()
         row = tab.row()
         if self.debug_log:                             # arith_code.py:170 (a truthy list, as there)
             self.debug_log.append((self.l, self.h, "recv", symbol))
-        digs, (rc, n_ok) = self._encode_rows([row], [symbol])
+        digs, (rc, n_ok) = self._encode_rows(row if tab.static else row[None, :], [symbol])
         if rc:
             _raise_for(rc, symbol)
         if self.debug_log:
             self._log_emits_back(digs[0])
-        self.predictor.accept(symbol)
+        tab.accept(symbol)
         yield from digs[0]
 
     def _log_emits_back(self, digits):
@@ -394,8 +540,7 @@ class A_to_bin:
 
     def flush(self):
         if self._coder is None:
-            tab = _Tables(self.predictor)
-            self._ensure(len(tab.row()), 0)
+            self._ensure(len(self._tables().row()), 0)
         l, h = (self.l, self.h) if self.debug_log else (0, 0)
         self._coder.finish()
         rc, err, step = self._coder.status()
@@ -412,16 +557,41 @@ class A_to_bin:
         self._plane_bits = 0
         self._nsym = 0
 
-    def _collect(self, symbols):
-        tab = _Tables(self.predictor)
-        rows, syms = [], []
-        for s in symbols:
-            rows.append(tab.row())
-            syms.append(s)
-            if not (0 <= int(s) < len(rows[-1])):
-                break                                   # the reference raises at this symbol
-            self.predictor.accept(s)
-        return rows, syms
+    @staticmethod
+    def _static_symbols(symbols, V):
+        """All symbols as an int64 array, cut after the first one outside [0, V)
+        (the reference raises there); -> (array, index of that symbol or None,
+        that symbol as given)."""
+        syms = symbols if isinstance(symbols, (list, tuple, np.ndarray)) else list(symbols)
+        try:
+            a = np.asarray(syms, dtype=np.int64).reshape(-1)
+        except (OverflowError, TypeError, ValueError):
+            a = np.array([int(s) if -2 ** 63 <= int(s) < 2 ** 63 else -1 for s in syms], dtype=np.int64)
+        bad = np.flatnonzero((a < 0) | (a >= V))
+        if bad.size:
+            k = int(bad[0])
+            return a[:k + 1], k, syms[k]
+        return a, None, None
+
+    def _chunks(self, tab, symbols):
+        """(rows, syms, stop_here) batches of an adaptive predictor: at most
+        _CHUNK_BYTES of rows each; accept runs for every symbol in range."""
+        it = iter(symbols)
+        while True:
+            rows, syms = [], []
+            for s in it:
+                r = tab.row()
+                rows.append(r)
+                syms.append(s)
+                if not (0 <= int(s) < len(r)):
+                    yield np.stack(rows), syms, True            # the reference raises at this symbol
+                    return
+                tab.accept(s)
+                if len(rows) * r.nbytes >= self._CHUNK_BYTES:
+                    break
+            if not syms:
+                return
+            yield np.stack(rows), syms, False
 
     def run(self, symbols, stop=1):
         if self.debug_log:                             # per-symbol registers for the log
@@ -430,23 +600,61 @@ class A_to_bin:
             if stop:
                 yield from self.flush()
             return
-        rows, syms = self._collect(symbols)
-        if syms:
+        tab = self._tables()
+        if tab.static:
+            row = tab.row()
+            syms, bad, bad_sym = self._static_symbols(symbols, len(row))
+            batches = [(row, syms)] if len(syms) else []
+        else:
+            batches = ((rows, syms) for rows, syms, _ in self._chunks(tab, symbols))
+            bad = None
+        for rows, syms in batches:
             digs, (rc, n_ok) = self._encode_rows(rows, syms)
             for d in digs:
                 yield from d
             if rc:
-                _raise_for(rc, syms[n_ok])
+                _raise_for(rc, bad_sym if bad is not None and n_ok == bad else int(syms[n_ok]))
         if stop:
             yield from self.flush()
 
+    def _encode_static_whole(self, tab, symbols):
+        """encode(symbols) of a fresh coder on a static model: one launch, the
+        flush and carry resolution on the device, R read from the packed bytes
+        (bytes(group_bits(bits())) is exactly R's L-bit binary)."""
+        row = tab.row()
+        V = len(row)
+        syms, bad, bad_sym = self._static_symbols(symbols, V)
+        n = len(syms) if bad is None else bad
+        self._ensure(V, n)
+        if n:
+            self._coder.encode(tab.row_dev(self._coder.device), self._sym_tensor(syms[:n]))
+            rc, err, step = self._coder.status()
+            if rc:
+                k = min(max(int(step[0]), 0), n - 1)
+                self._nsym = k
+                self._plane_bits = 1                   # registers are mid-stream now
+                _raise_for(rc, int(syms[k]))
+            self._nsym = n
+            self._plane_bits = 1
+        if bad is not None:
+            raise AssertionError("unknown symbol", bad_sym)
+        self._coder.finish()
+        data, nbits = self._coder.to_bytes()
+        L = int(nbits[0])
+        R = int.from_bytes(data[0], "big") >> (8 * len(data[0]) - L) if L else 0
+        self.emitted_bits += L
+        self._coder.reset()
+        self._plane_bits = 0
+        self._nsym = 0
+        return R, L
+
     def encode(self, symbols, stop=1):
-        r = 0
-        length = 0
-        for v in self.run(symbols, stop):
-            r = (r << 1) + v
-            length += 1
-        return r, length
+        if stop and not self.debug_log and not isinstance(self, MappedEncoderMixin) and self._fresh():
+            tab = self._tables()
+            if tab.static:
+                return self._encode_static_whole(tab, symbols)
+        d = np.fromiter(self.run(symbols, stop), dtype=np.int8)
+        return digits_value(d), len(d)
 
     @property
     def info(self):
@@ -463,8 +671,24 @@ class A_to_bin:
     def bits(self, symbols, stop=1):
         """Output bits (binary of sum d_k 2^(L-1-k), exactly L of them)."""
         r, L = self.encode(symbols, stop)
-        for k in range(L - 1, -1, -1):
-            yield (r >> k) & 1
+        if L:
+            b = np.unpackbits(np.frombuffer(r.to_bytes((L + 7) // 8, "big"), dtype=np.uint8))
+            yield from b[len(b) - L:].tolist()
+
+
+def digits_value(d):
+    """R = sum d_k 2^(L-1-k) of raw digits d (int8 array: 0..3, and -1 from a
+    flush whose l went negative, arith_code.py:193-202) in O(L): each digit
+    plane as one binary number, weighted."""
+    L = len(d)
+    if not L:
+        return 0
+    pad = (-L) % 8
+
+    def plane(m):
+        return int.from_bytes(np.packbits(m.astype(np.uint8)).tobytes(), "big") >> pad
+
+    return plane((d > 0) & (d & 1 == 1)) + (plane(d >= 2) << 1) - plane(d < 0)
 
 
 # ------------------------------------------------------------------ decoder
@@ -499,7 +723,7 @@ class _Session:
     def __init__(self, dec):
         self.dec = dec
         self.prec = dec.precision
-        self.tab = _Tables(dec.predictor)
+        self.tab = _Tables(dec.predictor, dec.precision)
         self.bits = []
         self.buf = np.zeros(64, dtype=np.uint8)
         self.dev = None
@@ -596,13 +820,13 @@ class _Session:
             if int(new["ndet"][0]) != 1:
                 return                                       # not determined by the bits so far
             self.st = new
-            self.dec.predictor.accept(s)
+            self.tab.accept(s)
             yield s
         while True:
             code, s = self.tail_step(_lib.LAC_TAIL_DECIDE)
             if code == 1:
                 return
-            self.dec.predictor.accept(s)
+            self.tab.accept(s)
             yield s
 
     def to_tail(self):
@@ -642,7 +866,7 @@ class _Session:
             code, s = self.tail_step(_lib.LAC_TAIL_FLUSH)
             if code == 1:
                 return
-            self.dec.predictor.accept(s)
+            self.tab.accept(s)
             yield s
 
     def close(self):
@@ -730,9 +954,13 @@ class A_from_bin:
                 sess.add_bit(b)
                 yield from sess.decide()
             return
-        data = bytes(group_bits(iter(bl)))
+        data = np.packbits(np.asarray(bl, dtype=np.uint8)).tobytes()     # group_bits' format
         sess.load_bits(bl, data)
         tab = sess.tab
+        if tab.static:
+            yield from self._fast_static(sess, max_symbols)
+            yield from sess.decide()
+            return
         for _ in range(max_symbols):
             row = tab.row()
             c = sess._coder_for(len(row))
@@ -745,9 +973,59 @@ class A_from_bin:
             if int(new["err"][0]) or int(new["ndet"][0]) != int(st["ndet"][0]) + 1:
                 break
             sess.st = new
-            self.predictor.accept(s)
+            tab.accept(s)
             yield s
         yield from sess.decide()                   # undetermined: nothing; window off [l, h]: the reference's way
+
+    def _fast_static(self, sess, max_symbols):
+        """Determined symbols of a static model in a few launches: chunks of
+        stride-0 steps (doubling) until one holds a symbol the bits do not
+        determine (or whose window leaves [l, h]); that chunk is then replayed
+        from its first registers up to the last determined symbol, so the session
+        parks exactly where the per-symbol loop would."""
+        tab = sess.tab
+        row = tab.row()
+        V = len(row)
+        c = sess._coder_for(V)
+        c.decode_open(sess.dev, sess.nb)
+        start = sess.st.copy()
+        start["det"] = 1
+        check(c.lib.lac_decode_set_state(c.ctx, start.ctypes.data_as(C.c_void_p), c._stream))
+        pmf = tab.row_dev(c.device).view(1, 1, V)
+        # first chunk: the bits over the table's entropy (+10 %), what a stream drawn
+        # from the table holds; doubling covers the rest, a replay the overshoot
+        p = row[row > 0].astype(np.float64)
+        p /= p.sum()
+        H = float(-(p * np.log2(p)).sum())
+        done, n = 0, int(min(1 << 20, 64 + 1.1 * len(sess.bits) / max(H, 1e-9)))
+        while done < max_symbols:
+            n = min(n, max_symbols - done)
+            out = c.decode(pmf.expand(n, 1, V))
+            new = np.zeros(1, dtype=_DEC_STATE)
+            check(c.lib.lac_decode_get_state(c.ctx, new.ctypes.data_as(C.c_void_p), c._stream))
+            got = int(new["ndet"][0]) - int(start["ndet"][0])
+            if int(new["err"][0]):
+                got = min(got, max(int(new["err_step"][0]) - int(start["nsym"][0]), 0))
+            if not int(new["err"][0]) and got == n:
+                syms = out[:, 0].cpu().tolist()
+                start = new
+            else:
+                k = max(min(got, n), 0)
+                syms = []
+                if k:                                   # replay the determined part of the chunk
+                    check(c.lib.lac_decode_set_state(c.ctx, start.ctypes.data_as(C.c_void_p), c._stream))
+                    syms = c.decode(pmf.expand(k, 1, V))[:, 0].cpu().tolist()
+                    start = np.zeros(1, dtype=_DEC_STATE)
+                    check(c.lib.lac_decode_get_state(c.ctx, start.ctypes.data_as(C.c_void_p), c._stream))
+                n = 0
+            for s in syms:
+                tab.accept(s)
+                yield s
+            done += len(syms)
+            sess.st = start
+            if not n:
+                return
+            n *= 2
 
     # ---- registers (arith_code.py:249-263): l, h and the received-bit interval [lb, hb]
     def _regs(self):
@@ -843,35 +1121,46 @@ class A_from_bin:
 
     def _decode_bytes(self, data, nbits, n, max_symbols=1 << 24):
         import torch
-        tab = _Tables(self.predictor)
+        tab = _Tables(self.predictor, self.precision)
         out = []
         coder = None
         limit = n if n is not None else max_symbols
-        for i in range(limit):
-            row = tab.row()
-            V = len(row)
-            if coder is None:
-                coder = BatchCoder(V, 1, prec=self.precision, pmf_bits=64, capacity_bits=max(nbits, 64) + 64)
-                coder.set_mapping(tab.mapping)
-                stride = ((len(data) + 7) // 8 + 1) * 8
-                buf = np.zeros((1, stride), dtype=np.uint8)
-                buf[0, :len(data)] = np.frombuffer(data, dtype=np.uint8)
-                self._bits = torch.from_numpy(buf).to(coder.device)
-                self._nbits = torch.tensor([nbits], dtype=torch.int64, device=coder.device)
-                coder.decode_open(self._bits, self._nbits)
-            pmf = torch.from_numpy(row.view(np.int64).reshape(1, 1, V)).to(coder.device)
-            s = int(coder.decode(pmf).cpu()[0, 0])
-            if s < 0:
-                rc, err, step = coder.status()
-                if n is None:
+        try:
+            for i in range(limit):
+                row = tab.row()
+                V = len(row)
+                if coder is None:
+                    coder = BatchCoder(V, 1, prec=self.precision, pmf_bits=64, capacity_bits=max(nbits, 64) + 64)
+                    coder.set_mapping(tab.mapping)
+                    stride = ((len(data) + 7) // 8 + 1) * 8
+                    buf = np.zeros((1, stride), dtype=np.uint8)
+                    buf[0, :len(data)] = np.frombuffer(data, dtype=np.uint8)
+                    self._bits = torch.from_numpy(buf).to(coder.device)
+                    self._nbits = torch.tensor([nbits], dtype=torch.int64, device=coder.device)
+                    coder.decode_open(self._bits, self._nbits)
+                if tab.static and n is not None:         # a static model: all n symbols in one launch
+                    syms = coder.decode(tab.row_dev(coder.device).view(1, 1, V).expand(n - i, 1, V))
+                    rc, err, step = coder.status()
+                    if rc:
+                        _raise_for(int(err[0]) or _lib.LAC_E_DECODE_RANGE)
+                    for s in syms[:, 0].cpu().tolist():
+                        out.append(s)
+                        tab.accept(s)
                     break
-                _raise_for(int(err[0]) or _lib.LAC_E_DECODE_RANGE)
-            if n is None and int(coder.determined()[0]) <= i:
-                break                                   # the bits do not determine symbol i
-            out.append(s)
-            self.predictor.accept(s)
-        if coder is not None:
-            coder.close()
+                pmf = torch.from_numpy(row.view(np.int64).reshape(1, 1, V)).to(coder.device)
+                s = int(coder.decode(pmf).cpu()[0, 0])
+                if s < 0:
+                    rc, err, step = coder.status()
+                    if n is None:
+                        break
+                    _raise_for(int(err[0]) or _lib.LAC_E_DECODE_RANGE)
+                if n is None and int(coder.determined()[0]) <= i:
+                    break                                   # the bits do not determine symbol i
+                out.append(s)
+                tab.accept(s)
+        finally:
+            if coder is not None:
+                coder.close()
         return out
 
 
@@ -928,13 +1217,38 @@ def ungroup_bits(groups, b=8):
 
 
 def measure_compress(comp, inp, print_every_out=100, print_every_inp=100, save_bits=None, inp_cb=lambda t: ""):
-    """bytes(group_bits(comp.bits(inp))) -- arith_code.py:401-420 (one GPU launch)."""
+    """bytes(group_bits(comp.bits(inp))) with progress lines -- arith_code.py:401-420.
+
+    The input is consumed lazily, as ``comp.bits`` pulls it, and every output
+    bit is appended to ``save_bits``.  A progress line ("n -> entropy  bits/tok",
+    carriage-return terminated) is printed as each input arrives while the
+    output count is a multiple of ``print_every_inp`` (the reference tests the
+    output count there, :409) and after every ``print_every_out`` output bits."""
     if save_bits is None:
         save_bits = []
-    syms = list(inp)
-    bits = list(comp.bits(iter(syms)))
-    save_bits.extend(bits)
-    if syms and print_every_inp:
+    n_in = n_out = 0
+    last = None
+
+    def progress():
         info = comp.total_encoded_entropy
-        print(len(syms), "->", info, "   ", info / len(syms), " bits/tok ", inp_cb(syms[-1]))
-    return bytes(group_bits(iter(bits)))
+        print(n_in, "->", info, "   ", info / n_in, " bits/tok ", inp_cb(last), end="        \r")
+
+    def inputs():
+        nonlocal n_in, last
+        for v in inp:
+            yield v
+            last = v
+            n_in += 1
+            if n_out % print_every_inp == 0:
+                progress()
+
+    def outputs(bits):
+        nonlocal n_out
+        for b in bits:
+            save_bits.append(b)
+            yield b
+            n_out += 1
+            if n_out % print_every_out == 0:
+                progress()
+
+    return bytes(group_bits(outputs(comp.bits(inputs()))))

@@ -159,31 +159,41 @@ class BitstreamGatherer:
     Per job, on every rank (``submit``): the coder's streams are packed on the
     device into a header of bit counts (2 bytes per stream when the coder's
     capacity is below 2^16 bits, else 4) plus the streams' bytes back to back
-    (``pack_bitstreams``), and the packed length -- one int64 -- is all-gathered,
-    asynchronously.  The sizes reach the host through a pinned copy on a side
-    stream, so the host waits only for this job's packing, never for the next
-    job's encode, which it has already enqueued.  At the next ``submit`` (or
-    ``drain``) every rank sends exactly its packed bytes to ``root`` and the root
-    receives them (one grouped send/recv batch: RCCL over xGMI), ordered after the
-    packing only.  xGMI carries the payload, the header and 8 bytes per rank --
-    not a worst-case slot per stream, and not to every rank.
+    (``pack_bitstreams``), and four int64 -- the packed length, the rank's stream
+    count, its slot width and header size -- are all-gathered, asynchronously.
+    Ranks may hold different numbers of streams (uneven shards).  Under nccl the
+    sizes reach the host through a pinned copy on a side stream, so the host
+    waits only for this job's packing, never for the next job's encode, which it
+    has already enqueued.  At the next ``submit`` (or ``drain``) every rank sends
+    exactly its packed bytes to ``root`` and the root receives them (one grouped
+    send/recv batch on the side stream: RCCL over xGMI), ordered after the
+    packing only.  Under nccl the root's own share takes the same batch as a send
+    to itself (``self_p2p``; NCCL group semantics), so a one-rank job runs every
+    line of the RCCL path; gloo has no self-pair, the root copies its share.
+    xGMI carries the payload, the header and 32 bytes per rank -- not a
+    worst-case slot per stream, and not to every rank.
 
-    On the root, ``last`` is the list of (payload, length) per rank of the last
-    job and ``last_unpacked()`` its streams as (bits [world * B, width], nbits).
-    ``bytes_sent`` / ``payload_bytes`` count what crossed the links and the
-    encoded bytes themselves (bench.py reports both).
+    On the root, ``last`` describes the last finished job (``last_job`` its
+    number, counting from 1) and ``last_unpacked()`` returns its streams as
+    (bits [sum of streams, width], nbits).  A job is finished when its slot is
+    reused (``depth`` jobs later) or by ``drain``.  ``bytes_sent`` /
+    ``payload_bytes`` count what crossed the links and the encoded bytes
+    themselves (bench.py reports both).
 
-    Under ``gloo`` (CPU tests, one-GPU rehearsals) the same exchange runs on host
-    tensors, synchronously.
+    Under ``gloo`` (CPU tests, one-GPU rehearsals) the same deferred exchange runs
+    on host tensors; only the streams, events and pinned copies are nccl's.
     """
 
-    def __init__(self, coder, group=None, depth: int = 2, root: int = 0):
+    META = 4                                                 # int64 per rank: L, streams, width, hdr
+
+    def __init__(self, coder, group=None, depth: int = 2, root: int = 0, self_p2p=None):
         import torch
         import torch.distributed as dist
         self.coder, self.group, self.depth, self.root = coder, group, max(1, int(depth)), int(root)
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.gloo = dist.get_backend(group) == "gloo"
+        self.self_p2p = (not self.gloo) if self_p2p is None else bool(self_p2p)
         self.width = coder.bits_stride()                      # cap_words * 8 bytes per stream
         self.hdr = 2 if self.width * 8 < (1 << 16) else 4
         B, dev = coder.streams, coder.device
@@ -192,16 +202,19 @@ class BitstreamGatherer:
         self.io_dev = torch.device("cpu") if self.gloo else torch.device(dev)
         self.slots = [(torch.empty((B, self.width), dtype=torch.uint8, device=dev),
                        torch.empty((B,), dtype=torch.int64, device=dev)) for _ in range(self.depth)]
-        self.recv = [[torch.empty(self.cap, dtype=torch.uint8, device=self.io_dev) for _ in range(self.world)]
-                     if self.rank == self.root else None for _ in range(self.depth)]
-        self.lens = [torch.empty(self.world, dtype=torch.int64, device=self.io_dev) for _ in range(self.depth)]
-        self.lens_host = [torch.empty(self.world, dtype=torch.int64).pin_memory()
-                          if not self.gloo and torch.cuda.is_available() else torch.empty(self.world, dtype=torch.int64)
-                          for _ in range(self.depth)]
+        # root: per slot and rank a receive buffer, (re)sized to the largest payload seen
+        self.recv = [[None] * self.world if self.rank == self.root else None for _ in range(self.depth)]
+        self.meta = [torch.empty(self.world * self.META, dtype=torch.int64, device=self.io_dev)
+                     for _ in range(self.depth)]
+        self.meta_host = [torch.empty(self.world * self.META, dtype=torch.int64).pin_memory()
+                          if not self.gloo and torch.cuda.is_available()
+                          else torch.empty(self.world * self.META, dtype=torch.int64) for _ in range(self.depth)]
+        self._shape_meta = torch.tensor([B, self.width, self.hdr], dtype=torch.int64, device=dev)
         self.state = [None] * self.depth                        # per slot: dict of the job in flight
         self.side = torch.cuda.Stream(device=dev) if not self.gloo else None
         self.k = 0
         self.last = None
+        self.last_job = 0
         self.bytes_sent = 0
         self.payload_bytes = 0
         self.jobs = 0
@@ -219,25 +232,23 @@ class BitstreamGatherer:
         self.coder.copy_bits_into(bits)                          # on the caller's stream
         self.coder.copy_nbits_into(nbits)
         payload, L = pack_bitstreams(bits, nbits, self.hdr)
+        mine = torch.cat([L.to(torch.int64).reshape(1), self._shape_meta])
         st = {"payload": payload, "nbits": nbits, "job": self.k}
         if self.gloo:
-            _all_gather(self.lens[i], L.reshape(1).to(torch.int64).cpu(), self.group, self.world)
-            st["lens"] = self.lens[i].tolist()
+            _all_gather(self.meta[i], mine.cpu(), self.group, self.world)
+            st["meta"] = self.meta[i].view(self.world, self.META).tolist()
             st["payload"] = payload.cpu()
             self.state[i] = st
-            self._send(i)
-            self._finish(i)
             return i
         ev = torch.cuda.Event()
         ev.record()                                             # packing done (caller's stream)
-        work = dist.all_gather_into_tensor(self.lens[i], L.reshape(1).to(torch.int64), group=self.group,
-                                           async_op=True)
+        work = dist.all_gather_into_tensor(self.meta[i], mine, group=self.group, async_op=True)
         with torch.cuda.stream(self.side):
             self.side.wait_event(ev)
             work.wait()                                         # the side stream waits for the sizes
-            self.lens_host[i].copy_(self.lens[i], non_blocking=True)
-            st["lens_ready"] = torch.cuda.Event()
-            st["lens_ready"].record(self.side)
+            self.meta_host[i].copy_(self.meta[i], non_blocking=True)
+            st["meta_ready"] = torch.cuda.Event()
+            st["meta_ready"].record(self.side)
         st["packed"] = ev
         self.state[i] = st
         return i
@@ -248,6 +259,13 @@ class BitstreamGatherer:
         for _, i in sorted((st["job"], i) for i, st in enumerate(self.state) if st is not None):
             self._send(i)
 
+    def _recv_buffer(self, i, r, n):
+        import torch
+        buf = self.recv[i][r]
+        if buf is None or buf.numel() < n:
+            buf = self.recv[i][r] = torch.empty(max(n, self.cap), dtype=torch.uint8, device=self.io_dev)
+        return buf
+
     def _send(self, i):
         """Post job i's exact-size send (every rank) / receives (root), once its
         sizes are on the host."""
@@ -256,26 +274,28 @@ class BitstreamGatherer:
         st = self.state[i]
         if st is None or "works" in st:
             return
-        if "lens" not in st:
-            st["lens_ready"].synchronize()                      # this job's packing + size gather only
-            st["lens"] = self.lens_host[i].tolist()
-        lens = st["lens"]
+        if "meta" not in st:
+            st["meta_ready"].synchronize()                      # this job's packing + size gather only
+            st["meta"] = self.meta_host[i].view(self.world, self.META).tolist()
+        lens = [m[0] for m in st["meta"]]
         ops = []
         if self.rank == self.root:
             for r in range(self.world):
-                if r != self.root:
-                    ops.append(dist.P2POp(dist.irecv, self.recv[i][r][:lens[r]], r, group=self.group))
-        else:
+                if r != self.root or self.self_p2p:
+                    ops.append(dist.P2POp(dist.irecv, self._recv_buffer(i, r, lens[r])[:lens[r]], r,
+                                          group=self.group))
+        if self.rank != self.root or self.self_p2p:
             ops.append(dist.P2POp(dist.isend, st["payload"][:lens[self.rank]], self.root, group=self.group))
         ctx = torch.cuda.stream(self.side) if not self.gloo else _nullctx()
         with ctx:
             if not self.gloo:
                 self.side.wait_event(st["packed"])
             st["works"] = dist.batch_isend_irecv(ops) if ops else []
-        if self.rank == self.root:                              # the root's own share: a local copy
-            self.recv[i][self.root][:lens[self.root]].copy_(st["payload"][:lens[self.root]], non_blocking=True)
-        self.bytes_sent += sum(lens) - lens[self.root] + 8 * self.world
-        self.payload_bytes += sum(lens) - self.world * self.B * self.hdr
+        if self.rank == self.root and not self.self_p2p:        # the root's own share: a local copy
+            buf = self._recv_buffer(i, self.root, lens[self.root])
+            buf[:lens[self.root]].copy_(st["payload"][:lens[self.root]], non_blocking=True)
+        self.bytes_sent += sum(lens) - lens[self.root] + 8 * self.META * self.world
+        self.payload_bytes += sum(lens) - sum(m[1] * m[3] for m in st["meta"])
         self.jobs += 1
 
     def _finish(self, i):
@@ -289,7 +309,8 @@ class BitstreamGatherer:
         if not self.gloo:
             torch.cuda.current_stream().wait_stream(self.side)   # later work sees the received bytes
         if self.rank == self.root:
-            self.last = [(self.recv[i][r], st["lens"][r]) for r in range(self.world)]
+            self.last = [(self.recv[i][r], m[0], m[1], m[2], m[3]) for r, m in enumerate(st["meta"])]
+            self.last_job = st["job"]
         self.state[i] = None
 
     def drain(self):
@@ -300,10 +321,13 @@ class BitstreamGatherer:
         return self.last
 
     def last_unpacked(self):
-        """Root: the last job's streams as (bits [world * B, width], nbits [world * B])."""
+        """Root: the last finished job's streams, rank by rank, as (bits [streams,
+        width], nbits [streams]) with width the widest rank's slot."""
         import torch
-        parts = [unpack_bitstreams(p[:n], self.B, self.width, self.hdr) for p, n in self.last]
-        return torch.cat([p[0] for p in parts]), torch.cat([p[1] for p in parts])
+        parts = [unpack_bitstreams(p[:n], b, w, h) for p, n, b, w, h in self.last]
+        W = max(p[0].shape[1] for p in parts)
+        bits = [torch.nn.functional.pad(p[0], (0, W - p[0].shape[1])) for p in parts]
+        return torch.cat(bits), torch.cat([p[1] for p in parts])
 
 
 class _nullctx:

@@ -58,7 +58,11 @@ def fudged_dist(cdf, minp, denom):
 
 def symbol_to_range(cdf, minp, s, denom):
     """CDFPredictor.symbol_to_range -- arith_code.py:98-110 (ceil mapping)."""
-    dist = fudged_dist(cdf, minp, denom)
+    return _range_on(fudged_dist(cdf, minp, denom), s, denom)
+
+
+def _range_on(dist, s, denom):
+    """symbol_to_range's arithmetic on an already fudged dist (arith_code.py:102-110)."""
     if s >= len(dist) or s < 0:
         raise AssertionError("unknown symbol", s)
     hd = dist[s]
@@ -69,7 +73,10 @@ def symbol_to_range(cdf, minp, s, denom):
 
 def val_to_symbol(cdf, minp, v, denom):
     """CDFPredictor.val_to_symbol -- arith_code.py:94-97 (bisect_right)."""
-    dist = fudged_dist(cdf, minp, denom)
+    return _symbol_on(fudged_dist(cdf, minp, denom), v, denom)
+
+
+def _symbol_on(dist, v, denom):
     return bisect.bisect_right(dist, (v * dist[-1]) // denom)
 
 
@@ -220,19 +227,29 @@ class _Uniform:
 
 
 class _Table:
-    """CDFPredictor over replayed rows: step i uses rows[min(i, len-1)]."""
+    """CDFPredictor over replayed rows: step i uses rows[min(i, len-1)].  The
+    fudged dist of the current (row, width) is kept: fudged_dist depends on
+    nothing else, and the flush ranks every straddled candidate at one width
+    (the reference recomputes it per candidate: O(V^2) per flush step at
+    V = 32000, tools/gen_golden_flush_long.py)."""
 
     def __init__(self, rows):
         self.R = _Rows(rows)
         self.i = 0
+        self._fd = (None, None, None)
+
+    def _dist(self, denom):
+        i = min(self.i, len(self.R.rows) - 1)
+        if self._fd[:2] != (i, denom):
+            cdf, minp = self.R.get(self.i)
+            self._fd = (i, denom, fudged_dist(cdf, minp, denom))
+        return self._fd[2]
 
     def val_to_symbol(self, v, denom):
-        cdf, minp = self.R.get(self.i)
-        return val_to_symbol(cdf, minp, v, denom)
+        return _symbol_on(self._dist(denom), v, denom)
 
     def symbol_to_range(self, s, denom):
-        cdf, minp = self.R.get(self.i)
-        return symbol_to_range(cdf, minp, s, denom)
+        return _range_on(self._dist(denom), s, denom)
 
 
 def decode_run(rows, bits, prec, stop=1, uniform=None):

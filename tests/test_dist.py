@@ -64,16 +64,23 @@ def test_gather_bitstreams_gloo_world2():
 
 
 class _FakeCoder:
-    """CPU stand-in for BatchCoder's output accessors (the gatherer's only dependency)."""
+    """CPU stand-in for BatchCoder's output accessors (the gatherer's only
+    dependency): job j of rank r is a pure function of (r, j), so the parent
+    process can rebuild every rank's streams to check the root's copy."""
 
-    def __init__(self, streams, stride, seed):
-        self.streams, self.stride, self.device = streams, stride, "cpu"
-        self.g = torch.Generator().manual_seed(seed)
-        self.new_job()
+    def __init__(self, streams, stride, rank):
+        self.streams, self.stride, self.device, self.rank = streams, stride, "cpu", rank
+        self.new_job(0)
 
-    def new_job(self):
-        self.nbits = torch.randint(0, self.stride * 8 + 1, (self.streams,), generator=self.g, dtype=torch.int64)
-        self.bits = torch.randint(0, 256, (self.streams, self.stride), generator=self.g, dtype=torch.uint8)
+    @staticmethod
+    def job_data(streams, stride, rank, j):
+        g = torch.Generator().manual_seed(1000 * rank + j)
+        nbits = torch.randint(0, stride * 8 + 1, (streams,), generator=g, dtype=torch.int64)
+        bits = torch.randint(0, 256, (streams, stride), generator=g, dtype=torch.uint8)
+        return bits, nbits
+
+    def new_job(self, j):
+        self.bits, self.nbits = self.job_data(self.streams, self.stride, self.rank, j)
 
     def bits_stride(self):
         return self.stride
@@ -85,56 +92,76 @@ class _FakeCoder:
         out.copy_(self.nbits)
 
 
-def _gatherer_worker(rank, world, port, q, streams, stride, jobs):
+def _gatherer_worker(rank, world, port, q, shards, stride, jobs, depth):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    coder = _FakeCoder(streams, stride, seed=100 + rank)
-    g = BitstreamGatherer(coder, depth=2)
-    out = []
-    for _ in range(jobs):                               # more jobs than slots: slots are reused
-        coder.new_job()
+    coder = _FakeCoder(shards[rank], stride, rank)
+    g = BitstreamGatherer(coder, depth=depth)
+    seen = []
+    for j in range(1, jobs + 1):                         # more jobs than slots: slots are reused
+        coder.new_job(j)
         g.submit()
-        got = g.last_unpacked() if rank == 0 else None
-        out.append((coder.bits.tolist(), coder.nbits.tolist(),
-                    None if got is None else (got[0].tolist(), got[1].tolist())))
+        if rank == 0 and g.last is not None:
+            b, n = g.last_unpacked()
+            seen.append((g.last_job, b.tolist(), n.tolist()))
     g.drain()
-    q.put((rank, out, g.bytes_sent, g.payload_bytes, g.jobs, g.hdr))
+    if rank == 0:
+        b, n = g.last_unpacked()
+        seen.append((g.last_job, b.tolist(), n.tolist()))
+    q.put((rank, seen, g.bytes_sent, g.payload_bytes, g.jobs, g.hdr))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def _run_gatherer(streams, stride, jobs):
+def _run_gatherer(shards, stride, jobs, depth=2):
+    world = len(shards)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_gatherer_worker, args=(r, 2, port, q, streams, stride, jobs)) for r in range(2)]
+    ps = [ctx.Process(target=_gatherer_worker, args=(r, world, port, q, shards, stride, jobs, depth))
+          for r in range(world)]
     for p in ps:
         p.start()
-    res = {r[0]: r[1:] for r in (q.get(timeout=180) for _ in range(2))}
+    res = {r[0]: r[1:] for r in (q.get(timeout=300) for _ in range(world))}
     for p in ps:
-        p.join(timeout=60)
+        p.join(timeout=120)
         assert p.exitcode == 0
     return res
 
 
-def _check_root(res, jobs):
-    for j in range(jobs):
-        b0, n0, got = res[0][0][j]
-        b1, n1, _ = res[1][0][j]
-        bits, nbits = got
-        assert nbits == n0 + n1                          # the root holds every stream's bit count
-        for row, want, n in zip(bits, b0 + b1, n0 + n1):
+def _check_root(res, shards, stride, jobs, depth=2):
+    """The root saw every job exactly when its slot came round (job j after
+    submitting job j + depth) and once more for the last job after drain(); each
+    holds every rank's streams, bytes and bit counts, exactly."""
+    seen = res[0][0]
+    assert [s[0] for s in seen] == list(range(1, jobs - depth + 1)) + [jobs]
+    for j, bits, nbits in seen:
+        want = [_FakeCoder.job_data(shards[r], stride, r, j) for r in range(len(shards))]
+        assert nbits == [int(x) for _, n in want for x in n]
+        rows = [row for b, _ in want for row in b.tolist()]
+        for row, got, n in zip(rows, bits, nbits):
             nb = (n + 7) // 8
-            assert row[:nb] == want[:nb] and not any(row[nb:])   # exactly the stream's bytes
+            assert got[:nb] == row[:nb] and not any(got[nb:])   # exactly the stream's bytes
 
 
 def test_bitstream_gatherer_gloo_world2():
     """Jobs through the payload-sized gather to rank 0: the root holds every
     stream's bytes and bit count, exactly; 2-byte headers (capacity < 2^16 bits)."""
-    res = _run_gatherer(3, 24, 5)
-    _check_root(res, 5)
+    res = _run_gatherer([3, 3], 24, 5)
+    _check_root(res, [3, 3], 24, 5)
     assert res[0][4] == 2
+
+
+@pytest.mark.parametrize("shards,jobs,depth", [([3, 0, 5, 2], 7, 2), ([1, 2, 2, 2, 2, 2, 2, 2], 6, 3),
+                                               ([4096 // 8] * 8, 3, 2)])
+def test_bitstream_gatherer_gloo_world4_world8_uneven(shards, jobs, depth):
+    """World 4 and 8 (the c5 node), uneven shards (one rank with no streams, 15
+    streams over 8 ranks), more jobs than slots at depth 2 and 3: seven senders,
+    the root's receive order, slot reuse -- the deferred path RCCL takes, minus
+    its streams and events."""
+    res = _run_gatherer(shards, 40, jobs, depth)
+    _check_root(res, shards, 40, jobs, depth)
 
 
 def test_bitstream_gatherer_long_job_sized_to_payload():
@@ -142,51 +169,59 @@ def test_bitstream_gatherer_long_job_sized_to_payload():
     links per job stays within 1.2x the encoded bytes, where
     the fixed-width slots of round 2 moved the whole capacity to every rank."""
     stride = (4096 * 50 + 256) // 8
-    res = _run_gatherer(6, stride, 3)
-    _check_root(res, 3)
+    res = _run_gatherer([6, 6], stride, 3)
+    _check_root(res, [6, 6], stride, 3)
     sent = res[0][1]                                    # (every rank counts the whole job)
     payload = res[0][2]
     assert res[0][4] == 4 and payload > 0 and sent <= 1.2 * payload, (sent, payload)
 
 
-def _scatter_worker(rank, world, port, q):
+def _scatter_worker(rank, world, port, q, total):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    # a job of 7 streams (uneven shards 3 + 4) held by rank 0 is scattered ...
+    # a job of `total` streams (uneven shards) held by rank 0 is scattered ...
     g = torch.Generator().manual_seed(7)
-    total, width = 7, 24
+    width = 24
     nbits = torch.randint(0, width * 8 + 1, (total,), generator=g, dtype=torch.int64)
     bits = torch.randint(0, 256, (total, width), generator=g, dtype=torch.uint8)
     mb, mn = scatter_bitstreams(bits if rank == 0 else None, nbits if rank == 0 else None, total_streams=total)
-    # ... and an even job's shards gathered back reproduce it (gather pads to the
-    # widest stream of the job, so compare the bytes every stream owns)
-    eb, en = scatter_bitstreams(bits[:6] if rank == 0 else None, nbits[:6] if rank == 0 else None)
+    # ... and an even job's shards (2 per rank) gathered back reproduce it (gather pads
+    # to the widest stream of the job, so compare the bytes every stream owns)
+    ev = 2 * world
+    g2 = torch.Generator().manual_seed(8)
+    nb2 = torch.randint(0, width * 8 + 1, (ev,), generator=g2, dtype=torch.int64)
+    b2 = torch.randint(0, 256, (ev, width), generator=g2, dtype=torch.uint8)
+    eb, en = scatter_bitstreams(b2 if rank == 0 else None, nb2 if rank == 0 else None)
     ab, an = gather_bitstreams(eb, en)
-    q.put((rank, mb.tolist(), mn.tolist(), bits.tolist(), nbits.tolist(), ab.tolist(), an.tolist()))
+    q.put((rank, mb.tolist(), mn.tolist(), bits.tolist(), nbits.tolist(), ab.tolist(), an.tolist(),
+           b2.tolist(), nb2.tolist()))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_scatter_bitstreams_gloo_world2():
-    """Decode-side exchange: uneven shards of a job held by rank 0, then the
-    gather of those shards round-trips to the source job."""
+@pytest.mark.parametrize("world,total", [(2, 7), (4, 7), (8, 13), (8, 3)])
+def test_scatter_bitstreams_gloo(world, total):
+    """Decode-side exchange: uneven shards of a job held by rank 0 (at world 8 with
+    3 streams, five ranks get none), then the gather of an even job's shards
+    round-trips to the source job."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_scatter_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_scatter_worker, args=(r, world, port, q, total)) for r in range(world)]
     for p in ps:
         p.start()
-    res = dict((r[0], r[1:]) for r in (q.get(timeout=120) for _ in range(2)))
+    res = dict((r[0], r[1:]) for r in (q.get(timeout=300) for _ in range(world)))
     for p in ps:
-        p.join(timeout=60)
+        p.join(timeout=120)
         assert p.exitcode == 0
     bits, nbits = res[0][2], res[0][3]
-    for rank in (0, 1):
-        lo, hi = shard_range(7, rank, 2)
+    b2, nb2 = res[0][6], res[0][7]
+    for rank in range(world):
+        lo, hi = shard_range(total, rank, world)
         mb, mn = res[rank][0], res[rank][1]
         assert mn == nbits[lo:hi] and mb == bits[lo:hi]
         ab, an = res[rank][4], res[rank][5]
-        assert an == nbits[:6]
-        for i, n in enumerate(nbits[:6]):
-            assert ab[i][:(n + 7) // 8] == bits[i][:(n + 7) // 8]
+        assert an == nb2
+        for i, n in enumerate(nb2):
+            assert ab[i][:(n + 7) // 8] == b2[i][:(n + 7) // 8]

@@ -62,17 +62,23 @@ def test_cdfpredictor_against_golden(kind):
             return Replay(self.rows)
 
     cases = [c for c in load_golden("small_cases.json")[kind] if c["syms"]][:40]
-    for c in cases:
-        ac = AC(Replay(c["rows"]), c["prec"])
-        R, L = ac.to_bin.encode(c["syms"])
-        assert L == c["L"]
-        data = measure_compress(ac.to_bin, iter(c["syms"]), print_every_inp=0)
-        assert data.hex() == c["bytes"]
-        bits = list(ac.to_bin.bits(c["syms"]))
-        assert bytes(group_bits(iter(bits))).hex() == c["bytes"]
-        assert list(ac.from_bin.run(bits, stop=0, n=len(c["syms"]))) == c["syms"]
-        # without n: exactly what the reference's bit-serial run(bits, stop=0) emits
-        assert list(ac.from_bin.run(bits, stop=0)) == c["syms"] + c["decoded_extra"]
+    makers = [lambda c: Replay(c["rows"])]
+    if kind == "static":            # a plain CDFPredictor: the static-model (stride-0) paths
+        makers.append(lambda c: CDFPredictor(np.cumsum(np.asarray(c["rows"][0], dtype=object)).tolist()))
+    for mk in makers:
+        for c in cases:
+            ac = AC(mk(c), c["prec"])
+            R, L = ac.to_bin.encode(c["syms"])
+            assert L == c["L"] and R == int(c["bytes"] or "0", 16) >> ((-L) % 8)
+            data = measure_compress(ac.to_bin, iter(c["syms"]), print_every_inp=1 << 30, print_every_out=1 << 30)
+            assert data.hex() == c["bytes"]
+            bits = list(ac.to_bin.bits(c["syms"]))
+            assert bytes(group_bits(iter(bits))).hex() == c["bytes"]
+            digits = list(ac.to_bin.run(c["syms"]))
+            assert digits == [d for st in c["trace"] for d in st] + c["flush"]
+            assert list(ac.from_bin.run(bits, stop=0, n=len(c["syms"]))) == c["syms"]
+            # without n: exactly what the reference's bit-serial run(bits, stop=0) emits
+            assert list(ac.from_bin.run(bits, stop=0)) == c["syms"] + c["decoded_extra"]
 
 
 def test_bit_serial_step_matches_reference():

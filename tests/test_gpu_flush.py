@@ -74,6 +74,25 @@ def test_run_stop1_matches_reference(variant):
         assert got == (c["out"], c["exc"]), (c["src"], variant, got, c["out"], c["exc"])
 
 
+def test_static_cdfpredictor_matches_reference():
+    """The one-table golden cases decoded with a plain CDFPredictor -- a static
+    model: chunked stride-0 decode (coder.A_from_bin._fast_static), then the
+    tail -- yield the reference's symbols and exceptions on whole, prefix and
+    flipped-bit streams, through run(bits) and decode(R, L)."""
+    from lac_amd.coder import AC, CDFPredictor
+    cases = [c for c in flush_util.cases() if c["src"].startswith("small/static/")]
+    assert len(cases) > 100
+    for c in cases:
+        row = flush_util.rows_for(c, SMALL, GEN)[0]
+        mk = lambda: CDFPredictor(np.cumsum(np.asarray(row, dtype=object)).tolist())  # noqa: E731
+        bits = flush_util.bits_for(c)
+        assert flush_util.drain(AC(mk(), c["prec"]).from_bin.run(bits)) == (c["out"], c["exc"]), c["src"]
+        if "decode_out" in c:
+            R = int("".join(map(str, bits)) or "0", 2)
+            got = flush_util.drain(AC(mk(), c["prec"]).from_bin.decode(R, len(bits)))
+            assert got == (c["decode_out"], c["decode_exc"]), c["src"]
+
+
 def test_decode_R_L_matches_reference():
     """decode(R, L) (arith_code.py:327-334): run with stop, then a second flush."""
     from lac_amd.coder import AC

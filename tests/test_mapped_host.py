@@ -84,9 +84,60 @@ def test_table_predictor_with_stale_minp_is_refused():
             self.dist = [5, 8, 40]               # minp stays the first table's
 
     p = Swap([2, 9, 10])
-    assert list(_Tables(p).row()) == [2, 7, 1]
+    assert list(_Tables(p, 6).row()) == [2, 7, 1]
     p.accept(0)
+    # minp 1 against the table's 3: T = 40 fudges for w < 40 with minp 1 and for
+    # w < 14 with 3 -- at prec 6 (w in 33..64) the decisions differ at w = 33..39
     with pytest.raises(ValueError):
-        _Tables(p).row()
+        _Tables(p, 6).row()
+    with pytest.raises(ValueError):
+        _Tables(p).row()                         # no precision given: equality required
+    # at prec 16 (w > 2^15) neither fudges: the same code either way, accepted
+    assert list(_Tables(p, 16).row()) == [5, 3, 32]
     p.minp = 3
-    assert list(_Tables(p).row()) == [5, 3, 32]
+    assert list(_Tables(p, 6).row()) == [5, 3, 32]
+
+
+def test_fudge_decisions_agree_matches_brute_force():
+    """fudge_decisions_agree == 'T > w*minp' and 'T > w*min_pos' agree for every w
+    in (2^(prec-1), 2^prec] (arith_code.py:84), minp 0 included (Llama_AC on rows
+    with zero CDF steps, llama_compress.py:43-45)."""
+    import random
+    from lac_amd.coder import fudge_decisions_agree
+    rng = random.Random(5)
+    for _ in range(3000):
+        prec = rng.randint(2, 9)
+        T = rng.randint(1, 1 << rng.randint(1, 14))
+        m1, m2 = rng.randint(0, 300), rng.randint(1, 300)
+        ws = range((1 << (prec - 1)) + 1, (1 << prec) + 1)
+        want = all((T > w * m1) == (T > w * m2) for w in ws)
+        assert fudge_decisions_agree(T, m1, m2, prec) == want, (T, m1, m2, prec)
+
+
+def test_llama_minp_zero_rows_accepted_when_both_fudge():
+    """a Llama_AC row whose float cumsum has zero steps has
+    minp 0 -- the reference always fudges.  The kernels fudge when T > 2^prec *
+    min_pos; with T ~ 2^60 at prec 48 both always fudge, so the row is coded
+    (it was refused); a table where the kernels would not fudge is still refused."""
+    from lac_amd.coder import ProbPredictor, _Tables
+
+    class ZeroStep(ProbPredictor):
+        def __init__(self, cdf):
+            super().__init__(len(cdf))
+            self.cdf = cdf
+
+        def calc_dist(self):
+            self.dcache = self.cdf
+            return self.dcache
+
+        @property
+        def minp(self):                           # Llama_AC's: zeros included
+            return int(min(self.dist[0], np.min(np.diff(self.dist))))
+
+    cdf = np.cumsum(np.array([2, 0, 5, 1 << 59, 0, 3], dtype=np.int64))
+    p = ZeroStep(cdf)
+    assert p.minp == 0
+    assert list(_Tables(p, 48).row()) == [2, 0, 5, 1 << 59, 0, 3]
+    small = ZeroStep(np.cumsum(np.array([4, 0, 4], dtype=np.int64)))
+    with pytest.raises(ValueError):
+        _Tables(small, 48).row()

@@ -178,6 +178,17 @@ def test_restated_flush_matches_reference():
     assert n > 2000
 
 
+def test_flush_fixtures_complete():
+    """Every recorded reference flush finished (tools/gen_golden_flush_long.py re-ran
+    the V=32000 streams the 60 s limit had cut off, with no limit), and the
+    headline vocab has fudged whole streams among them."""
+    cases = load_golden("flush_cases.json")["cases"]
+    assert not [c["src"] for c in cases if c["exc"] == "timeout"]
+    fudged32k = {c["src"] for c in cases if c["variant"] == "whole" and c["src"] in (
+        "gen/lu32000_p24", "gen/llama64_32000_p48", "gen/llama64_32000_p40", "gen/lu32000_p20")}
+    assert len(fudged32k) == 4
+
+
 def test_c_bitserial_decoder_counts_match_reference():
     """oracle.decode_bitserial (A_from_bin.run(bits, stop=0) in C) == the reference's
     decoded symbols, extra determined symbols included, on every small and
