@@ -404,8 +404,11 @@ class BatchCoder:
         return out
 
     def set_q1_shape(self, shape: int):
-        """Logits row-stats block shape (0 auto, 1..21 forced, include/lac.h
-        LAC_OPT_Q1_SHAPE; identical results)."""
+        """Logits row-stats block shape (include/lac.h LAC_OPT_Q1_SHAPE; identical
+        results, only speed differs): 0 auto, 1..18 forced single-block forms,
+        19 / 20 / 21 row groups -- a row of > 16384 vectors in 2..16 segments, one
+        per row slot of 1 / 2 / 4 rows per 16-wave block --, 22 one row of <= 20480
+        vectors whole in the registers of one 8-wave block, 23 groups of such blocks."""
         check(self.lib.lac_set_option(self.ctx, _lib.LAC_OPT_Q1_SHAPE, int(shape)))
 
     def q1_k(self):

@@ -36,6 +36,7 @@
 #include "lac.h"
 #include "lac_core.h"
 #include "lac_q1_table.h"
+#include "lac_hc.h"
 
 using namespace lac;
 
@@ -4633,81 +4634,25 @@ int lac_decode_tail_set_state(lac_ctx *c, const lac_tail_state *host_in, void *s
 }
 
 // ---- host-side register arithmetic for predictors with their own mapping --------
-// (include/lac.h "predictor-mapped coding"; no device work)
-static int hc_regs_ok(int64_t a, int64_t b) {
-    const int64_t lim = (int64_t)1 << 62;
-    return a > -lim && a < lim && b > -lim && b < lim;
-}
-
+// (include/lac.h "predictor-mapped coding"; no device work): lac_hc.h, shared with
+// the host sanitizer build (tests/native)
 int lac_hc_encode_symbol(int prec, int64_t *l, int64_t *h, int64_t lo, int64_t hi, int8_t *digits,
                          int32_t *ndigits) {
-    if (!l || !h || !digits || !ndigits) return fail(LAC_E_ARG, "NULL argument");
-    if (prec < 2 || prec > 61) return fail(LAC_E_PREC, "prec %d outside [2, 61]", prec);
-    *ndigits = 0;
-    if (hi <= lo) return fail(LAC_E_ZERO_WIDTH, "empty range [%lld, %lld): the reference loops forever",
-                              (long long)lo, (long long)hi);
-    const int64_t D = (int64_t)1 << prec, H = D >> 1;
-    const i128 nl = (i128)*l + lo, nh = (i128)*l + hi - 1;
-    if (!hc_regs_ok((int64_t)nl, (int64_t)nh) || nl != (i128)(int64_t)nl || nh != (i128)(int64_t)nh)
-        return fail(LAC_E_ARG, "range moves the registers beyond +-2^62");
-    int64_t L = (int64_t)nl, Hh = (int64_t)nh;
-    int n = 0;
-    while (Hh - L < H) {                                   // decide_bit / emit_bit, arith_code.py:176-186
-        const int64_t d = floordiv_pos(L, H);
-        if (n >= 64 || d < -128 || d > 127) return fail(LAC_E_ARG, "renormalisation out of range");
-        digits[n++] = (int8_t)d;
-        L = L * 2 - d * D;
-        Hh = Hh * 2 + 1 - d * D;
-        if (!hc_regs_ok(L, Hh)) return fail(LAC_E_ARG, "registers beyond +-2^62");
-    }
-    *l = L;
-    *h = Hh;
-    *ndigits = n;
-    return LAC_OK;
+    const char *msg = "";
+    const int rc = lac::hc::encode_symbol(prec, l, h, lo, hi, digits, ndigits, &msg);
+    return rc ? fail(rc, "%s", msg) : LAC_OK;
 }
 
 int lac_hc_encode_flush(int prec, int64_t l, int64_t h, int8_t *digits, int32_t *ndigits) {
-    if (!digits || !ndigits) return fail(LAC_E_ARG, "NULL argument");
-    if (prec < 2 || prec > 61) return fail(LAC_E_PREC, "prec %d outside [2, 61]", prec);
-    const int64_t D = (int64_t)1 << prec, Hd = D >> 1;
-    int n = 0;
-    while (l > 0 || h + 1 < D) {                           // A_to_bin.flush, arith_code.py:193-202
-        int64_t d = floordiv_pos(l, Hd);
-        if (overlap(l, h, d * Hd, (d + 1) * Hd) < overlap(l, h, (d + 1) * Hd, (d + 2) * Hd)) d += 1;
-        if (n >= 64 || d < -128 || d > 127) return fail(LAC_E_ARG, "flush out of range");
-        digits[n++] = (int8_t)d;
-        l = l * 2 - d * D;
-        h = h * 2 + 1 - d * D;
-        if (!hc_regs_ok(l, h)) return fail(LAC_E_ARG, "registers beyond +-2^62");
-    }
-    *ndigits = n;
-    return LAC_OK;
+    const char *msg = "";
+    const int rc = lac::hc::encode_flush(prec, l, h, digits, ndigits, &msg);
+    return rc ? fail(rc, "%s", msg) : LAC_OK;
 }
 
 int lac_hc_decode_emit(int prec, int64_t *regs, int64_t lo, int64_t hi, int renormalise) {
-    if (!regs) return fail(LAC_E_ARG, "NULL argument");
-    if (prec < 2 || prec > 61) return fail(LAC_E_PREC, "prec %d outside [2, 61]", prec);
-    int64_t l = regs[0], h = regs[1], lb = regs[2], hb = regs[3];
-    const i128 nl = (i128)l + lo, nh = (i128)l + hi - 1;
-    // emit_symbol, arith_code.py:274-283: the range must meet the received window
-    const i128 ov = (nh < (i128)hb ? nh : (i128)hb) - (nl > (i128)lb ? nl : (i128)lb) + 1;
-    if (ov <= 0) return fail(LAC_E_DECODE_RANGE, "predictor range does not correspond to val");
-    if (nl != (i128)(int64_t)nl || nh != (i128)(int64_t)nh || !hc_regs_ok((int64_t)nl, (int64_t)nh))
-        return fail(LAC_E_ARG, "range moves the registers beyond +-2^62");
-    l = (int64_t)nl;
-    h = (int64_t)nh;
-    const int64_t D = (int64_t)1 << prec, H = D >> 1;
-    int n = 0;
-    while (renormalise && h - l < H) {                     // emit_bit, :284-291
-        const int64_t d = floordiv_pos(l, H);
-        l = l * 2 - d * D;
-        h = h * 2 + 1 - d * D;
-        lb = lb * 2 - d * D;
-        hb = hb * 2 + 1 - d * D;
-        if (++n > 128 || !hc_regs_ok(l, h) || !hc_regs_ok(lb, hb)) return fail(LAC_E_ARG, "registers out of range");
-    }
-    regs[0] = l; regs[1] = h; regs[2] = lb; regs[3] = hb;
-    return LAC_OK;
+    const char *msg = "";
+    const int rc = lac::hc::decode_emit(prec, regs, lo, hi, renormalise, &msg);
+    return rc ? fail(rc, "%s", msg) : LAC_OK;
 }
 
 int lac_q1_group_aborted(lac_ctx *c, int64_t *aborted, void *stream) {

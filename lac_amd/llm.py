@@ -86,8 +86,10 @@ class TorchLLM:
     A module with ``init_cache(B, T)`` / ``step(tokens[B], cache, t)`` (as
     TinyCausalLM) is run incrementally: each evaluated token is one step against
     a key/value cache, so a sequence costs O(T) steps as with llama.cpp's own KV
-    cache.  Past ``n_ctx`` tokens the window slides and is re-evaluated from an
-    empty cache (Llama_AC resets before that happens).  Any other module
+    cache.  Past ``n_ctx`` tokens the window slides with every token, so each
+    eval is one forward over the window and the history is trimmed to it
+    (Llama_AC resets before that happens).  ``eval([])`` keeps the last logits.
+    Any other module
     (``module(tokens[1, t]) -> logits[1, t, V]``) re-runs the window on every
     ``eval``.  Either way the encode and decode sides issue the same sequence of
     calls, which is what makes the logits -- and the tables and bitstream --
@@ -113,19 +115,28 @@ class TorchLLM:
     def eval(self, tokens):
         import torch
         new = [int(t) for t in tokens]
+        if not new:
+            if self._scores is None:
+                raise ValueError("eval([]) before any token: there are no logits yet")
+            return                                          # nothing new: the last logits stand
         self.tokens.extend(new)
         with torch.no_grad():
-            if self.incremental:
-                if self._cache is None or len(self.tokens) > self._n_ctx:
+            if self.incremental and len(self.tokens) <= self._n_ctx:
+                if self._cache is None:                     # fresh (or after a slide): replay the window
                     self._cache = self.module.init_cache(1, self._n_ctx)
                     self._pos = 0
-                    new = self.tokens[-self._n_ctx:]
+                    new = self.tokens
                 for t in new:
                     x = torch.tensor([t], dtype=torch.long, device=self.device)
                     logits = self.module.step(x, self._cache, self._pos)[0].float()
                     self._pos += 1
             else:
+                # past n_ctx the window slides every token, so its positions shift and a
+                # cache cannot be reused: one forward over the window, the history
+                # trimmed to it (tokens before it can no longer matter)
                 window = self.tokens[-self._n_ctx:]
+                self.tokens = list(window)
+                self._cache = None
                 x = torch.tensor([window], dtype=torch.long, device=self.device)
                 logits = self.module(x)[0, -1].float()
         self._scores = logits.cpu().numpy()[None, :]

@@ -21,6 +21,18 @@ import numpy as np
 from . import _lib
 
 _I8x64 = C.c_int8 * 64
+_I64_MIN, _I64_MAX = -(1 << 63), (1 << 63) - 1
+
+
+def _range(lo, hi):
+    """A predictor's (lo, hi) as int64 arguments: ctypes would wrap anything wider
+    silently ((1 << 64) + 5 arrives as 5), so a bound beyond int64 is refused."""
+    lo, hi = int(lo), int(hi)
+    for v in (lo, hi):
+        if not _I64_MIN <= v <= _I64_MAX:
+            raise _lib.LacError(_lib.LAC_E_ARG, f"symbol range bound {v} does not fit int64 (the host "
+                                                "register functions keep registers within +-2^62)")
+    return lo, hi
 
 
 def _check(rc):
@@ -63,14 +75,13 @@ class MappedEncoderMixin:
     def step(self, symbol):
         if self.debug_log:
             self.debug_log.append((self._l, self._h, "recv", symbol))
-        lo, hi = self.predictor.symbol_to_range(symbol, self._h - self._l + 1)
+        lo, hi = _range(*self.predictor.symbol_to_range(symbol, self._h - self._l + 1))
         l, h = C.c_int64(self._l), C.c_int64(self._h)
         dig, n = _I8x64(), C.c_int32()
-        _check(self._lib.lac_hc_encode_symbol(self.precision, C.byref(l), C.byref(h), int(lo), int(hi), dig,
-                                              C.byref(n)))
+        _check(self._lib.lac_hc_encode_symbol(self.precision, C.byref(l), C.byref(h), lo, hi, dig, C.byref(n)))
         digits = list(dig[:n.value])
         if self.debug_log:
-            self._l, self._h = self._l + int(lo), self._l + int(hi) - 1
+            self._l, self._h = self._l + lo, self._l + hi - 1
             self._log_emits(digits)
         self._l, self._h = l.value, h.value
         self.predictor.accept(symbol)
@@ -114,8 +125,8 @@ class MappedDecoderMixin:
 
     def _emit(self, s, renormalise):
         l, h = int(self._r[0]), int(self._r[1])
-        lo, hi = self.predictor.symbol_to_range(s, h - l + 1)
-        _check(self._lib.lac_hc_decode_emit(self.precision, self._r.ctypes.data_as(C.c_void_p), int(lo), int(hi),
+        lo, hi = _range(*self.predictor.symbol_to_range(s, h - l + 1))
+        _check(self._lib.lac_hc_decode_emit(self.precision, self._r.ctypes.data_as(C.c_void_p), lo, hi,
                                             int(renormalise)))
         self.predictor.accept(s)
         return s

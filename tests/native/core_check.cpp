@@ -12,10 +12,25 @@
 #include <vector>
 
 #include "lac_core.h"
+#include "lac_hc.h"
 
 using namespace lac;
 
 extern "C" {
+
+// the predictor-mapped host register functions (lac_hc.h, liblac's lac_hc_*)
+int cc_hc_encode_symbol(int prec, int64_t *l, int64_t *h, int64_t lo, int64_t hi, int8_t *digits, int32_t *n) {
+    const char *m = "";
+    return hc::encode_symbol(prec, l, h, lo, hi, digits, n, &m);
+}
+int cc_hc_encode_flush(int prec, int64_t l, int64_t h, int8_t *digits, int32_t *n) {
+    const char *m = "";
+    return hc::encode_flush(prec, l, h, digits, n, &m);
+}
+int cc_hc_decode_emit(int prec, int64_t *regs, int64_t lo, int64_t hi, int renormalise) {
+    const char *m = "";
+    return hc::decode_emit(prec, regs, lo, hi, renormalise, &m);
+}
 
 uint64_t cc_div_floor(uint64_t nh, uint64_t nl, uint64_t d) { return div_floor(((u128)nh << 64) | nl, d); }
 uint64_t cc_div_floor_inv(uint64_t nh, uint64_t nl, uint64_t d) {

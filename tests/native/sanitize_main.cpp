@@ -29,6 +29,67 @@ int lacref_decode(const void *pmf, int elem_bytes, int64_t V, int64_t nsym, int6
                   const uint8_t *bytes, uint64_t nbits, int prec, int32_t *syms_out);
 int64_t lacref_decode_bitserial(const void *pmf, int elem_bytes, int64_t V, int64_t nrows, int64_t step_stride,
                                 const uint8_t *bytes, uint64_t nbits, int prec, int32_t *syms_out, int64_t max_out);
+int cc_hc_encode_symbol(int prec, int64_t *l, int64_t *h, int64_t lo, int64_t hi, int8_t *digits, int32_t *n);
+int cc_hc_encode_flush(int prec, int64_t l, int64_t h, int8_t *digits, int32_t *n);
+int cc_hc_decode_emit(int prec, int64_t *regs, int64_t lo, int64_t hi, int renormalise);
+}
+
+// ---- the reference's register arithmetic (arith_code.py:169-202, 274-291) in 128
+// bits, with lac_hc.h's refusal rule (registers must stay within +-2^62), as the
+// model the host functions are checked against
+typedef __int128 i128;
+static const i128 LIM = (i128)1 << 62;
+static bool in_lim(i128 a, i128 b) { return a > -LIM && a < LIM && b > -LIM && b < LIM; }
+static i128 fdiv(i128 a, i128 b) { i128 q = a / b; return (a % b != 0 && a < 0) ? q - 1 : q; }
+static i128 ovl(i128 a, i128 b, i128 c, i128 d) { i128 r = (d < b ? d : b) - (a > c ? a : c) + 1; return r > 0 ? r : 0; }
+
+static int m_encode_symbol(int prec, i128 &l, i128 &h, i128 lo, i128 hi, std::vector<int> &dig) {
+    if (hi <= lo) return -4;
+    if (!in_lim(l, h)) return -1;
+    i128 L = l + lo, H = l + hi - 1;
+    if (!in_lim(L, H)) return -1;
+    const i128 D = (i128)1 << prec, Hd = D >> 1;
+    while (H - L < Hd) {
+        const i128 d = fdiv(L, Hd);
+        if (dig.size() >= 64 || d < -128 || d > 127) return -1;
+        dig.push_back((int)d);
+        L = 2 * L - d * D;
+        H = 2 * H + 1 - d * D;
+        if (!in_lim(L, H)) return -1;
+    }
+    l = L, h = H;
+    return 0;
+}
+
+static int m_encode_flush(int prec, i128 l, i128 h, std::vector<int> &dig) {
+    if (!in_lim(l, h)) return -1;
+    const i128 D = (i128)1 << prec, Hd = D >> 1;
+    while (l > 0 || h + 1 < D) {
+        i128 d = fdiv(l, Hd);
+        if (ovl(l, h, d * Hd, (d + 1) * Hd) < ovl(l, h, (d + 1) * Hd, (d + 2) * Hd)) d += 1;
+        if (dig.size() >= 64 || d < -128 || d > 127) return -1;
+        dig.push_back((int)d);
+        l = 2 * l - d * D;
+        h = 2 * h + 1 - d * D;
+        if (!in_lim(l, h)) return -1;
+    }
+    return 0;
+}
+
+static int m_decode_emit(int prec, i128 *r, i128 lo, i128 hi, int renorm) {
+    if (!in_lim(r[0], r[1]) || !in_lim(r[2], r[3])) return -1;
+    i128 l = r[0] + lo, h = r[0] + hi - 1, lb = r[2], hb = r[3];
+    if (ovl(l, h, lb, hb) == 0) return -6;
+    if (!in_lim(l, h)) return -1;
+    const i128 D = (i128)1 << prec, Hd = D >> 1;
+    int n = 0;
+    while (renorm && h - l < Hd) {
+        const i128 d = fdiv(l, Hd);
+        l = 2 * l - d * D, h = 2 * h + 1 - d * D, lb = 2 * lb - d * D, hb = 2 * hb + 1 - d * D;
+        if (++n > 128 || !in_lim(l, h) || !in_lim(lb, hb)) return -1;
+    }
+    r[0] = l, r[1] = h, r[2] = lb, r[3] = hb;
+    return 0;
 }
 
 static uint64_t s = 0x9E3779B97F4A7C15ull;
@@ -66,6 +127,56 @@ int main() {
         CHECK(cc_frac_mul_div(c, w, T, 0) == fl && cc_frac_mul_div(c, w, T, 1) == ce, "frac_mul_div");
     }
     fprintf(stderr, "frac ok\n");
+    // predictor-mapped host register functions (lac_hc.h) at every prec up to 61,
+    // registers up to +-2^62, ranges anywhere in int64: equal to the 128-bit model,
+    // and (this build) free of signed overflow
+    for (int i = 0; i < 300000; i++) {
+        const int prec = 2 + (int)below(60);
+        const int64_t D = (int64_t)1 << prec;
+        auto reg = [&]() -> int64_t {
+            switch (below(4)) {
+            case 0: return (int64_t)below((uint64_t)2 * D);                     // a coder's own range
+            case 1: return ((int64_t)1 << 62) - 1 - (int64_t)below(1 << 20);    // at the limit
+            case 2: return -((int64_t)1 << 62) + 1 + (int64_t)below(1 << 20);
+            default: return (int64_t)rnd();                                    // anything
+            }
+        };
+        int64_t l = reg(), h = reg();
+        if (below(3) && l < ((int64_t)1 << 62) - D) h = l + (int64_t)below((uint64_t)D);
+        const i128 w128 = (i128)h - l + 1;
+        const uint64_t w = w128 > 0 && w128 < ((i128)1 << 62) ? (uint64_t)w128 : 1;
+        int64_t lo = below(4) ? (int64_t)below(w) : (int64_t)rnd();
+        int64_t hi = below(4) && lo < ((int64_t)1 << 62) ? lo + 1 + (int64_t)below(w) : (int64_t)rnd();
+        if (below(8) == 0) hi = lo;
+        int64_t L = l, H = h;
+        int8_t dg[64];
+        int32_t nd = 0;
+        const int rc = cc_hc_encode_symbol(prec, &L, &H, lo, hi, dg, &nd);
+        i128 ml = l, mh = h;
+        std::vector<int> md;
+        const int mrc = m_encode_symbol(prec, ml, mh, lo, hi, md);
+        CHECK(rc == mrc, "hc_encode_symbol rc %d vs %d (prec %d)", rc, mrc, prec);
+        if (rc == 0 && mrc == 0) {
+            CHECK(L == (int64_t)ml && H == (int64_t)mh && nd == (int)md.size(), "hc_encode_symbol registers");
+            for (int k = 0; k < nd && k < (int)md.size(); k++) CHECK(dg[k] == md[k], "hc_encode_symbol digit");
+        }
+        nd = 0;
+        const int rf = cc_hc_encode_flush(prec, l, h, dg, &nd);
+        md.clear();
+        const int mrf = m_encode_flush(prec, l, h, md);
+        CHECK(rf == mrf && (rf || nd == (int)md.size()), "hc_encode_flush rc %d vs %d (prec %d)", rf, mrf, prec);
+        for (int k = 0; rf == 0 && k < nd && k < (int)md.size(); k++) CHECK(dg[k] == md[k], "hc_encode_flush digit");
+        int64_t r4[4] = {l, h, reg(), 0};
+        r4[3] = below(2) && r4[2] < ((int64_t)1 << 62) - D ? r4[2] + (int64_t)below((uint64_t)D) : reg();
+        i128 m4[4] = {r4[0], r4[1], r4[2], r4[3]};
+        const int ren = (int)below(2);
+        const int re = cc_hc_decode_emit(prec, r4, lo, hi, ren);
+        const int mre = m_decode_emit(prec, m4, lo, hi, ren);
+        CHECK(re == mre, "hc_decode_emit rc %d vs %d (prec %d)", re, mre, prec);
+        if (re == 0 && mre == 0)
+            for (int k = 0; k < 4; k++) CHECK(r4[k] == (int64_t)m4[k], "hc_decode_emit registers");
+    }
+    fprintf(stderr, "hc ok\n");
     // Python-rounded ratios: the double nearest a/b (checked by exact integer bounds)
     for (int i = 0; i < 200000; i++) {
         const uint64_t b = 1 + (rnd() >> (1 + below(63)));

@@ -20,10 +20,11 @@ SRC = os.path.join(REPO, "tests", "native", "core_check.cpp")
 
 @pytest.fixture(scope="module")
 def core():
-    if not os.path.exists(SO) or os.path.getmtime(SO) < max(os.path.getmtime(SRC), os.path.getmtime(
-            os.path.join(REPO, "lac_amd", "csrc", "lac_core.h"))):
+    deps = [SRC] + [os.path.join(REPO, "lac_amd", "csrc", h) for h in ("lac_core.h", "lac_hc.h")] + [
+        os.path.join(REPO, "include", "lac.h")]
+    if not os.path.exists(SO) or os.path.getmtime(SO) < max(os.path.getmtime(d) for d in deps):
         subprocess.run(["hipcc", "-O2", "-std=c++17", "-fPIC", "-shared", "-I", os.path.join(REPO, "lac_amd", "csrc"),
-                        SRC, "-o", SO], check=True)
+                        "-I", os.path.join(REPO, "include"), SRC, "-o", SO], check=True)
     lib = C.CDLL(SO)
     lib.cc_div_floor.restype = C.c_uint64
     lib.cc_div_floor.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64]

@@ -77,8 +77,16 @@ def test_tiny_lm_cached_steps_match_forward():
         inc.eval([t])
         win.eval([t])
         assert np.allclose(inc._scores, win._scores, atol=1e-4), t
+    assert len(inc.tokens) == 12                                # trimmed to the window past n_ctx
+    before = inc._scores.copy()
+    inc.eval([])                                               # nothing new: the last logits stand
+    assert np.array_equal(inc._scores, before)
     inc.reset()
+    with pytest.raises(ValueError):
+        inc.eval([])
     inc.eval([1, 2, 3])
     win.reset()
     win.eval([1, 2, 3])
+    assert np.allclose(inc._scores, win._scores, atol=1e-4)
+    inc.eval([])
     assert np.allclose(inc._scores, win._scores, atol=1e-4)

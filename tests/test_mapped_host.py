@@ -141,3 +141,22 @@ def test_llama_minp_zero_rows_accepted_when_both_fudge():
     small = ZeroStep(np.cumsum(np.array([4, 0, 4], dtype=np.int64)))
     with pytest.raises(ValueError):
         _Tables(small, 48).row()
+
+
+def test_mapped_range_beyond_int64_is_refused():
+    """ADVICE/VERDICT r3: a predictor whose symbol_to_range returns a bound beyond
+    int64 is refused (LacError), not wrapped by ctypes ((1 << 64) + 5 -> 5)."""
+    from lac_amd._lib import LacError
+    from lac_amd.coder import AC, Predictor
+
+    class Wide(Predictor):
+        def symbol_to_range(self, s, denom):
+            return (1 << 64) + 5, (1 << 64) + 9
+
+        def val_to_symbol(self, v, denom):
+            return 0
+
+    with pytest.raises(LacError):
+        list(AC(Wide(2), 16).to_bin.run([0]))
+    with pytest.raises(LacError):
+        list(AC(Wide(2), 16).from_bin.run([1, 0, 1]))
