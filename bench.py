@@ -89,7 +89,7 @@ def main():
                     help="pmf = max(1 or 2, floor(softmax * 2^k)); 0 = 31 for u32, 60 (llama-scale) for u64")
     ap.add_argument("--cpu-baseline", default="on", choices=("on", "off"))
     ap.add_argument("--cpu-threads", type=int, default=0, help="cpu_baseline threads (0 = nproc: host_cores())")
-    ap.add_argument("--decode-reps", type=int, default=3, help="timed decode passes after a warm one (median)")
+    ap.add_argument("--decode-reps", type=int, default=3, help="timed decode passes, back to back, after a warm one")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="minimum CPU-baseline sample time")
     ap.add_argument("--cpu-streams", type=int, default=0, help="oracle sample streams (0 = all)")
     ap.add_argument("--path", default="auto", choices=("auto", "split", "fused"), help="encode kernel path")
@@ -228,29 +228,33 @@ def main():
     dec = decode(pmf)                                      # warm (the clocks ramp after a workload switch)
     torch.cuda.synchronize()
     round_trip = bool(torch.equal(dec, sym)) and rc == 0
-    passes = []                                            # (wall s, {kernel id: ms}) per timed pass
-    for _ in range(max(1, args.decode_reps)):
-        coder.lib.lac_profile_read(coder.ctx, None, None, 1)
-        coder.lib.lac_profile_enable(coder.ctx, 1)
-        d0 = time.perf_counter()
+    # the timed passes back to back with one synchronisation, as the encode jobs run (a
+    # pass timed alone after a host sync paid the clocks' ramp after the idle gap: bf16
+    # Qwen2 decode row stats 209 us per step alone, 182 us back to back, tools/q1_b2b.py)
+    reps = max(1, args.decode_reps)
+    coder.lib.lac_profile_read(coder.ctx, None, None, 1)
+    coder.lib.lac_profile_enable(coder.ctx, 1)
+    outs = []
+    d0 = time.perf_counter()
+    for _ in range(reps):
         coder.decode_open()
-        dec = decode(pmf)
-        torch.cuda.synchronize()
-        d1 = time.perf_counter()
-        coder.lib.lac_profile_enable(coder.ctx, 0)
-        dms = (C.c_double * 8)()
-        dcnt = (C.c_int64 * 8)()
-        coder.lib.lac_profile_read(coder.ctx, C.cast(dms, C.c_void_p), C.cast(dcnt, C.c_void_p), 1)
-        passes.append((d1 - d0, {k: dms[k] for k in (3, 5, 6, 7) if dcnt[k]}))
+        outs.append(decode(pmf))
+    torch.cuda.synchronize()
+    d1 = time.perf_counter()
+    coder.lib.lac_profile_enable(coder.ctx, 0)
+    dms = (C.c_double * 8)()
+    dcnt = (C.c_int64 * 8)()
+    coder.lib.lac_profile_read(coder.ctx, C.cast(dms, C.c_void_p), C.cast(dcnt, C.c_void_p), 1)
+    for dec in outs:
         round_trip = round_trip and bool(torch.equal(dec, sym))
-    mid = sorted(passes, key=lambda p: p[0])[len(passes) // 2]          # the median pass
+    del outs
+    mid = ((d1 - d0) / reps, {k: dms[k] / reps for k in (3, 5, 6, 7) if dcnt[k]})
     dkids = sorted(mid[1])                                     # decode_step|stats path, decode_wave, q1 pair
     dstep_ms = sum(mid[1].values()) / max(T, 1)
     names = {3: "k_decode_step or k_dec_stats+k_decode_seq", 5: "k_decode_wave(_fine) or k_decode_block", 6: "k_q1_stats",
              7: "k_q1_decode"}
     decode_info = {"symbols_per_s": B * T / mid[0], "kernel": "+".join(names[k] for k in dkids),
-                   "passes": f"median of {len(passes)} timed passes after a warm one",
-                   "symbols_per_s_each": [B * T / p[0] for p in passes],
+                   "passes": f"{reps} passes back to back after a warm one (mean)",
                    "kernel_ms_per_step": dstep_ms,
                    "kernel_ms_per_step_each": {names[k]: mid[1][k] / max(T, 1) for k in dkids},
                    "achieved_GBps": B * (V * ebytes + 4) / (dstep_ms * 1e-3) / 1e9 if dkids else None}

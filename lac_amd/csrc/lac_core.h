@@ -22,6 +22,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
 
 namespace lac {
 
@@ -143,6 +144,47 @@ __host__ __device__ inline uint64_t div_floor_inv_n(u128 N, uint64_t d, double i
 }
 __host__ __device__ inline uint64_t div_floor_inv(u128 N, uint64_t d, double inv) {
     return div_floor_inv_n(N, d, inv, nullptr);
+}
+
+// Exact conversions between integers below 2^52 and doubles by the 2^52 magic: the
+// integer as the mantissa of a double of exponent 52 (one OR and one subtract, where a
+// general u64 <-> f64 conversion is four or six operations on the vector unit).
+constexpr double kTwo52 = 4503599627370496.0;
+__host__ __device__ inline double small_to_f64(uint64_t n) {          // n < 2^52
+    const uint64_t b = 0x4330000000000000ull | n;
+    double d;
+    memcpy(&d, &b, 8);
+    return d - kTwo52;
+}
+__host__ __device__ inline uint64_t f64_to_small(double e) {          // nearest integer, 0 <= e < 2^52
+    const double d = e + kTwo52;
+    uint64_t b;
+    memcpy(&b, &d, 8);
+    return b & 0x000FFFFFFFFFFFFFull;
+}
+
+// floor((n*m + add) / d) when the quotient is below 2^50 and n, m, add < 2^52 (the
+// decoder's targets floor(v*T/w) and ranges ceil(c*w/T) at prec <= 50 with totals
+// below 2^50): one fused double estimate, fma(n, m, add) * inv rounded to the nearest
+// integer, is within q * (2^-52 + err(inv)) + 1/2 of the quotient -- under 2 for an
+// inv good to 2^-50 (the device reciprocal after its Newton step) -- so the remainder
+// n*m + add - q*d lies in (-3d, 3d) and wrapping 64-bit arithmetic holds it exactly;
+// at most two corrections follow.  No 128-bit products: the decode step's chain of
+// quarter-rate multiplies (div_floor_inv: two estimates and 128-bit remainders)
+// becomes one FMA, one multiply and a 64-bit remainder.
+constexpr uint64_t kSmallQuot = 1ull << 50;
+__host__ __device__ inline uint64_t div_small_est(uint64_t n, uint64_t m, uint64_t add, double inv) {
+    const double e = __builtin_fma(small_to_f64(n), small_to_f64(m), small_to_f64(add)) * inv;
+    return f64_to_small(e > 0.0 ? e : 0.0);
+}
+__host__ __device__ inline uint64_t div_small_fix(uint64_t q, uint64_t n, uint64_t m, uint64_t add, uint64_t d) {
+    int64_t r = (int64_t)(n * m + add - q * d);
+    while (r < 0) { q -= 1; r += (int64_t)d; }
+    while (r >= (int64_t)d) { q += 1; r -= (int64_t)d; }
+    return q;
+}
+__host__ __device__ inline uint64_t div_small(uint64_t n, uint64_t m, uint64_t add, uint64_t d, double inv) {
+    return div_small_fix(div_small_est(n, m, add, inv), n, m, add, d);
 }
 
 // CDFPredictor.fudged_dist test (arith_code.py:84): fudged iff T > w*minp.

@@ -861,6 +861,20 @@ __device__ inline uint64_t window_bits(const BitWin &win, uint64_t nbits, uint64
     return v;
 }
 
+// A decoder state loaded by one wave for its own stream, moved to SGPRs: the compiler
+// cannot tell a value loaded from a wave-uniform address is uniform.
+__device__ inline void dec_state_uniform(DecState &st) {
+    st.l = (int64_t)rfl_u64((uint64_t)st.l);
+    st.h = (int64_t)rfl_u64((uint64_t)st.h);
+    st.x = (int64_t)rfl_u64((uint64_t)st.x);
+    st.pos = rfl_u64(st.pos);
+    st.nsym = (int64_t)rfl_u64((uint64_t)st.nsym);
+    st.err = __builtin_amdgcn_readfirstlane(st.err);
+    st.det = __builtin_amdgcn_readfirstlane(st.det);
+    st.err_step = (int64_t)rfl_u64((uint64_t)st.err_step);
+    st.ndet = (int64_t)rfl_u64((uint64_t)st.ndet);
+}
+
 __global__ void k_dec_init(DecState *states, int64_t B, int prec, const uint8_t *bits, uint64_t stride,
                            const uint64_t *nbits) {
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -896,9 +910,14 @@ __global__ void k_dec_init(DecState *states, int64_t B, int prec, const uint8_t 
 // wave-wide reductions on the serial path.  Needs cb <= tgt < cb + the chunk's
 // total (find_chunk guarantees it; zero-filled vectors past the row end then
 // cannot be the first to exceed); returns false otherwise.
-template <typename E, int VEC>
+struct NoIdle {
+    __device__ void operator()() {}
+};
+// `idle` runs once, right after the first round of loads is issued: work of the next
+// step that the re-read's round trip can hide (k_decode_seq: its chunk-total scan).
+template <typename E, int VEC, typename Idle = NoIdle>
 __device__ inline bool scan_chunk(const E *row, int64_t nvec, int64_t cv0, int G, uint64_t cb, uint64_t tgt,
-                                  uint64_t *cnt_out, uint64_t *lo_out, uint64_t *hi_out) {
+                                  uint64_t *cnt_out, uint64_t *lo_out, uint64_t *hi_out, Idle idle = Idle()) {
     constexpr int PF = 4;                                     // loads in flight: the scan is latency-bound
     for (int g0 = 0; g0 < G; g0 += PF) {
         typename VecT<E, VEC>::type xs[PF];
@@ -907,6 +926,7 @@ __device__ inline bool scan_chunk(const E *row, int64_t nvec, int64_t cv0, int G
             const int64_t vi = cv0 + (int64_t)(g0 + u) * 64 + (int64_t)lane_id();
             xs[u] = load_vec_or0<E, VEC>(row, g0 + u < G ? vi : nvec, nvec);
         }
+        if (g0 == 0) idle();
 #pragma unroll
         for (int u = 0; u < PF; u++) {
             if (g0 + u >= G) break;
@@ -1035,7 +1055,10 @@ __device__ inline int decode_fudged(const E *row, int64_t V, uint64_t w, uint64_
 }
 
 // Narrow to symbol s and renormalise, pulling k fresh bits into x
-// (emit_symbol + emit_bit, arith_code.py:274-291, value form).
+// (emit_symbol + emit_bit, arith_code.py:274-291, value form).  UNI: the state is
+// wave-uniform (SGPRs) and the window words are read back from the vector loads that
+// fetched them, so the renormalisation stays on the scalar unit.
+template <bool UNI = false>
 __device__ inline int decode_advance(DecState &st, uint64_t a, uint64_t bb, const BitWin &win, uint64_t nbits,
                                      int prec) {
     const int64_t l = st.l, x = st.x;
@@ -1047,7 +1070,8 @@ __device__ inline int decode_advance(DecState &st, uint64_t a, uint64_t bb, cons
     int64_t nx = x;
     if (k > 0) {
         const int sh = prec - k;
-        nx = (int64_t)((((uint64_t)x - (Ev << sh)) << k) | window_bits(win, nbits, st.pos, k));
+        const BitWin wu = UNI ? BitWin{rfl_u64(win.w0), rfl_u64(win.w1)} : win;
+        nx = (int64_t)((((uint64_t)x - (Ev << sh)) << k) | window_bits(wu, nbits, st.pos, k));
         st.pos += (uint64_t)k;
     }
     st.l = nl;
@@ -1057,12 +1081,55 @@ __device__ inline int decode_advance(DecState &st, uint64_t a, uint64_t bb, cons
     return 0;
 }
 
+// Per-phase cycle accounting of the sequential decode step (tools/dec_phase_probe.sh
+// builds a separate library with -DLAC_DEC_PHASES=1; the product build passes no clock
+// and the marks compile to nothing).  Phases: 0 row totals + scan, 1 targets, 2 chunk
+// search, 3 re-read + scan of the chunk, 4 ranges, 5 narrowing + renormalisation.
+struct NoClock {
+    __device__ void mark(int) {}
+};
+#ifndef LAC_DEC_PHASES
+#define LAC_DEC_PHASES 0
+#endif
+#if LAC_DEC_PHASES
+struct PhaseClock {
+    uint64_t prev = 0, acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    __device__ void start() { prev = __builtin_amdgcn_s_memtime(); }
+    __device__ void mark(int k) {
+        const uint64_t now = __builtin_amdgcn_s_memtime();
+        acc[k] += now - prev;
+        prev = now;
+    }
+};
+__device__ unsigned long long g_dec_phase[8];
+#endif
+
+// div_small with wave-uniform arguments: the double estimate on the vector unit (the
+// SALU has no FP64), read back, the 64-bit remainder and its corrections on the SALU.
+__device__ inline uint64_t div_small_u(uint64_t n, uint64_t m, uint64_t add, uint64_t d, double inv) {
+    return div_small_fix(rfl_u64(div_small_est(n, m, add, inv)), n, m, add, d);
+}
+// Two of them with one divisor (the ranges ceil(lo*w/T), ceil(hi*w/T)): both estimates
+// first, so the two FP64 chains overlap, then both corrections.
+__device__ inline void div_small_u2(uint64_t n0, uint64_t n1, uint64_t m, uint64_t add, uint64_t d, double inv,
+                                    uint64_t *q0, uint64_t *q1) {
+    const uint64_t e0 = rfl_u64(div_small_est(n0, m, add, inv)), e1 = rfl_u64(div_small_est(n1, m, add, inv));
+    *q0 = div_small_fix(e0, n0, m, add, d);
+    *q1 = div_small_fix(e1, n1, m, add, d);
+}
+
 // Everything after the row's totals are known: val_to_symbol + symbol_to_range
 // + advance.  `find_chunk(tgt, &cv0, &G, &cb)` locates the chunk holding tgt.
-template <typename E, int VEC, typename FindChunk>
+// UNI: the decoder state is wave-uniform (held in SGPRs by the caller), so the
+// serial chain runs on the scalar unit with div_small's quotients where they are
+// below 2^50 (prec <= 50, totals < 2^50): the few-stream decoders' step.
+template <typename E, int VEC, typename FindChunk, bool UNI = false, typename Clock = NoClock, typename Idle = NoIdle>
 __device__ inline int decode_symbol(DecState &st, const E *row, int64_t V, uint64_t T, uint64_t minp, int prec,
                                     int mapping, const uint8_t *bits, uint64_t nbits, FindChunk find_chunk,
-                                    int64_t *s_out) {
+                                    int64_t *s_out, Clock *clk = nullptr, Idle idle = Idle()) {
+    auto mark = [&](int k) {
+        if (clk) clk->mark(k);
+    };
     const BitWin win = bit_window(bits, nbits, st.pos);       // in flight during the search
     const int64_t l = st.l, h = st.h, x = st.x;
     if (x < l || x > h) return LAC_E_DECODE_RANGE;            // corrupted state / bits
@@ -1079,25 +1146,48 @@ __device__ inline int decode_symbol(DecState &st, const E *row, int64_t V, uint6
     bool det;
     if (mapping == LAC_MAP_FLOOR || !is_fudged(T, w, minp)) {
         uint64_t tgt, thi;                                    // targets of the 0- and 1-padded ends
-        div_pair(v, vhi < w ? vhi : 0, T, 0, w, recip(w), &tgt, &thi);   // tgt < T
+        const bool small = UNI && T < kSmallQuot && prec <= 50;   // uniform
+        if (small) {
+            const double iw = recip(w);
+            tgt = div_small_u(v, T, 0, w, iw);
+            thi = vhi == v ? tgt : (vhi < w ? div_small_u(vhi, T, 0, w, iw) : 0);
+        } else {
+            div_pair(v, vhi < w ? vhi : 0, T, 0, w, recip(w), &tgt, &thi);   // tgt < T
+        }
+        mark(1);
         int64_t cv0;
         int G;
         uint64_t cb;
         if (!find_chunk(tgt, &cv0, &G, &cb)) return LAC_E_DECODE_RANGE;
+        mark(2);
         uint64_t cnt, lo_c, hi_c;
-        if (!scan_chunk<E, VEC>(row, V / VEC, cv0, G, cb, tgt, &cnt, &lo_c, &hi_c)) return LAC_E_DECODE_RANGE;
+        if (!scan_chunk<E, VEC>(row, V / VEC, cv0, G, cb, tgt, &cnt, &lo_c, &hi_c, idle)) return LAC_E_DECODE_RANGE;
+        mark(3);
         s = cv0 * VEC + (int64_t)cnt;
-        div_pair(lo_c, hi_c, w, mapping == LAC_MAP_FLOOR ? 0 : T - 1, T, recip(T), &a, &bb);
+        const uint64_t add = mapping == LAC_MAP_FLOOR ? 0 : T - 1;
+        if (small) {
+            div_small_u2(lo_c, hi_c, w, add, T, recip(T), &a, &bb);
+        } else {
+            div_pair(lo_c, hi_c, w, add, T, recip(T), &a, &bb);
+        }
+        mark(4);
         det = vhi < w && thi < hi_c;                          // bisect_right(cdf, t_hi) == s
     } else {
         const int e = decode_fudged<E>(row, V, w, v, T, &s, &a, &bb);
         if (e) return e;
+        if (UNI) {                  // (from the wave reductions: back to SGPRs)
+            a = rfl_u64(a);
+            bb = rfl_u64(bb);
+            s = (int64_t)rfl_u64((uint64_t)s);
+        }
         det = vhi < bb;                                       // f_s > v_hi
     }
     if (st.det && det) st.ndet++;
     else st.det = 0;
     *s_out = s;
-    return decode_advance(st, a, bb, win, nbits, prec);
+    const int rc = decode_advance<UNI>(st, a, bb, win, nbits, prec);
+    mark(5);
+    return rc;
 }
 
 // One decode step for every stream, NW waves per stream (small stream counts:
@@ -1794,16 +1884,27 @@ __global__ __launch_bounds__(256) void k_decode_seq(const E *__restrict__ pmf, i
                                             const uint8_t *bits, uint64_t stride, const uint64_t *nbits,
                                             int32_t *sym_out, int64_t B, int mapping) {
     const int lane = (int)lane_id();
-    const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    // the stream index and its decoder state wave-uniform (SGPRs): the serial chain --
+    // the targets, the ranges, the renormalisation -- then runs on the scalar unit
+    // (decode_symbol<..., true>), with uniform branches instead of exec-masked ones
+    const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + wave_in_block();
     if (b >= B) return;
     DecState st = states[b];
+    dec_state_uniform(st);
     const uint8_t *mybits = bits + b * stride;
     const uint64_t mynbits = nbits[b];
     int64_t CI, nch;
     dec_chunk_layout<E, VEC>(V, &CI, &nch);
     uint64_t next = nsteps > 0 ? chunks[b * 64 + lane] : 0;
     DecRowMeta nmeta = nsteps > 0 ? meta[b] : DecRowMeta{0, 0};
+#if LAC_DEC_PHASES
+    PhaseClock clock, *clk = &clock;
+    clock.start();
+#else
+    NoClock *clk = nullptr;
+#endif
     for (int64_t i = 0; i < nsteps; i++) {
+        dec_state_uniform(st);                                 // (the loop's phis are not seen as uniform)
         const int64_t t = t0 + i;
         const uint64_t mine = next;
         const DecRowMeta rm = nmeta;
@@ -1832,7 +1933,9 @@ __global__ __launch_bounds__(256) void k_decode_seq(const E *__restrict__ pmf, i
                 *cb = readlane_u64(ex, src);
                 return true;
             };
-            err = decode_symbol<E, VEC>(st, row, V, rm.T, rm.minp, prec, mapping, mybits, mynbits, find_chunk, &s);
+            if (clk) clk->mark(0);
+            err = decode_symbol<E, VEC, decltype(find_chunk), true>(st, row, V, rfl_u64(rm.T), rfl_u64(rm.minp), prec,
+                                                                   mapping, mybits, mynbits, find_chunk, &s, clk);
         }
         if (err) {
             st.err = err;
@@ -1841,6 +1944,12 @@ __global__ __launch_bounds__(256) void k_decode_seq(const E *__restrict__ pmf, i
         if (lane == 0) *out = err ? -1 : (int32_t)s;
     }
     if (lane == 0) states[b] = st;
+#if LAC_DEC_PHASES
+    if (lane == 0) {
+        for (int k = 0; k < 6; k++) atomicAdd(&g_dec_phase[k], (unsigned long long)clock.acc[k]);
+        atomicAdd(&g_dec_phase[6], (unsigned long long)nsteps);
+    }
+#endif
 }
 
 // ================================================================ q1 logits path
@@ -2975,9 +3084,10 @@ __global__ __launch_bounds__(512, 2) void k_q1_stats_wide(const LT *__restrict__
     // pass 1 waits vmcnt(0) itself and a slot is refilled after lgkmcnt(0)); lanes past
     // the row load its last vector (masked when read)
     const uint32_t slot_base = (uint32_t)(uintptr_t)(lvoid_t *)&slots[w * 64];   // wave-uniform
-    auto ld_slot = [&](const LT *rw, int k) {
-        const int vi = tid + NT * (R + k);
-        const u32x4 *src = reinterpret_cast<const u32x4 *>(rw) + (vi < nvec ? vi : nvec - 1);
+    auto ld_slot = [&](const LT *rw, int k, int ti_, int nv_) {
+        // (ti_, nv_ opaque per row: 11 hoisted clamped offsets spilled the bf16 decode form)
+        const int vi = ti_ + NT * (R + k);
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(rw) + (vi < nv_ ? vi : nv_ - 1);
         uint32_t keep;
         asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" LAC_Q1_DMA_POLICY "\n\ts_mov_b32 m0, %0"
                      : "=&s"(keep)
@@ -2991,7 +3101,7 @@ __global__ __launch_bounds__(512, 2) void k_q1_stats_wide(const LT *__restrict__
         for (int j = 0; j < R; j++) x[j] = load_vec(rs, j);
         if (L > 0 && r0 < rows) {
 #pragma unroll
-            for (int kk = 0; kk < L; kk++) ld_slot(row_of(r0), kk);
+            for (int kk = 0; kk < L; kk++) ld_slot(row_of(r0), kk, tid, nvec);
         }
     }
     if (DEC && w == 0) bins[lane] = 0;
@@ -3001,6 +3111,12 @@ __global__ __launch_bounds__(512, 2) void k_q1_stats_wide(const LT *__restrict__
     // pass 2 once pass 1 has made it -inf; subtracted from the totals instead of masking
     // each vector (per-vector masks are loop-invariant: hoisted, they spilled)
     const uint32_t tab0 = q1_entry(0, xsh);
+    // decode: group grp's chunk, grp / G, by a multiply with m = ceil(2^32 / G) (exact
+    // for grp * G < 2^32; groups < 2^16 here): per-lane divisions by the runtime G were
+    // hoisted out of the row loop, one per batch, and spilled
+    const bool g1 = G <= 1;                                    // (m = 2^32 does not fit: G = 1 is the identity)
+    const uint32_t gmag = g1 ? 0u : (uint32_t)((0xFFFFFFFFull + (uint64_t)G) / (uint64_t)G);
+    auto chunk_of = [&](int grp) { return g1 ? grp : (int)__umulhi((uint32_t)grp, gmag); };
     for (int64_t r = r0; r < rows; r += stride) {          // (GROUP: a group's members share r)
         // (the row was loaded during the previous row's pass 2: rolling prefetch)
         pok = true;
@@ -3167,10 +3283,12 @@ __global__ __launch_bounds__(512, 2) void k_q1_stats_wide(const LT *__restrict__
                 // group (w + 8 j) = vectors [64 (w + 8 j), +64): wave w's vector j
                 uint64_t gsum = wave_multi_sum32<8>(sv);        // lane l < 8: vector j0 + q_index<8>(l)
                 if (lane < 8) {
-                    const int grp = w + NW * (j0 + q_index<8>(lane)), past = (grp + 1) * 64 - nv;
+                    // (the lane index fresh here: hoisted, the 7 batches' bin addresses spilled and
+                    //  their reloads' vmcnt(0) drained the rolling prefetch)
+                    const int grp = w + NW * (j0 + q_index<8>(lane_fresh())), past = (grp + 1) * 64 - nv;
                     if (past > 0 && past < 64) gsum -= (uint64_t)past * N * tab0;   // the row's last group
                     // (GROUP: segment group grp is the row's group vofs / 64 + grp; split is a multiple of 64)
-                    if (grp * 64 < nv) atomicAdd(&bins[(vofs / 64 + grp) / (int)G], (unsigned long long)gsum);
+                    if (grp * 64 < nv) atomicAdd(&bins[chunk_of(vofs / 64 + grp)], (unsigned long long)gsum);
                 }
             } else {
                 uint32_t bt = 0, bl = 0;
@@ -3205,16 +3323,16 @@ __global__ __launch_bounds__(512, 2) void k_q1_stats_wide(const LT *__restrict__
                 if (nxt) {
 #pragma unroll
                     for (int u = 0; u < 8; u++)
-                        if (k0 + u < L) ld_slot(nrw, k0 + u);
+                        if (k0 + u < L) ld_slot(nrw, k0 + u, ti, nv);
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 const int j0 = R + k0;
                 if constexpr (DEC) {
                     uint64_t gsum = wave_multi_sum32<8>(sv);
                     if (lane < 8) {
-                        const int grp = w + NW * (j0 + q_index<8>(lane)), past = (grp + 1) * 64 - nv;
+                        const int grp = w + NW * (j0 + q_index<8>(lane_fresh())), past = (grp + 1) * 64 - nv;
                         if (past > 0 && past < 64) gsum -= (uint64_t)past * N * tab0;
-                        if (grp * 64 < nv) atomicAdd(&bins[(vofs / 64 + grp) / (int)G], (unsigned long long)gsum);
+                        if (grp * 64 < nv) atomicAdd(&bins[chunk_of(vofs / 64 + grp)], (unsigned long long)gsum);
                     }
                 } else {
                     uint32_t bt = 0, bl = 0;
@@ -3298,18 +3416,26 @@ __global__ LAC_DEC_BOUNDS void k_q1_decode(const LT *__restrict__ lg, int64_t st
     q1_load_tab(tab, xsh);
     constexpr int N = LogitN<LT>::N;
     const int lane = (int)lane_id();
-    const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    // (round 4) the stream and its decoder state wave-uniform (SGPRs): the serial chain
+    // -- targets, ranges, renormalisation, the determined test -- runs on the scalar
+    // unit with uniform branches, its quotients by div_small (q1 totals are <= 2^(prec-1),
+    // so at prec <= 50 every quotient is below 2^50); the vector unit keeps the chunk
+    // scan and the re-quantisation of one 64-vector group per search round
+    const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + wave_in_block();
     if (b >= B) return;
     DecState st = states[b];
+    dec_state_uniform(st);
     const uint8_t *mybits = bits + b * stride;
-    const uint64_t mynbits = nbits[b];
+    const uint64_t mynbits = rfl_u64(nbits[b]);
     const int64_t nvec = V / N;
+    const bool small = prec <= 50;
     uint64_t next = nsteps > 0 ? chunks[b * 64 + lane] : 0;
     float mnext = nsteps > 0 ? mrow[b] : 0.f;
     for (int64_t i = 0; i < nsteps; i++) {
+        dec_state_uniform(st);                                 // (the loop's phis are not seen as uniform)
         const int64_t t = t0 + i, r = i * B + b;
         const uint64_t mine = next;
-        const float mcur = mnext;
+        const float mcur = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, mnext)));
         if (i + 1 < nsteps) {                                  // prefetch: independent of the state
             next = chunks[(r + B) * 64 + lane];
             mnext = mrow[r + B];
@@ -3329,13 +3455,17 @@ __global__ LAC_DEC_BOUNDS void k_q1_decode(const LT *__restrict__ lg, int64_t st
         const int64_t l = st.l, h = st.h, x = st.x;
         if (x < l || x > h) err = LAC_E_DECODE_RANGE;
         const uint64_t w = (uint64_t)(h - l + 1), v = (uint64_t)(x - l);
-        if (!err && is_fudged(T, w, 1)) err = LAC_E_TABLE;             // impossible by the choice of k
+        if (!err && T > w) err = LAC_E_TABLE;                  // fudged (minp 1): impossible by the choice of k
         if (!err) {
+            const uint64_t past = st.pos > mynbits ? st.pos - mynbits : 0;
+            const int u = past < (uint64_t)prec ? (int)past : prec;
+            const uint64_t vh = v + ((1ull << u) - 1);
             uint64_t tgt, thi;
-            {
-                const uint64_t past = st.pos > mynbits ? st.pos - mynbits : 0;
-                const int u = past < (uint64_t)prec ? (int)past : prec;
-                const uint64_t vh = v + ((1ull << u) - 1);
+            if (small) {
+                const double iw = recip(w);
+                tgt = div_small_u(v, T, 0, w, iw);
+                thi = vh == v ? tgt : (vh < w ? div_small_u(vh, T, 0, w, iw) : 0);
+            } else {
                 div_pair(v, vh < w ? vh : 0, T, 0, w, recip(w), &tgt, &thi);
             }
             const uint64_t ex = incl - mine;
@@ -3345,14 +3475,16 @@ __global__ LAC_DEC_BOUNDS void k_q1_decode(const LT *__restrict__ lg, int64_t st
                 const int src = __ffsll((unsigned long long)mask) - 1;
                 uint64_t cb = readlane_u64(ex, src);
                 const int64_t cv0 = (int64_t)src * G * 64;
-                // the crossing lane by ballot, as scan_chunk (entries <= tgt are a prefix)
+                // the crossing lane by ballot, as scan_chunk (entries <= tgt are a prefix);
+                // a lane's 8 (bf16) / 4 (f32) entries are <= 2^24 each, so its own prefix
+                // runs in 32 bits and only the wave scan needs 64
                 uint64_t lo_c = cb, hi_c = ~0ull, cnt = 0;
                 bool found = false;
                 for (int64_t g = 0; g < G && !found; g++) {
                     const int64_t vi = cv0 + g * 64 + lane;
                     const bool valid = vi < nvec;
                     const u32x4 xv = ld16(row, valid ? vi : nvec - 1, false);
-                    uint64_t loc[N], ls = 0;
+                    uint32_t loc[N], ls = 0;
 #pragma unroll
                     for (int j = 0; j < N; j++) {
                         // looked up unconditionally (xv is a clamped in-row vector), masked
@@ -3362,23 +3494,25 @@ __global__ LAC_DEC_BOUNDS void k_q1_decode(const LT *__restrict__ lg, int64_t st
                         ls += valid ? q : 0u;
                         loc[j] = ls;
                     }
-                    const uint64_t in = wave_incl_scan_u64(ls);
+                    const uint64_t in = wave_incl_scan_u64((uint64_t)ls);
                     const uint64_t exb = cb + in - ls;
                     const uint64_t m = __ballot(exb + ls > tgt);
                     if (m) {
                         const int L = __ffsll((unsigned long long)m) - 1;
-                        uint64_t k = 0, lo = exb, hi = ~0ull;
+                        // lane L: exb <= tgt < exb + ls, so tgt - exb fits 32 bits there
+                        const uint32_t rel = (uint32_t)(tgt - exb);
+                        uint32_t k = 0, lo = 0, hi = ~0u;
 #pragma unroll
                         for (int j = 0; j < N; j++) {
-                            const uint64_t ce = exb + loc[j];
-                            const bool le = ce <= tgt;
-                            k += le ? 1 : 0;
-                            lo = le ? ce : lo;
-                            hi = (!le && ce < hi) ? ce : hi;
+                            const bool le = loc[j] <= rel;
+                            k += le ? 1u : 0u;
+                            lo = le ? loc[j] : lo;
+                            hi = (!le && loc[j] < hi) ? loc[j] : hi;
                         }
-                        cnt = (uint64_t)(g * 64 + L) * N + readlane_u64(k, L);
-                        lo_c = readlane_u64(lo, L);
-                        hi_c = readlane_u64(hi, L);
+                        const uint64_t eb = readlane_u64(exb, L);
+                        cnt = (uint64_t)(g * 64 + L) * N + (uint64_t)__builtin_amdgcn_readlane((int)k, L);
+                        lo_c = eb + (uint32_t)__builtin_amdgcn_readlane((int)lo, L);
+                        hi_c = eb + (uint32_t)__builtin_amdgcn_readlane((int)hi, L);
                         found = true;
                     }
                     cb += readlane_u64(in, 63);
@@ -3388,14 +3522,15 @@ __global__ LAC_DEC_BOUNDS void k_q1_decode(const LT *__restrict__ lg, int64_t st
                 } else {
                     s = cv0 * N + (int64_t)cnt;
                     uint64_t a, bb;
-                    div_pair(lo_c, hi_c, w, T - 1, T, recip(T), &a, &bb);
-                    const uint64_t past = st.pos > mynbits ? st.pos - mynbits : 0;
-                    const int u = past < (uint64_t)prec ? (int)past : prec;
-                    const uint64_t vhi = v + ((1ull << u) - 1);
-                    const bool det = vhi < w && thi < hi_c;
+                    if (small) {
+                        div_small_u2(lo_c, hi_c, w, T - 1, T, recip(T), &a, &bb);
+                    } else {
+                        div_pair(lo_c, hi_c, w, T - 1, T, recip(T), &a, &bb);
+                    }
+                    const bool det = vh < w && thi < hi_c;
                     if (st.det && det) st.ndet++;
                     else st.det = 0;
-                    err = decode_advance(st, a, bb, win, mynbits, prec);
+                    err = decode_advance<true>(st, a, bb, win, mynbits, prec);
                 }
             }
         }
@@ -4052,9 +4187,12 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
         // Rows of 20481..26112 vectors add 11 vectors per thread in LDS slots (same box,
         // profiles/r03/vocabs/: bf16 V = 202048 (Llama-4) 66.9 -> 81.1 %, bf16 200024
         // (o200k) 65.8 -> 76.0 %, f32 100280 (cl100k) 72.4 -> 80.4 %, f32 102400
-        // (DeepSeek) 78.5 -> 86.7 %; f32 decode stats 8-11 % faster); not the bf16
-        // decode form, which spills 21 VGPRs there (368 vs 306 us per step at 202048)
-        if (sh == 0 && nvec <= kQ1WideSlotMaxVec && !(DEC && sizeof(LT) == 2 && nvec > kQ1WideMaxVec)) sh = 22;
+        // (DeepSeek) 78.5 -> 86.7 %; f32 decode stats 8-11 % faster).  The bf16 decode form
+        // spilled 21 VGPRs there until round 4 (hoisted LDS-DMA offsets and per-batch bin
+        // addresses, now recomputed where used): spill-free, bf16 V = 202048 decode stats
+        // 313 -> 269 us per step (65.9 -> 76.9 % of peak), 200024 317 -> 275 us
+        // (profiles/r04/ab_dec/), so AUTO takes it in both directions
+        if (sh == 0 && nvec <= kQ1WideSlotMaxVec) sh = 22;
         // longer rows: row groups (shapes 19 / 20 / 21: segments in row slots of 1 / 2 / 4
         // rows per block), the form that keeps the most bytes in flight (q1_group).
         // Round 2 had whole blocks per segment (kg = 2..4 blocks of 1 or 2 rows): bf16
@@ -4666,6 +4804,20 @@ int lac_q1_group_aborted(lac_ctx *c, int64_t *aborted, void *stream) {
     *aborted = v ? 1 : 0;
     return LAC_OK;
 }
+
+#if LAC_DEC_PHASES
+// probe builds only (tools/dec_phase_probe.sh): the k_decode_seq phase cycle sums
+// (s_memtime) and the steps they cover; reset != 0 clears them
+int lac_debug_dec_phases(uint64_t *out8, int reset) {
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_dec_phase), sizeof(uint64_t) * 8));
+    if (reset) {
+        const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_dec_phase), z, sizeof z));
+    }
+    return LAC_OK;
+}
+#endif
 
 int lac_profile_enable(lac_ctx *c, int on) {
     if (!c) return fail(LAC_E_ARG, "ctx is NULL");

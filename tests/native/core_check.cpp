@@ -55,6 +55,12 @@ uint64_t cc_cr_ratio(uint64_t a, uint64_t b) {
 }
 
 // floor/ceil(c*w/T) through the row fraction (~0 for rows without one).
+// div_small with the reciprocal `rel` (relative) off the correctly rounded 1/d, as
+// the device's v_rcp_f64 + Newton can be
+uint64_t cc_div_small(uint64_t n, uint64_t m, uint64_t add, uint64_t d, double rel) {
+    return div_small(n, m, add, d, (1.0 / (double)d) * (1.0 + rel));
+}
+
 uint64_t cc_frac_mul_div(uint64_t c, uint64_t w, uint64_t T, int ceil) {
     const uint64_t f = row_frac(c, T);
     return f == kNoFrac ? ~0ull : frac_mul_div(f, c, w, T, ceil != 0);

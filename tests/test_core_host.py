@@ -80,6 +80,37 @@ def test_frac_mul_div_exact(core):
     assert core.cc_frac_mul_div(5, 1 << 47, 1 << 63, 1) == (1 << 64) - 1     # T >= 2^63: no fraction
 
 
+def test_div_small_exact(core):
+    """div_small (the decode step's quotient at prec <= 50 / totals < 2^50): exact
+    floor((n*m + add)/d) for quotients below 2^50, with the reciprocal up to 2^-49
+    off (the device's v_rcp_f64 after one Newton step is good to ~2^-50)."""
+    import random
+    core.cc_div_small.restype = C.c_uint64
+    core.cc_div_small.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_double]
+    rng = random.Random(11)
+    n_cases = 0
+    while n_cases < 40000:
+        d = rng.randint(1, (1 << rng.randint(1, 50)))
+        n = rng.randint(0, (1 << rng.randint(0, 50)))
+        m = rng.randint(0, (1 << rng.randint(0, 50)))
+        add = rng.choice([0, d - 1, rng.randint(0, d)])
+        q = (n * m + add) // d
+        if q >= 1 << 50:
+            continue
+        rel = rng.choice([0.0, 2.0 ** -49, -2.0 ** -49, rng.uniform(-1, 1) * 2.0 ** -50])
+        assert core.cc_div_small(n, m, add, d, rel) == q, (n, m, add, d, rel)
+        n_cases += 1
+    # the decoder's own shapes: targets floor(v*T/w), v < w, and ranges ceil(c*w/T), c <= T
+    for _ in range(20000):
+        prec = rng.randint(2, 50)
+        w = rng.randint((1 << (prec - 1)) + 1, 1 << prec)
+        T = rng.randint(1, (1 << 50) - 1)
+        v = rng.randint(0, w - 1)
+        c = rng.randint(0, T)
+        assert core.cc_div_small(v, T, 0, w, 2.0 ** -50) == v * T // w
+        assert core.cc_div_small(c, w, T - 1, T, -2.0 ** -50) == -(-(c * w) // T)
+
+
 def test_core_matches_golden(core):
     for kind in ("static", "perstep"):
         for c in load_golden("small_cases.json")[kind]:

@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""Where one few-stream decode step spends its time: the c2
+workload (V=32000, 1 stream, T steps) decoded by the stats path with a probe build
+of liblac (-DLAC_DEC_PHASES=1, tools/dec_phase_probe.sh) whose k_decode_seq adds
+s_memtime marks between the phases of the sequential step:
+
+  0 row totals + their wave scan (loop top, prefetch of the next row's totals)
+  1 targets floor(v*T/w) (and the 1-padded twin)
+  2 chunk search (ballot over the 64 chunk totals)
+  3 re-read of the target chunk (one round of loads) + its scan to the symbol
+  4 ranges ceil(c*w/T)
+  5 narrowing, renormalisation, bit window
+
+    LAC_LIB=tools/_probe/liblac_phases.so python tools/dec_phase_probe.py [--tokens 4096]
+
+Prints one JSON line: shader cycles per step per phase (the marks cost a few
+cycles each) and the decode kernels' hipEvent time per step for scale.
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--vocab", type=int, default=32000)
+    ap.add_argument("--tokens", type=int, default=4096)
+    ap.add_argument("--streams", type=int, default=1)
+    a = ap.parse_args()
+    import torch
+    from lac_amd import synth
+    from lac_amd.batch import BatchCoder
+    dev = torch.device("cuda", 0)
+    V, B, T, P = a.vocab, a.streams, a.tokens, 48
+    coder = BatchCoder(V, B, prec=P, pmf_bits=32, capacity_bits=T * (P + 2) + 256, device=dev)
+    pmf, sym = synth.softmax_tables(T, B, V, seed=1234, device=dev, scale_bits=31, storage_bits=32)
+    coder.encode_job(pmf, sym)
+    lib = coder.lib
+    lib.lac_debug_dec_phases.argtypes = [C.c_void_p, C.c_int]
+    out = (C.c_uint64 * 8)()
+    res = {}
+    for rep in range(3):
+        coder.decode_open()
+        lib.lac_debug_dec_phases(C.cast(out, C.c_void_p), 1)
+        ms = (C.c_double * 8)()
+        cnt = (C.c_int64 * 8)()
+        lib.lac_profile_read(coder.ctx, None, None, 1)
+        lib.lac_profile_enable(coder.ctx, 1)
+        dec = coder.decode(pmf)
+        torch.cuda.synchronize()
+        lib.lac_profile_enable(coder.ctx, 0)
+        lib.lac_profile_read(coder.ctx, C.cast(ms, C.c_void_p), C.cast(cnt, C.c_void_p), 1)
+        lib.lac_debug_dec_phases(C.cast(out, C.c_void_p), 1)
+        steps = max(int(out[6]), 1)
+        names = ["totals+scan", "targets", "chunk_search", "reread+scan", "ranges", "renorm"]
+        cyc = {n: out[k] / steps for k, n in enumerate(names)}
+        res = {"rep": rep, "steps": steps, "cycles_per_step": cyc, "cycles_total_per_step": sum(cyc.values()),
+               "kernel_us_per_step": {"decode (stats + seq)": 1e3 * ms[3] / max(T, 1)},
+               "round_trip": bool(torch.equal(dec, sym))}
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
