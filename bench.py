@@ -224,13 +224,14 @@ def main():
     rc, err, err_step = coder.status()
     data, nbits = coder.to_bytes() if rc == 0 else ([], None)
     decode = coder.decode_logits if logits_in else coder.decode
-    coder.decode_open()
-    dec = decode(pmf)                                      # warm (the clocks ramp after a workload switch)
-    torch.cuda.synchronize()
-    round_trip = bool(torch.equal(dec, sym)) and rc == 0
-    # the timed passes back to back with one synchronisation, as the encode jobs run (a
-    # pass timed alone after a host sync paid the clocks' ramp after the idle gap: bf16
-    # Qwen2 decode row stats 209 us per step alone, 182 us back to back, tools/q1_b2b.py)
+    # two warm passes, then the timed passes, all back to back with one synchronisation, as
+    # the encode jobs run (a pass timed alone after a host sync paid the clocks' ramp after
+    # the idle gap: bf16 Qwen2 decode row stats 209 us per step alone, 182 us back to back,
+    # tools/q1_b2b.py)
+    warm = []
+    for _ in range(2):
+        coder.decode_open()
+        warm.append(decode(pmf))
     reps = max(1, args.decode_reps)
     coder.lib.lac_profile_read(coder.ctx, None, None, 1)
     coder.lib.lac_profile_enable(coder.ctx, 1)
@@ -245,16 +246,17 @@ def main():
     dms = (C.c_double * 8)()
     dcnt = (C.c_int64 * 8)()
     coder.lib.lac_profile_read(coder.ctx, C.cast(dms, C.c_void_p), C.cast(dcnt, C.c_void_p), 1)
-    for dec in outs:
+    round_trip = rc == 0
+    for dec in warm + outs:
         round_trip = round_trip and bool(torch.equal(dec, sym))
-    del outs
+    del outs, warm
     mid = ((d1 - d0) / reps, {k: dms[k] / reps for k in (3, 5, 6, 7) if dcnt[k]})
     dkids = sorted(mid[1])                                     # decode_step|stats path, decode_wave, q1 pair
     dstep_ms = sum(mid[1].values()) / max(T, 1)
     names = {3: "k_decode_step or k_dec_stats+k_decode_seq", 5: "k_decode_wave(_fine) or k_decode_block", 6: "k_q1_stats",
              7: "k_q1_decode"}
     decode_info = {"symbols_per_s": B * T / mid[0], "kernel": "+".join(names[k] for k in dkids),
-                   "passes": f"{reps} passes back to back after a warm one (mean)",
+                   "passes": f"{reps} passes back to back after two warm ones (mean)",
                    "kernel_ms_per_step": dstep_ms,
                    "kernel_ms_per_step_each": {names[k]: mid[1][k] / max(T, 1) for k in dkids},
                    "achieved_GBps": B * (V * ebytes + 4) / (dstep_ms * 1e-3) / 1e9 if dkids else None}

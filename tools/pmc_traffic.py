@@ -19,13 +19,24 @@ import statistics
 import sys
 
 STREAMING = ("k_encode_fused", "k_row_stats", "k_decode_step", "k_decode_wave_fine", "k_decode_wave",
-             "k_q1_stats", "k_dec_stats")
+             "k_q1_stats", "k_q1_stats_dec", "k_dec_stats")
+
+
+def _q1_decode_form(name):
+    """True when a k_q1_stats* kernel name is the decode form (its DEC template argument)."""
+    import re
+    m = re.search(r"::(k_q1_stats(?:_wide|_rl)?)<([^>]*)>", name)
+    if not m:
+        return False
+    args = [x.strip() for x in m.group(2).split(",")]
+    pos = {"k_q1_stats": 3, "k_q1_stats_wide": 2, "k_q1_stats_rl": 1}[m.group(1)]
+    return len(args) > pos and args[pos] == "true"
 
 
 def short(name):
-    if "::k_q1_stats_rl<" in name or "::k_q1_stats_wide<" in name:   # register + LDS-slot / 8-wave row stats
-        return "k_q1_stats"
-    for k in STREAMING + ("k_encode", "k_finish", "k_q1_decode"):
+    if "::k_q1_stats" in name:        # the row stats (incl. register + LDS-slot / 8-wave forms), by direction
+        return "k_q1_stats_dec" if _q1_decode_form(name) else "k_q1_stats"
+    for k in STREAMING + ("k_encode", "k_finish", "k_q1_decode", "k_decode_seq"):
         if f"::{k}<" in name or f"::{k}(" in name:
             return k
     return None
