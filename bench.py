@@ -236,12 +236,16 @@ def main():
     coder.lib.lac_profile_read(coder.ctx, None, None, 1)
     coder.lib.lac_profile_enable(coder.ctx, 1)
     outs = []
-    d0 = time.perf_counter()
+    # device time of the timed passes: events on the coder's stream (torch's current one),
+    # the first recorded behind the warm passes, which are still running when it is queued
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
     for _ in range(reps):
         coder.decode_open()
         outs.append(decode(pmf))
+    e1.record()
     torch.cuda.synchronize()
-    d1 = time.perf_counter()
+    d0, d1 = 0.0, e0.elapsed_time(e1) * 1e-3
     coder.lib.lac_profile_enable(coder.ctx, 0)
     dms = (C.c_double * 8)()
     dcnt = (C.c_int64 * 8)()

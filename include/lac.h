@@ -198,6 +198,15 @@ int lac_copy_bits_dev(lac_ctx *ctx, uint8_t *dst_dev, uint64_t dst_stride, void 
 /* Per-stream bit counts (uint64 [streams]) copied device to device (async). */
 int lac_copy_nbits_dev(lac_ctx *ctx, uint64_t *dst_dev, void *stream);
 
+/* The encoded streams packed back to back for the wire (after lac_encode_finish): a
+ * header of every stream's bit count in `hdr_bytes` = 2 or 4 bytes each (little
+ * endian), then stream b's ceil(nbits_b / 8) bytes (measure_compress's
+ * bytes(group_bits(bits())), arith_code.py:401-420) for b = 0, 1, ...; *len_dev
+ * (device uint64) receives the total length.  dst_dev holds at least
+ * streams * (hdr_bytes + 8 * ceil(capacity_bits / 64)) bytes.  Two small launches,
+ * asynchronous on `stream`: the multi-GPU gather's payload (lac_amd.dist). */
+int lac_pack_bits(lac_ctx *ctx, uint8_t *dst_dev, int hdr_bytes, uint64_t *len_dev, void *stream);
+
 /* Synchronise and copy each stream's coder registers l, h (A_to_bin.l/.h,
  * arith_code.py:161-162); either pointer may be NULL. */
 int lac_encoder_registers(lac_ctx *ctx, int64_t *l_host, int64_t *h_host, void *stream);

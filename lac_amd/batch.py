@@ -252,6 +252,20 @@ class BatchCoder:
         check(self.lib.lac_copy_nbits_dev(self.ctx, C.c_void_p(out.data_ptr()), self._stream))
         return out
 
+    def pack_bits(self, out, hdr_bytes, length):
+        """The finished streams packed for the wire into the uint8 device tensor ``out``
+        (include/lac.h lac_pack_bits: a header of bit counts, ``hdr_bytes`` = 2 or 4 each,
+        then each stream's bytes back to back); ``length`` (a one-element 8-byte integer
+        device tensor) receives the packed length.  Asynchronous; no host sync."""
+        need = self.streams * (hdr_bytes + self.bits_stride())
+        if out.dtype != _torch().uint8 or not out.is_contiguous() or out.numel() < need or out.device != self.device:
+            raise ValueError(f"out must be a contiguous uint8 device tensor of >= {need} bytes on {self.device}")
+        if length.numel() != 1 or length.element_size() != 8 or length.device != self.device:
+            raise ValueError("length must be a one-element 8-byte integer tensor on the coder's device")
+        check(self.lib.lac_pack_bits(self.ctx, C.c_void_p(out.data_ptr()), int(hdr_bytes),
+                                     C.c_void_p(length.data_ptr()), self._stream))
+        return out, length
+
     def nbits_tensor(self):
         """Per-stream bit counts as a fresh int64 device tensor (asynchronous copy)."""
         torch = _torch()

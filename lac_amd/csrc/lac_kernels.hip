@@ -802,6 +802,48 @@ __global__ __launch_bounds__(256) void k_finish(EncState *states, uint64_t *plan
 // trace (A_to_bin.step / run in lac_amd/coder.py) so a stream of any length
 // fits a fixed capacity; the packed output of lac_encode_finish then holds
 // only the tail, but the flush digits are exact.
+// lac_pack_bits: the streams' byte offsets (an exclusive scan of ceil(nbits / 8) behind
+// the header, one 1024-thread block: thread t sums a contiguous run of streams, the
+// block scans the 1024 run sums) and the header of bit counts; then one wave per
+// stream copies its packed bytes (planeA, big-endian, after k_finish).
+__global__ __launch_bounds__(1024) void k_pack_scan(const uint64_t *__restrict__ nbits, int64_t B, int hdr,
+                                                    uint64_t *__restrict__ off, uint8_t *__restrict__ dst,
+                                                    uint64_t *__restrict__ len) {
+    __shared__ uint64_t part[1024];
+    const int t = threadIdx.x;
+    const int64_t per = (B + 1023) / 1024, b0 = t * per, b1 = b0 + per < B ? b0 + per : B;
+    uint64_t sum = 0;
+    for (int64_t b = b0; b < b1; b++) sum += (nbits[b] + 7) >> 3;
+    part[t] = sum;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {                       // Hillis-Steele inclusive scan
+        const uint64_t v = t >= d ? part[t - d] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint64_t o = (uint64_t)hdr * (uint64_t)B + part[t] - sum;
+    for (int64_t b = b0; b < b1; b++) {
+        const uint64_t n = nbits[b];
+        off[b] = o;
+        o += (n + 7) >> 3;
+        for (int i = 0; i < hdr; i++) dst[b * hdr + i] = (uint8_t)(n >> (8 * i));
+    }
+    if (t == 1023) *len = (uint64_t)hdr * (uint64_t)B + part[1023];
+}
+
+__global__ __launch_bounds__(256) void k_pack_copy(const uint64_t *__restrict__ planeA, uint64_t cap_words,
+                                                   const uint64_t *__restrict__ nbits,
+                                                   const uint64_t *__restrict__ off, int64_t B,
+                                                   uint8_t *__restrict__ dst) {
+    const int64_t b = (int64_t)blockIdx.x * 4 + wave_in_block();
+    if (b >= B) return;
+    const uint64_t n = (nbits[b] + 7) >> 3;
+    const uint8_t *src = reinterpret_cast<const uint8_t *>(planeA + (uint64_t)b * cap_words);
+    uint8_t *d = dst + off[b];
+    for (uint64_t i = lane_id(); i < n; i += 64) d[i] = src[i];
+}
+
 __global__ void k_enc_rebase(EncState *states, int64_t B) {
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= B) return;
@@ -3612,6 +3654,7 @@ struct lac_ctx {
     void *dmeta = nullptr;              // stats-path decode: [chunk_steps * B] DecRowMeta
     float *q1m = nullptr;               //                [chunk_steps * B] row maxima
     uint64_t *pxch = nullptr;           // paired row stats (shape 19): [2 * cus] maximum words
+    uint64_t *pack_off = nullptr;       // lac_pack_bits: [B] byte offsets of the streams
     int64_t xch_abort = -1;             // word of pxch holding the last row-group launch's abort flag
     // live kernel timing (lac_profile_enable): hipEvent pairs around launches
     bool prof = false;
@@ -4373,6 +4416,7 @@ int lac_close(lac_ctx *c) {
     (void)hipFree(c->dmeta);
     (void)hipFree(c->q1m);
     (void)hipFree(c->pxch);
+    (void)hipFree(c->pack_off);
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
     delete c;
     return LAC_OK;
@@ -4518,6 +4562,20 @@ int lac_copy_bits_dev(lac_ctx *c, uint8_t *dst, uint64_t dst_stride, void *strea
     const uint64_t width = dst_stride < src_stride ? dst_stride : src_stride;
     HIPCHK(hipMemcpy2DAsync(dst, dst_stride, c->planeA, src_stride, width, (size_t)c->B, hipMemcpyDeviceToDevice,
                             S(stream)));
+    return LAC_OK;
+}
+
+int lac_pack_bits(lac_ctx *c, uint8_t *dst, int hdr_bytes, uint64_t *len_dev, void *stream) {
+    if (!c || !dst || !len_dev || (hdr_bytes != 2 && hdr_bytes != 4)) return fail(LAC_E_ARG, "bad argument");
+    HIPCHK(hipSetDevice(c->device));
+    if (!c->pack_off) HIPCHK(hipMalloc(&c->pack_off, sizeof(uint64_t) * (c->B > 0 ? c->B : 1)));
+    k_pack_scan<<<1, 1024, 0, S(stream)>>>(c->nbits, c->B, hdr_bytes, c->pack_off, dst, len_dev);
+    CHECK_LAUNCH();
+    if (c->B > 0) {
+        k_pack_copy<<<(unsigned)((c->B + 3) / 4), 256, 0, S(stream)>>>(c->planeA, c->cap_words, c->nbits, c->pack_off,
+                                                                       c->B, dst);
+        CHECK_LAUNCH();
+    }
     return LAC_OK;
 }
 

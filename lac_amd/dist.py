@@ -200,8 +200,17 @@ class BitstreamGatherer:
         self.B = B
         self.cap = B * self.hdr + B * self.width + 1
         self.io_dev = torch.device("cpu") if self.gloo else torch.device(dev)
-        self.slots = [(torch.empty((B, self.width), dtype=torch.uint8, device=dev),
-                       torch.empty((B,), dtype=torch.int64, device=dev)) for _ in range(self.depth)]
+        # per slot the packed payload (a BatchCoder packs its planes directly, lac_pack_bits)
+        # or, for other coders, the copies pack_bitstreams works from
+        if hasattr(coder, "pack_bits"):
+            self.packed = [(torch.empty(self.cap, dtype=torch.uint8, device=dev),
+                            torch.tensor([0, B, self.width, self.hdr], dtype=torch.int64, device=dev))
+                           for _ in range(self.depth)]
+            self.slots = None
+        else:
+            self.packed = None
+            self.slots = [(torch.empty((B, self.width), dtype=torch.uint8, device=dev),
+                           torch.empty((B,), dtype=torch.int64, device=dev)) for _ in range(self.depth)]
         # root: per slot and rank a receive buffer, (re)sized to the largest payload seen
         self.recv = [[None] * self.world if self.rank == self.root else None for _ in range(self.depth)]
         self.meta = [torch.empty(self.world * self.META, dtype=torch.int64, device=self.io_dev)
@@ -228,12 +237,16 @@ class BitstreamGatherer:
         self.k += 1
         self._finish(i)                                         # slot i's previous job, if any
         self._send_pending()                                    # the jobs queued since: their exact sends
-        bits, nbits = self.slots[i]
-        self.coder.copy_bits_into(bits)                          # on the caller's stream
-        self.coder.copy_nbits_into(nbits)
-        payload, L = pack_bitstreams(bits, nbits, self.hdr)
-        mine = torch.cat([L.to(torch.int64).reshape(1), self._shape_meta])
-        st = {"payload": payload, "nbits": nbits, "job": self.k}
+        if self.packed is not None:                              # BatchCoder: one pack on the device,
+            payload, mine = self.packed[i]                       # its length straight into the sizes row
+            self.coder.pack_bits(payload, self.hdr, mine[:1])    # (on the caller's stream)
+        else:                                                    # any coder with the copy accessors
+            bits, nbits = self.slots[i]
+            self.coder.copy_bits_into(bits)
+            self.coder.copy_nbits_into(nbits)
+            payload, L = pack_bitstreams(bits, nbits, self.hdr)
+            mine = torch.cat([L.to(torch.int64).reshape(1), self._shape_meta])
+        st = {"payload": payload, "job": self.k}
         if self.gloo:
             _all_gather(self.meta[i], mine.cpu(), self.group, self.world)
             st["meta"] = self.meta[i].view(self.world, self.META).tolist()
@@ -304,10 +317,12 @@ class BitstreamGatherer:
         if st is None:
             return
         self._send_pending()                                    # older jobs first, then this one
+        # the caller's stream waits for this job's sends and receives only (its payload
+        # slot is about to be reused; the root's received bytes are then visible) -- not
+        # for the whole side stream, which already holds later jobs' size exchanges: that
+        # wait cost ~60 us of cross-queue hops per job (profiles/r04/gather/)
         for w in st["works"]:
             w.wait()
-        if not self.gloo:
-            torch.cuda.current_stream().wait_stream(self.side)   # later work sees the received bytes
         if self.rank == self.root:
             self.last = [(self.recv[i][r], m[0], m[1], m[2], m[3]) for r, m in enumerate(st["meta"])]
             self.last_job = st["job"]

@@ -83,3 +83,29 @@ def test_rccl_gather_and_scatter_world1_decode(nccl_world1):
     out = coder.decode(torch.from_numpy(pmf.view(np.int32)).to(nccl_world1))
     assert torch.equal(out.cpu(), torch.from_numpy(sym))
     coder.close()
+
+
+@pytest.mark.parametrize("hdr", [2, 4])
+def test_pack_bits_kernel_equals_torch_packing(nccl_world1, hdr):
+    """lac_pack_bits (BatchCoder.pack_bits, the gatherer's payload) == the torch
+    reference packing pack_bitstreams of the same streams: header of bit counts, then
+    each stream's bytes back to back; ragged lengths, and a job of empty streams."""
+    from lac_amd.batch import BatchCoder
+    from lac_amd.dist import pack_bitstreams, unpack_bitstreams
+    V, B, T = 1000, 777, 9
+    coder = BatchCoder(V, B, prec=48, capacity_bits=T * 50 + 256, device=nccl_world1)
+    bits, nbits, _, _ = _job(coder, 21, T, B, V)
+    want, wlen = pack_bitstreams(bits, nbits, hdr)
+    out = torch.full((B * (hdr + coder.bits_stride()) + 1,), 0xAB, dtype=torch.uint8, device=nccl_world1)
+    ln = torch.zeros(1, dtype=torch.int64, device=nccl_world1)
+    coder.pack_bits(out, hdr, ln)
+    n = int(wlen)
+    assert int(ln) == n and torch.equal(out[:n], want[:n])
+    ub, un = unpack_bitstreams(out[:n], B, coder.bits_stride(), hdr)
+    assert torch.equal(un, nbits)
+    # no streams coded: every count 0, only the header
+    coder.reset()
+    coder.finish()
+    coder.pack_bits(out, hdr, ln)
+    assert int(ln) == B * hdr
+    coder.close()
