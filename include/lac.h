@@ -215,6 +215,29 @@ int lac_encoder_registers(lac_ctx *ctx, int64_t *l_host, int64_t *h_host, void *
  * count_host[streams].  Synchronises. */
 int lac_flush_digits(lac_ctx *ctx, int8_t *digits_host, int32_t *count_host, void *stream);
 
+/* Encoder checkpoint / resume.  Everything an encoder holds per stream: its registers
+ * and counters (A_to_bin's l, h and emitted bits, arith_code.py:157-163, in the O(1)
+ * renormalisation's plane form) and the output words written so far.  get copies
+ * them to the host; set restores them into a context of the same prec, vocab,
+ * streams and capacity, so a job can stop after any lac_encode call and continue
+ * later -- in this process or another -- bit for bit.  planes_host, when not NULL, is
+ * [2][streams][cap_words] uint64 (plane A, then plane C; cap_words =
+ * ceil(capacity_bits / 64)).  set refuses (LAC_E_ARG, nothing copied) register sets no
+ * encoder reaches: l outside [0, 2^(prec+1)), h < l, h - l >= 2^prec, L beyond the
+ * capacity, nflush outside [-1, 8] (streams with err set are copied as they are);
+ * get refuses a decoding context (LAC_E_STATE).
+ * Synchronise `stream`. */
+typedef struct lac_enc_state {
+    int64_t l, h;
+    uint64_t L, wa, wc;
+    int64_t nsym;
+    int32_t err, nflush;
+    int64_t err_step;
+    int8_t flush[8];
+} lac_enc_state;
+int lac_encode_get_state(lac_ctx *ctx, lac_enc_state *host_out, uint64_t *planes_host, void *stream);
+int lac_encode_set_state(lac_ctx *ctx, const lac_enc_state *host_in, const uint64_t *planes_host, void *stream);
+
 /* Start decoding: stream b reads nbits_dev[b] bits at bits_dev + b*stride_bytes
  * (bits_dev == NULL: this context's own encoded streams).  The buffers are
  * borrowed until the next lac_decode_open / lac_close.  stride_bytes must be a

@@ -34,6 +34,11 @@ def _stream_handle(device):
     return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
+# include/lac.h lac_enc_state (EncState in lac_amd/csrc/lac_core.h)
+ENC_STATE = np.dtype([("l", "<i8"), ("h", "<i8"), ("L", "<u8"), ("wa", "<u8"), ("wc", "<u8"), ("nsym", "<i8"),
+                      ("err", "<i4"), ("nflush", "<i4"), ("err_step", "<i8"), ("flush", "i1", (8,))])
+
+
 class StreamError(LacError):
     """A coder error on one or more streams (sticky, reported per stream)."""
 
@@ -212,6 +217,30 @@ class BatchCoder:
         check(self.lib.lac_encoder_registers(self.ctx, l.ctypes.data_as(C.c_void_p), h.ctypes.data_as(C.c_void_p),
                                              self._stream))
         return l, h
+
+    def checkpoint(self):
+        """Everything the encoder holds (include/lac.h lac_encode_get_state): per-stream
+        registers and counters (a numpy ENC_STATE array) and the output planes
+        ([2, streams, cap_words] uint64).  restore() continues from it bit for bit."""
+        st = np.zeros(self.streams, dtype=ENC_STATE)
+        words = self.bits_stride() // 8
+        planes = np.zeros((2, self.streams, words), dtype=np.uint64)
+        check(self.lib.lac_encode_get_state(self.ctx, st.ctypes.data_as(C.c_void_p),
+                                            planes.ctypes.data_as(C.c_void_p), self._stream))
+        return {"state": st, "planes": planes, "prec": self.prec, "vocab": self.vocab}
+
+    def restore(self, ckpt):
+        """Load a checkpoint() of a coder with the same prec, vocab, streams and capacity."""
+        st, planes = ckpt["state"], ckpt["planes"]
+        if ckpt.get("prec", self.prec) != self.prec or ckpt.get("vocab", self.vocab) != self.vocab:
+            raise ValueError("checkpoint of a coder with another prec / vocab")
+        if st.dtype != ENC_STATE or st.shape != (self.streams,):
+            raise ValueError(f"state must be ENC_STATE[{self.streams}]")
+        if planes.dtype != np.uint64 or planes.shape != (2, self.streams, self.bits_stride() // 8):
+            raise ValueError("planes of another capacity or stream count")
+        st, planes = np.ascontiguousarray(st), np.ascontiguousarray(planes)
+        check(self.lib.lac_encode_set_state(self.ctx, st.ctypes.data_as(C.c_void_p),
+                                            planes.ctypes.data_as(C.c_void_p), self._stream))
 
     def lengths(self):
         n = np.zeros(self.streams, dtype=np.uint64)

@@ -4599,6 +4599,46 @@ int lac_encoder_registers(lac_ctx *c, int64_t *l_host, int64_t *h_host, void *st
     return LAC_OK;
 }
 
+static_assert(sizeof(lac_enc_state) == sizeof(EncState) && offsetof(lac_enc_state, nflush) == offsetof(EncState, nflush) &&
+                  offsetof(lac_enc_state, flush) == offsetof(EncState, flush),
+              "lac_enc_state mirrors EncState");
+
+int lac_encode_get_state(lac_ctx *c, lac_enc_state *host_out, uint64_t *planes_host, void *stream) {
+    if (!c || !host_out) return fail(LAC_E_ARG, "NULL argument");
+    if (c->mode != 0) return fail(LAC_E_STATE, "context is decoding");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemcpyAsync(host_out, c->enc, sizeof(EncState) * c->B, hipMemcpyDeviceToHost, S(stream)));
+    if (planes_host) {
+        const size_t n = sizeof(uint64_t) * c->cap_words * c->B;
+        HIPCHK(hipMemcpyAsync(planes_host, c->planeA, n, hipMemcpyDeviceToHost, S(stream)));
+        HIPCHK(hipMemcpyAsync(planes_host + c->cap_words * c->B, c->planeC, n, hipMemcpyDeviceToHost, S(stream)));
+    }
+    HIPCHK(hipStreamSynchronize(S(stream)));
+    return LAC_OK;
+}
+
+int lac_encode_set_state(lac_ctx *c, const lac_enc_state *host_in, const uint64_t *planes_host, void *stream) {
+    if (!c || !host_in) return fail(LAC_E_ARG, "NULL argument");
+    const int64_t D = (int64_t)1 << c->prec;
+    for (int64_t b = 0; b < c->B; b++) {
+        const lac_enc_state &q = host_in[b];
+        if (q.err) continue;
+        if (q.l < 0 || q.l >= 2 * D || q.h < q.l || q.h - q.l >= D || q.L > c->cap_words * 64 || q.nsym < 0 ||
+            q.nflush < -1 || q.nflush > 8)
+            return fail(LAC_E_ARG, "stream %lld: encoder registers out of range", (long long)b);
+    }
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemcpyAsync(c->enc, host_in, sizeof(EncState) * c->B, hipMemcpyHostToDevice, S(stream)));
+    if (planes_host) {
+        const size_t n = sizeof(uint64_t) * c->cap_words * c->B;
+        HIPCHK(hipMemcpyAsync(c->planeA, planes_host, n, hipMemcpyHostToDevice, S(stream)));
+        HIPCHK(hipMemcpyAsync(c->planeC, planes_host + c->cap_words * c->B, n, hipMemcpyHostToDevice, S(stream)));
+    }
+    c->mode = 0;
+    HIPCHK(hipStreamSynchronize(S(stream)));
+    return LAC_OK;
+}
+
 int lac_flush_digits(lac_ctx *c, int8_t *digits_host, int32_t *count_host, void *stream) {
     if (!c) return fail(LAC_E_ARG, "ctx is NULL");
     HIPCHK(hipSetDevice(c->device));
