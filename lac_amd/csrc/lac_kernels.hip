@@ -47,6 +47,12 @@ using namespace lac;
 #ifndef LAC_UNROLL
 #define LAC_UNROLL 8
 #endif
+#ifndef LAC_LEAN
+#define LAC_LEAN 1          // few-stream decode: k_decode_lean ahead of k_decode_seq (probe builds set 0)
+#endif
+#ifndef LAC_LEAN_PROD
+#define LAC_LEAN_PROD 1     // k_decode_lean: chunk by products, the target division in the loads' shadow
+#endif
 #ifndef LAC_NT
 #define LAC_NT 1
 #endif
@@ -883,7 +889,10 @@ __device__ inline uint64_t read_bits(const uint8_t *bits, uint64_t nbits, uint64
 struct BitWin {
     uint64_t w0, w1;
 };
-__device__ const uint64_t g_zero_words[1] = {0};
+// (not const: a const __device__ array is placed in the constant address space, and the
+// select between it and a stream pointer then turned the window loads into flat loads,
+// which count in both vmcnt and lgkmcnt)
+__device__ uint64_t g_zero_words[1] = {0};
 __device__ inline BitWin bit_window(const uint8_t *bits, uint64_t nbits, uint64_t pos) {
     const uint64_t nw = (nbits + 63) >> 6, wi = pos >> 6;
     const uint64_t *wp = nw ? reinterpret_cast<const uint64_t *>(bits) : g_zero_words;
@@ -1846,6 +1855,15 @@ __global__ __launch_bounds__(64 * NW) void k_decode_block(const E *__restrict__ 
 // and k_decode_seq walks each stream's steps touching only those 528 bytes plus
 // the one chunk holding the target (1/64 of the row; fudged rows take
 // decode_symbol's full-row form).
+// load_vec_or0 with the default (cache-allocating) policy instead of nontemporal.
+template <typename E, int VEC>
+__device__ inline typename VecT<E, VEC>::type load_vec_keep(const E *row, int64_t vi, int64_t nvec) {
+    typedef typename VecT<E, VEC>::type Vt;
+    const bool ok = vi < nvec;
+    const Vt x = reinterpret_cast<const Vt *>(row)[ok ? vi : nvec - 1];
+    return ok ? x : (Vt)0;
+}
+
 struct DecRowMeta {
     uint64_t T;            // 0 marks a bad row (empty or total >= 2^64)
     uint64_t minp;
@@ -1862,11 +1880,34 @@ __device__ inline void dec_chunk_layout(int64_t V, int64_t *CI, int64_t *nch) {
     *nch = (nit + ci - 1) / ci;
 }
 
-template <typename E, int VEC>
+// What k_decode_lean reads of a row whose total is below 2^32 (LEAN builds of k_dec_stats):
+struct LeanMeta {
+    uint64_t T;            // the total; 0: not for the lean step (bad row, T >= 2^32, minp 0)
+    uint64_t fthr;         // ceil(T / minp): the ceil mapping's range is fudged iff w < fthr (arith_code.py:84)
+    double iT;             // recip(T)
+    uint64_t pad;
+};
+
+__device__ inline uint32_t wave_incl_scan_u32(uint32_t v) {
+    v += dpp32<kDppShr1>(v);
+    v += dpp32<kDppShr2>(v);
+    v += dpp32<kDppShr4>(v);
+    v += dpp32<kDppShr8>(v);
+    v += dpp32<kDppBcast15, 0xA>(v);
+    v += dpp32<kDppBcast31, 0xC>(v);
+    return v;
+}
+
+// LEAN: also the row's vector-granular CDF for k_decode_lean -- vpre[row][v], the sum of
+// the row's entries before vector v (mod 2^32) -- its chunks' bounds lchunk[row][lane]
+// (exclusive | inclusive << 32) and a LeanMeta; exact where the total is below 2^32.
+template <typename E, int VEC, bool LEAN = false>
 __global__ __launch_bounds__(256) void k_dec_stats(const E *__restrict__ pmf, int64_t step_stride,
                                                    int64_t stream_stride, int64_t B, int64_t rows, int64_t V,
                                                    int64_t t0, uint64_t *__restrict__ chunks,
-                                                   DecRowMeta *__restrict__ meta) {
+                                                   DecRowMeta *__restrict__ meta, uint32_t *__restrict__ vpre = nullptr,
+                                                   uint64_t *__restrict__ lchunk = nullptr,
+                                                   LeanMeta *__restrict__ lmeta = nullptr) {
     const int lane = (int)lane_id();
     const int64_t r = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
     if (r >= rows) return;
@@ -1881,6 +1922,8 @@ __global__ __launch_bounds__(256) void k_dec_stats(const E *__restrict__ pmf, in
     // groups of 8 iterations (8 loads in flight per lane), their 8 totals from one
     // butterfly, each added into the lane of its chunk (chunk = iteration / CI)
     int64_t chunk = 0, left = CI;
+    uint32_t run = 0;                                          // LEAN: the row's sum so far, mod 2^32
+    uint32_t *vp = LEAN ? vpre + r * nvec : nullptr;
     for (int64_t g = 0; g < ngrp; g++) {
         typename VecT<E, VEC>::type x[8];
 #pragma unroll
@@ -1898,6 +1941,15 @@ __global__ __launch_bounds__(256) void k_dec_stats(const E *__restrict__ pmf, in
             }
             s8[u] = a;
         }
+        if constexpr (LEAN) {
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int64_t vi = (g * 8 + u) * 64 + lane;
+                const uint32_t in = wave_incl_scan_u32((uint32_t)s8[u]);
+                if (vi < nvec) vp[vi] = run + in - (uint32_t)s8[u];
+                run += (uint32_t)__builtin_amdgcn_readlane((int)in, 63);
+            }
+        }
         const uint64_t tot = wave_sum8_u64<W>(s8, ovf);       // lane l: iteration g*8 + (l & 7)
 #pragma unroll
         for (int u = 0; u < 8; u++) {
@@ -1914,6 +1966,14 @@ __global__ __launch_bounds__(256) void k_dec_stats(const E *__restrict__ pmf, in
     const bool bad = __any(ovf) || (acc128 >> 64) || acc128 == 0;
     chunks[r * 64 + lane] = mine;
     if (lane == 0) meta[r] = DecRowMeta{bad ? 0 : (uint64_t)acc128, minp};
+    if constexpr (LEAN) {
+        const uint32_t in = wave_incl_scan_u32((uint32_t)mine);
+        lchunk[r * 64 + lane] = (uint64_t)(in - (uint32_t)mine) | ((uint64_t)in << 32);
+        const uint64_t T = (uint64_t)acc128;
+        const bool ok = !bad && T < (1ull << 32) && minp != 0;
+        if (lane == 0)
+            lmeta[r] = LeanMeta{ok ? T : 0, ok ? (T + minp - 1) / minp : 0, recip(ok ? T : 1), 0};
+    }
 }
 
 template <typename E, int VEC>
@@ -1924,7 +1984,8 @@ __global__ __launch_bounds__(256) void k_decode_seq(const E *__restrict__ pmf, i
                                             const uint64_t *__restrict__ chunks,
                                             const DecRowMeta *__restrict__ meta, DecState *states,
                                             const uint8_t *bits, uint64_t stride, const uint64_t *nbits,
-                                            int32_t *sym_out, int64_t B, int mapping) {
+                                            int32_t *sym_out, int64_t B, int mapping,
+                                            const int64_t *__restrict__ resume = nullptr) {
     const int lane = (int)lane_id();
     // the stream index and its decoder state wave-uniform (SGPRs): the serial chain --
     // the targets, the ranges, the renormalisation -- then runs on the scalar unit
@@ -1937,15 +1998,18 @@ __global__ __launch_bounds__(256) void k_decode_seq(const E *__restrict__ pmf, i
     const uint64_t mynbits = nbits[b];
     int64_t CI, nch;
     dec_chunk_layout<E, VEC>(V, &CI, &nch);
-    uint64_t next = nsteps > 0 ? chunks[b * 64 + lane] : 0;
-    DecRowMeta nmeta = nsteps > 0 ? meta[b] : DecRowMeta{0, 0};
+    // after k_decode_lean: its steps are done, continue from the first it left
+    const int64_t i0 = resume ? (int64_t)rfl_u64((uint64_t)(resume[b] - t0)) : 0;
+    if (i0 >= nsteps) return;
+    uint64_t next = chunks[(i0 * B + b) * 64 + lane];
+    DecRowMeta nmeta = meta[i0 * B + b];
 #if LAC_DEC_PHASES
     PhaseClock clock, *clk = &clock;
     clock.start();
 #else
     NoClock *clk = nullptr;
 #endif
-    for (int64_t i = 0; i < nsteps; i++) {
+    for (int64_t i = i0; i < nsteps; i++) {
         dec_state_uniform(st);                                 // (the loop's phis are not seen as uniform)
         const int64_t t = t0 + i;
         const uint64_t mine = next;
@@ -1992,6 +2056,181 @@ __global__ __launch_bounds__(256) void k_decode_seq(const E *__restrict__ pmf, i
         atomicAdd(&g_dec_phase[6], (unsigned long long)nsteps);
     }
 #endif
+}
+
+// ---- lean few-stream decode step (stats path, prec <= 50, row totals < 2^32)
+// k_decode_seq's serial step for what few-stream decodes nearly always are -- u32-scale
+// rows (totals below 2^32), an unfudged range (or the floor mapping), prec <= 50 -- laid
+// out for the latency of one wave, whose instructions issue in order.  Everything that
+// depends on the row alone comes precomputed from k_dec_stats<..., LEAN>: the chunk
+// bounds, T's reciprocal, the fudge threshold ceil(T/minp) and the vector-granular CDF
+// vpre, loaded two steps ahead.  Left on the chain: a ballot over the chunk bounds,
+// compared with the target floor(v*T/w) as products (ex*w <= v*T < in*w, no division),
+// one round of loads (the chunk's entries and their vpre) with the target's division
+// in its shadow, the iteration holding the target by its first vpre, a ballot over the
+// lanes' cumulative sums -- no wave scan -- the two ranges and the renormalisation.  Symbols
+// collect one per lane and leave in one store per 64 steps.
+// Results are k_decode_seq's.  A step outside the case (a bad, large or fudged row, an
+// inconsistent state or stream) ends this kernel for its stream before the step changes
+// anything: resume[b] holds the step and k_decode_seq continues from it, raising the
+// error if there is one.  One wave per workgroup: streams spread over the XCDs.
+template <typename E, int VEC, int CIM>
+__global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ pmf, int64_t step_stride,
+                                                    int64_t stream_stride, int64_t t0, int64_t nsteps, int64_t V,
+                                                    int prec, const uint32_t *__restrict__ vpre,
+                                                    const uint64_t *__restrict__ lchunk,
+                                                    const LeanMeta *__restrict__ lmeta, DecState *states,
+                                                    const uint8_t *bits, uint64_t stride, const uint64_t *nbits,
+                                                    int32_t *sym_out, int64_t B, int mapping,
+                                                    int64_t *__restrict__ resume) {
+    typedef typename VecT<E, VEC>::type Vt;
+    const int lane = (int)lane_id();
+    const int64_t b = blockIdx.x;
+    if (b >= B) return;
+    DecState st = states[b];
+    dec_state_uniform(st);
+    const uint8_t *mybits = bits + b * stride;
+    const uint64_t mynbits = rfl_u64(nbits[b]);
+    int64_t CI, nch;
+    dec_chunk_layout<E, VEC>(V, &CI, &nch);
+    const int64_t nvec = V / VEC;
+    const bool ceil_map = mapping != LAC_MAP_FLOOR;
+    uint64_t cw = 0, cw1 = 0;                                   // lane's chunk bounds, steps i and i+1
+    LeanMeta lm{0, 0, 1.0, 0}, lm1{0, 0, 1.0, 0};
+    if (nsteps > 0) { cw = lchunk[b * 64 + lane]; lm = lmeta[b]; }
+    if (nsteps > 1) { cw1 = lchunk[(B + b) * 64 + lane]; lm1 = lmeta[B + b]; }
+    // running pointers (rows of this launch are r = i*B + b): row i, its vpre, row i+2's bounds
+    const E *rowp = pmf + t0 * step_stride + b * stream_stride;
+    const uint32_t *prp = vpre + b * nvec;
+    const uint64_t *lcp = lchunk + (2 * B + b) * 64 + lane;
+    const LeanMeta *lmp = lmeta + 2 * B + b;
+    const int64_t pr_step = B * nvec;
+    int32_t sbuf = -1;
+    int64_t i = 0;
+#if LAC_DEC_PHASES
+    PhaseClock clk;
+    clk.start();
+#else
+    NoClock clk;
+#endif
+    if (!st.err) {
+        for (; i < nsteps; i++) {
+            dec_state_uniform(st);
+            const uint64_t T = rfl_u64(lm.T), fthr = rfl_u64(lm.fthr);
+            const double iT = lm.iT;
+            const uint64_t cwi = cw;
+            cw = cw1;
+            lm = lm1;
+            if (i + 2 < nsteps) {                               // row i+2
+                cw1 = *lcp;
+                lm1 = *lmp;
+            }
+            lcp += B * 64;
+            lmp += B;
+            const E *row = rowp;
+            const uint32_t *pr = prp;
+            rowp += step_stride;
+            prp += pr_step;
+            const int64_t l = st.l, h = st.h, x = st.x;
+            const uint64_t w = (uint64_t)(h - l + 1), v = (uint64_t)(x - l);
+            if (T == 0 || x < l || x > h || (ceil_map && w < fthr)) break;
+            const BitWin win = bit_window(mybits, mynbits, st.pos);
+            clk.mark(0);
+#if LAC_LEAN_PROD
+            // the chunk holding tgt = floor(v*T/w) without the division: ex <= tgt < in
+            // iff ex*w <= v*T < in*w, products below 2^83 as (bits 32.., bits 0..31)
+            const uint64_t pl = (v & 0xffffffffull) * T, ph = (v >> 32) * T + (pl >> 32);
+            const uint32_t plo = (uint32_t)pl;
+            const uint32_t wl = (uint32_t)w, wh = (uint32_t)(w >> 32);
+            auto le_p = [&](uint32_t e) {                       // e*w <= v*T (no short circuits: no branches)
+                const uint64_t q0 = (uint64_t)e * wl, qh = (uint64_t)e * wh + (q0 >> 32);
+                return (qh < ph) | ((qh == ph) & ((uint32_t)q0 <= plo));
+            };
+            const uint64_t cm = __ballot((lane < nch) & le_p((uint32_t)cwi) & !le_p((uint32_t)(cwi >> 32)));
+#else
+            const uint64_t tgt = div_small_u(v, T, 0, w, recip(w));   // < T < 2^32
+            const uint32_t t32 = (uint32_t)tgt;
+            const uint64_t cm = __ballot((lane < nch) & ((uint32_t)cwi <= t32) & (t32 < (uint32_t)(cwi >> 32)));
+#endif
+            if (!cm) break;
+            const int64_t cv0 = (int64_t)(__ffsll((unsigned long long)cm) - 1) * CI * 64;
+            Vt xs[CIM];
+            uint32_t ps[CIM];
+#pragma unroll
+            for (int g = 0; g < CIM; g++) {
+                const int64_t vi = cv0 + g * 64 + lane, vc = vi < nvec ? vi : nvec - 1;
+                xs[g] = reinterpret_cast<const Vt *>(row)[vc];
+                ps[g] = pr[vc];
+            }
+#if LAC_LEAN_PROD
+            __builtin_amdgcn_sched_barrier(0);                   // the division below, after the loads
+            const uint64_t tgt = div_small_u(v, T, 0, w, recip(w));   // < T < 2^32
+            const uint32_t t32 = (uint32_t)tgt;
+#endif
+            clk.mark(1);
+            // in the loads' shadow: the 1-padded end's target
+            const uint64_t past = st.pos > mynbits ? st.pos - mynbits : 0;
+            const int u = past < (uint64_t)prec ? (int)past : prec;
+            const uint64_t vhi = v + ((1ull << u) - 1);
+            const uint64_t thi = vhi == v ? tgt : (vhi < w ? div_small_u(vhi, T, 0, w, recip(w)) : 0);
+            clk.mark(2);
+            // the iteration holding the target: the last whose first vector starts at or below it
+            int gs = 0;
+#pragma unroll
+            for (int g = 1; g < CIM; g++)
+                if (cv0 + g * 64 < nvec && (uint32_t)__builtin_amdgcn_readfirstlane((int)ps[g]) <= t32) gs = g;
+            Vt xg = xs[0];
+            uint32_t pg = ps[0];
+#pragma unroll
+            for (int g = 1; g < CIM; g++) {
+                xg = gs == g ? xs[g] : xg;
+                pg = gs == g ? ps[g] : pg;
+            }
+            const bool real = cv0 + gs * 64 + lane < nvec;
+            uint32_t c[VEC];
+            uint32_t acc = pg;
+#pragma unroll
+            for (int j = 0; j < VEC; j++) { acc += real ? (uint32_t)vget<E, VEC>(xg, j) : 0u; c[j] = acc; }
+            const uint64_t m2 = __ballot(real & (c[VEC - 1] > t32));
+            if (!m2) break;
+            const int L = __ffsll((unsigned long long)m2) - 1;
+            uint32_t k = 0, lo = pg, hi = c[VEC - 1];
+#pragma unroll
+            for (int j = VEC - 1; j >= 0; j--) {
+                const bool le = c[j] <= t32;
+                k += le ? 1 : 0;
+                hi = le ? hi : c[j];
+            }
+#pragma unroll
+            for (int j = 0; j < VEC; j++) lo = c[j] <= t32 ? c[j] : lo;
+            const uint64_t lo_c = (uint32_t)__builtin_amdgcn_readlane((int)lo, L);
+            const uint64_t hi_c = (uint32_t)__builtin_amdgcn_readlane((int)hi, L);
+            const int64_t s = (cv0 + gs * 64 + L) * VEC + (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)k, L);
+            clk.mark(3);
+            uint64_t a, bb;
+            div_small_u2(lo_c, hi_c, w, ceil_map ? T - 1 : 0, T, iT, &a, &bb);
+            if (!((l + (int64_t)a) <= x && x <= l + (int64_t)bb - 1)) break;
+            clk.mark(4);
+            const bool det = vhi < w && thi < hi_c;
+            if (st.det && det) st.ndet++;
+            else st.det = 0;
+            decode_advance<true>(st, a, bb, win, mynbits, prec);
+            if (lane == (int)(i & 63)) sbuf = (int32_t)s;
+            if ((i & 63) == 63) sym_out[(t0 + i - 63 + lane) * B + b] = sbuf;
+            clk.mark(5);
+        }
+    }
+#if LAC_DEC_PHASES
+    if (lane == 0) {
+        for (int k = 0; k < 6; k++) atomicAdd(&g_dec_phase[k], (unsigned long long)clk.acc[k]);
+        atomicAdd(&g_dec_phase[6], (unsigned long long)i);
+    }
+#endif
+    if (lane < (int)(i & 63)) sym_out[(t0 + (i & ~(int64_t)63) + lane) * B + b] = sbuf;
+    if (lane == 0) {
+        states[b] = st;
+        resume[b] = t0 + i;
+    }
 }
 
 // ================================================================ q1 logits path
@@ -3652,6 +3891,11 @@ struct lac_ctx {
     int q1_shape = 0;                   // logits stats block shape (0 auto; lac_set_option tuning)
     uint64_t *q1chunks = nullptr;       // logits / stats-path decode: [chunk_steps * B][64] chunk totals
     void *dmeta = nullptr;              // stats-path decode: [chunk_steps * B] DecRowMeta
+    int64_t *dresume = nullptr;         //                    [B] first step k_decode_lean left
+    void *lvpre = nullptr;              // lean decode: [lean_steps * B][V / VEC] uint32 vector CDF
+    uint64_t *lchunk = nullptr;         //              [lean_steps * B][64] chunk bounds
+    void *lmeta = nullptr;              //              [lean_steps * B] LeanMeta
+    int64_t lean_steps = 0;             //              steps per launch the buffers hold
     float *q1m = nullptr;               //                [chunk_steps * B] row maxima
     uint64_t *pxch = nullptr;           // paired row stats (shape 19): [2 * cus] maximum words
     uint64_t *pack_off = nullptr;       // lac_pack_bits: [B] byte offsets of the streams
@@ -3845,16 +4089,62 @@ static int decode_stats_path(lac_ctx *c, const E *pmf, int64_t step_stride, int6
     int rc = ensure_chunk_buffers(c);
     if (rc) return rc;
     const unsigned blocks = (unsigned)((c->B + kWavesPerBlock - 1) / kWavesPerBlock);
-    for (int64_t t0 = 0; t0 < steps; t0 += c->chunk_steps) {
-        const int64_t n = (steps - t0) < c->chunk_steps ? (steps - t0) : c->chunk_steps;
+    // k_decode_lean: u32 tables, prec <= 50, chunks of at most 4 iterations (V <= 65536); its
+    // buffers hold up to 64 MB of vector CDFs, so its launches take at most that many steps
+    const int64_t nvec = c->V / VEC, nit = (nvec + 63) / 64;
+    const int64_t CI = nit ? (nit + 63) / 64 : 1;
+    const bool lean = LAC_LEAN && sizeof(E) == 4 && c->prec <= 50 && CI <= 4 && nvec > 0;   // (u64 tables: totals >= 2^32)
+    int64_t cs = c->chunk_steps;
+    if (lean) {
+        const int64_t per = c->B * nvec * (int64_t)sizeof(uint32_t);
+        const int64_t fit = ((int64_t)64 << 20) / per;
+        const int64_t ls = fit < 64 ? 64 : fit / 64 * 64;
+        cs = ls < cs ? ls : cs;
+        if (c->lean_steps < cs) {
+            (void)hipFree(c->lvpre);
+            (void)hipFree(c->lchunk);
+            (void)hipFree(c->lmeta);
+            c->lvpre = nullptr;
+            c->lchunk = nullptr;
+            c->lmeta = nullptr;
+            c->lean_steps = 0;
+            HIPCHK(hipMalloc(&c->lvpre, sizeof(uint32_t) * cs * c->B * nvec));
+            HIPCHK(hipMalloc(&c->lchunk, sizeof(uint64_t) * 64 * cs * c->B));
+            HIPCHK(hipMalloc(&c->lmeta, sizeof(LeanMeta) * cs * c->B));
+            c->lean_steps = cs;
+        }
+        if (!c->dresume) HIPCHK(hipMalloc(&c->dresume, sizeof(int64_t) * c->B));
+    }
+    for (int64_t t0 = 0; t0 < steps; t0 += cs) {
+        const int64_t n = (steps - t0) < cs ? (steps - t0) : cs;
         const int64_t rows = n * c->B;
         ProfScope ps(c, KID_DECODE, st);
-        k_dec_stats<E, VEC><<<(unsigned)((rows + kWavesPerBlock - 1) / kWavesPerBlock), 64 * kWavesPerBlock, 0, st>>>(
-            pmf, step_stride, stream_stride, c->B, rows, c->V, t0, c->q1chunks, (DecRowMeta *)c->dmeta);
-        CHECK_LAUNCH();
+        const unsigned sblocks = (unsigned)((rows + kWavesPerBlock - 1) / kWavesPerBlock);
+        if (lean) {
+            k_dec_stats<E, VEC, true><<<sblocks, 64 * kWavesPerBlock, 0, st>>>(
+                pmf, step_stride, stream_stride, c->B, rows, c->V, t0, c->q1chunks, (DecRowMeta *)c->dmeta,
+                (uint32_t *)c->lvpre, c->lchunk, (LeanMeta *)c->lmeta);
+            CHECK_LAUNCH();
+#define LAC_LEAN_K(CIM)                                                                                          \
+    k_decode_lean<E, VEC, CIM><<<(unsigned)c->B, 64, 0, st>>>(                                                 \
+        pmf, step_stride, stream_stride, t0, n, c->V, c->prec, (const uint32_t *)c->lvpre, c->lchunk,          \
+        (const LeanMeta *)c->lmeta, c->dec, c->dbits, c->dstride, c->dnbits, out, c->B, c->mapping, c->dresume)
+            switch (CI) {
+            case 1: LAC_LEAN_K(1); break;
+            case 2: LAC_LEAN_K(2); break;
+            case 3: LAC_LEAN_K(3); break;
+            default: LAC_LEAN_K(4); break;
+            }
+#undef LAC_LEAN_K
+            CHECK_LAUNCH();
+        } else {
+            k_dec_stats<E, VEC><<<sblocks, 64 * kWavesPerBlock, 0, st>>>(
+                pmf, step_stride, stream_stride, c->B, rows, c->V, t0, c->q1chunks, (DecRowMeta *)c->dmeta);
+            CHECK_LAUNCH();
+        }
         k_decode_seq<E, VEC><<<blocks, 64 * kWavesPerBlock, 0, st>>>(
             pmf, step_stride, stream_stride, t0, n, c->V, c->prec, c->q1chunks, (const DecRowMeta *)c->dmeta, c->dec,
-            c->dbits, c->dstride, c->dnbits, out, c->B, c->mapping);
+            c->dbits, c->dstride, c->dnbits, out, c->B, c->mapping, lean ? c->dresume : nullptr);
         CHECK_LAUNCH();
     }
     return LAC_OK;
@@ -4414,6 +4704,10 @@ int lac_close(lac_ctx *c) {
     (void)hipFree(c->nbits);
     (void)hipFree(c->q1chunks);
     (void)hipFree(c->dmeta);
+    (void)hipFree(c->dresume);
+    (void)hipFree(c->lvpre);
+    (void)hipFree(c->lchunk);
+    (void)hipFree(c->lmeta);
     (void)hipFree(c->q1m);
     (void)hipFree(c->pxch);
     (void)hipFree(c->pack_off);

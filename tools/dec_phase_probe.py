@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--vocab", type=int, default=32000)
     ap.add_argument("--tokens", type=int, default=4096)
     ap.add_argument("--streams", type=int, default=1)
+    ap.add_argument("--kernel", default="lean", choices=("lean", "seq"),
+                    help="which sequential kernel the probe library runs (seq: a -DLAC_LEAN=0 build)")
     a = ap.parse_args()
     import torch
     from lac_amd import synth
@@ -56,7 +58,9 @@ def main():
         lib.lac_profile_read(coder.ctx, C.cast(ms, C.c_void_p), C.cast(cnt, C.c_void_p), 1)
         lib.lac_debug_dec_phases(C.cast(out, C.c_void_p), 1)
         steps = max(int(out[6]), 1)
-        names = ["totals+scan", "targets", "chunk_search", "reread+scan", "ranges", "renorm"]
+        names = (["top+window", "target+ballot+load_issue", "shadow(thi,next_row)", "wait+scan+select", "ranges",
+                  "advance+output"] if a.kernel == "lean" else
+                 ["totals+scan", "targets", "chunk_search", "reread+scan", "ranges", "renorm"])
         cyc = {n: out[k] / steps for k, n in enumerate(names)}
         res = {"rep": rep, "steps": steps, "cycles_per_step": cyc, "cycles_total_per_step": sum(cyc.values()),
                "kernel_us_per_step": {"decode (stats + seq)": 1e3 * ms[3] / max(T, 1)},
