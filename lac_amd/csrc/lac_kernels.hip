@@ -50,8 +50,8 @@ using namespace lac;
 #ifndef LAC_LEAN
 #define LAC_LEAN 1          // few-stream decode: k_decode_lean ahead of k_decode_seq (probe builds set 0)
 #endif
-#ifndef LAC_LEAN_PROD
-#define LAC_LEAN_PROD 1     // k_decode_lean: chunk by products, the target division in the loads' shadow
+#ifndef LAC_LEAN_HELP
+#define LAC_LEAN_HELP 1     // k_decode_lean: L2-prefetching helper workgroups for <= 16 streams
 #endif
 #ifndef LAC_NT
 #define LAC_NT 1
@@ -1155,18 +1155,36 @@ struct PhaseClock {
 __device__ unsigned long long g_dec_phase[8];
 #endif
 
+// r < 0 for a wave-uniform int64.  (Forcing the test onto the scalar unit -- the high
+// word's sign through an opaque SGPR -- measured slower in both sequential decoders,
+// c2 1.29 -> 1.43 us/step, profiles/r04/lean/: the vector compare it replaces overlaps.)
+__device__ inline bool neg_u(uint64_t r) { return (int64_t)r < 0; }
+
+// div_small_fix for wave-uniform values (|r| < 3d < 2^53).
+__device__ inline uint64_t div_small_fix_u(uint64_t q, uint64_t n, uint64_t m, uint64_t add, uint64_t d) {
+    uint64_t r = n * m + add - q * d;
+    while (neg_u(r)) { q -= 1; r += d; }
+    for (;;) {
+        const uint64_t t = r - d;
+        if (neg_u(t)) break;
+        q += 1;
+        r = t;
+    }
+    return q;
+}
+
 // div_small with wave-uniform arguments: the double estimate on the vector unit (the
 // SALU has no FP64), read back, the 64-bit remainder and its corrections on the SALU.
 __device__ inline uint64_t div_small_u(uint64_t n, uint64_t m, uint64_t add, uint64_t d, double inv) {
-    return div_small_fix(rfl_u64(div_small_est(n, m, add, inv)), n, m, add, d);
+    return div_small_fix_u(rfl_u64(div_small_est(n, m, add, inv)), n, m, add, d);
 }
 // Two of them with one divisor (the ranges ceil(lo*w/T), ceil(hi*w/T)): both estimates
 // first, so the two FP64 chains overlap, then both corrections.
 __device__ inline void div_small_u2(uint64_t n0, uint64_t n1, uint64_t m, uint64_t add, uint64_t d, double inv,
                                     uint64_t *q0, uint64_t *q1) {
     const uint64_t e0 = rfl_u64(div_small_est(n0, m, add, inv)), e1 = rfl_u64(div_small_est(n1, m, add, inv));
-    *q0 = div_small_fix(e0, n0, m, add, d);
-    *q1 = div_small_fix(e1, n1, m, add, d);
+    *q0 = div_small_fix_u(e0, n0, m, add, d);
+    *q1 = div_small_fix_u(e1, n1, m, add, d);
 }
 
 // Everything after the row's totals are known: val_to_symbol + symbol_to_range
@@ -2074,6 +2092,61 @@ __global__ __launch_bounds__(256) void k_decode_seq(const E *__restrict__ pmf, i
 // inconsistent state or stream) ends this kernel for its stream before the step changes
 // anything: resume[b] holds the step and k_decode_seq continues from it, raising the
 // error if there is one.  One wave per workgroup: streams spread over the XCDs.
+// Few-stream lean decode: the re-read of step i's chunk is one dependent load per step,
+// an HBM round trip when the row is cold.  Helper waves -- workgroups of the same launch
+// placed on the decoding wave's XCD (workgroups are dealt to the 8 XCDs round-robin, so
+// index = stream mod 8) -- read one dword of every 128-B line of the rows (and vpre rows)
+// a few steps ahead of the decoder, which then finds its chunk in that XCD's L2.  They
+// only read: the values are discarded (an empty asm consumes them so the loads stay).
+// They pace themselves by the decoder's progress (a relaxed agent-scope counter it sets
+// every 8 steps), never the other way round: results do not depend on them, and a
+// helper that sees no progress for ~10 ms gives up, so the grid always drains.
+constexpr int kLeanAhead = 8;                   // rows prefetched ahead of the decoder
+constexpr int kLeanHelpers = 16;                // helper waves per stream
+constexpr int kLeanHelpMaxStreams = 16;         // above: no helpers (L2: ~1.3 MB ahead per stream)
+
+__device__ inline int32_t lean_progress(const int32_t *p) {
+    return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+__device__ inline void lean_touch(const uint8_t *base, int64_t bytes) {
+    // one dword of every 128-B line of [base, base + bytes), 16 loads in flight per lane
+    if (bytes < 4) return;
+    const int64_t lines = (bytes - 4) / 128 + 1;
+    for (int64_t l0 = 0; l0 < lines; l0 += 16 * 64) {
+        uint32_t v[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++) {
+            const int64_t ln = l0 + u * 64 + (int64_t)lane_id(), lc = ln < lines ? ln : lines - 1;
+            v[u] = *reinterpret_cast<const uint32_t *>(base + lc * 128);
+        }
+#pragma unroll
+        for (int u = 0; u < 16; u++) asm volatile("" ::"v"(v[u]));   // (prefetch only: the value is unused)
+    }
+}
+
+template <typename E>
+__device__ void lean_helper(const E *pmf, int64_t step_stride, int64_t stream_stride, int64_t t0, int32_t n32,
+                            int64_t V, const uint32_t *vpre, int32_t nv32, int64_t B, int64_t B8,
+                            const int32_t *progress) {
+    const int64_t hidx = (int64_t)blockIdx.x - B8;
+    const int64_t b = hidx % B8, k = hidx / B8;                 // stream (same XCD: B8 % 8 == 0), helper
+    if (b >= B || k >= kLeanHelpers) return;
+    int32_t seen = 0;
+    for (int32_t t = (int32_t)k; t < n32; t += kLeanHelpers) {
+        int64_t idle = 0;
+        while (seen + kLeanAhead < t) {
+            seen = lean_progress(progress + b);
+            if (seen + kLeanAhead >= t) break;
+            if (++idle > (1 << 17)) return;                      // ~10 ms without progress
+            __builtin_amdgcn_s_sleep(2);
+        }
+        lean_touch(reinterpret_cast<const uint8_t *>(pmf + (t0 + t) * step_stride + b * stream_stride),
+                   V * (int64_t)sizeof(E));
+        lean_touch(reinterpret_cast<const uint8_t *>(vpre + ((int64_t)t * B + b) * nv32), (int64_t)nv32 * 4);
+    }
+}
+
 template <typename E, int VEC, int CIM>
 __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ pmf, int64_t step_stride,
                                                     int64_t stream_stride, int64_t t0, int64_t nsteps, int64_t V,
@@ -2082,9 +2155,16 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ pmf, i
                                                     const LeanMeta *__restrict__ lmeta, DecState *states,
                                                     const uint8_t *bits, uint64_t stride, const uint64_t *nbits,
                                                     int32_t *sym_out, int64_t B, int mapping,
-                                                    int64_t *__restrict__ resume) {
+                                                    int64_t *__restrict__ resume, int32_t *progress) {
     typedef typename VecT<E, VEC>::type Vt;
     const int lane = (int)lane_id();
+    const int64_t B8 = (B + 7) & ~(int64_t)7;
+    if ((int64_t)blockIdx.x >= B8) {                             // a helper workgroup
+        if (progress)
+            lean_helper<E>(pmf, step_stride, stream_stride, t0, (int32_t)nsteps, V, vpre, (int32_t)(V / VEC), B, B8,
+                           progress);
+        return;
+    }
     const int64_t b = blockIdx.x;
     if (b >= B) return;
     DecState st = states[b];
@@ -2093,20 +2173,30 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ pmf, i
     const uint64_t mynbits = rfl_u64(nbits[b]);
     int64_t CI, nch;
     dec_chunk_layout<E, VEC>(V, &CI, &nch);
-    const int64_t nvec = V / VEC;
+    const int32_t nv32 = (int32_t)(V / VEC);                    // (<= 16384: CI <= 4)
+    const uint32_t ci64 = (uint32_t)CI * 64;
+    const int32_t nch32 = (int32_t)nch;
     const bool ceil_map = mapping != LAC_MAP_FLOOR;
-    uint64_t cw = 0, cw1 = 0;                                   // lane's chunk bounds, steps i and i+1
+    const int32_t n32 = (int32_t)nsteps;                        // (<= chunk_steps)
+    // row data two steps ahead: the lane's chunk bounds (per-lane pointer) and the LeanMeta
+    // (by index, a scalar load); running pointers to row i and its vpre
+    uint64_t cw = 0, cw1 = 0;
     LeanMeta lm{0, 0, 1.0, 0}, lm1{0, 0, 1.0, 0};
-    if (nsteps > 0) { cw = lchunk[b * 64 + lane]; lm = lmeta[b]; }
-    if (nsteps > 1) { cw1 = lchunk[(B + b) * 64 + lane]; lm1 = lmeta[B + b]; }
-    // running pointers (rows of this launch are r = i*B + b): row i, its vpre, row i+2's bounds
+    if (n32 > 0) { cw = lchunk[b * 64 + lane]; lm = lmeta[b]; }
+    if (n32 > 1) { cw1 = lchunk[(B + b) * 64 + lane]; lm1 = lmeta[B + b]; }
+    const uint64_t *lcv = lchunk + (2 * B + b) * 64 + lane;
+    int32_t li = (int32_t)(2 * B + b);
+    const int32_t B32 = (int32_t)B;
     const E *rowp = pmf + t0 * step_stride + b * stream_stride;
-    const uint32_t *prp = vpre + b * nvec;
-    const uint64_t *lcp = lchunk + (2 * B + b) * 64 + lane;
-    const LeanMeta *lmp = lmeta + 2 * B + b;
-    const int64_t pr_step = B * nvec;
+    const uint32_t *prp = vpre + b * (int64_t)nv32;
+    const int64_t pr_step = B * (int64_t)nv32;
+    int32_t *outv = sym_out + (t0 + lane) * B + b;              // lane j: step 64k + j
+    // the registers as locals (SGPRs); the counters are settled after the loop
+    int64_t l = st.l, h = st.h, x = st.x;
+    uint64_t pos = st.pos;
+    int32_t firstnd = -1;                                       // first step not determined
     int32_t sbuf = -1;
-    int64_t i = 0;
+    int32_t i = 0;
 #if LAC_DEC_PHASES
     PhaseClock clk;
     clk.start();
@@ -2114,29 +2204,28 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ pmf, i
     NoClock clk;
 #endif
     if (!st.err) {
-        for (; i < nsteps; i++) {
-            dec_state_uniform(st);
+        for (; i < n32; i++) {
+            l = (int64_t)rfl_u64((uint64_t)l);                  // (the loop's phis are not seen as uniform)
+            h = (int64_t)rfl_u64((uint64_t)h);
+            x = (int64_t)rfl_u64((uint64_t)x);
+            pos = rfl_u64(pos);
             const uint64_t T = rfl_u64(lm.T), fthr = rfl_u64(lm.fthr);
             const double iT = lm.iT;
             const uint64_t cwi = cw;
             cw = cw1;
             lm = lm1;
-            if (i + 2 < nsteps) {                               // row i+2
-                cw1 = *lcp;
-                lm1 = *lmp;
+            if (i + 2 < n32) {                                  // row i+2
+                cw1 = *lcv;
+                lm1 = lmeta[li];
             }
-            lcp += B * 64;
-            lmp += B;
+            lcv += (int64_t)B32 * 64;
+            li += B32;
             const E *row = rowp;
             const uint32_t *pr = prp;
             rowp += step_stride;
             prp += pr_step;
-            const int64_t l = st.l, h = st.h, x = st.x;
             const uint64_t w = (uint64_t)(h - l + 1), v = (uint64_t)(x - l);
-            if (T == 0 || x < l || x > h || (ceil_map && w < fthr)) break;
-            const BitWin win = bit_window(mybits, mynbits, st.pos);
             clk.mark(0);
-#if LAC_LEAN_PROD
             // the chunk holding tgt = floor(v*T/w) without the division: ex <= tgt < in
             // iff ex*w <= v*T < in*w, products below 2^83 as (bits 32.., bits 0..31)
             const uint64_t pl = (v & 0xffffffffull) * T, ph = (v >> 32) * T + (pl >> 32);
@@ -2146,39 +2235,43 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ pmf, i
                 const uint64_t q0 = (uint64_t)e * wl, qh = (uint64_t)e * wh + (q0 >> 32);
                 return (qh < ph) | ((qh == ph) & ((uint32_t)q0 <= plo));
             };
-            const uint64_t cm = __ballot((lane < nch) & le_p((uint32_t)cwi) & !le_p((uint32_t)(cwi >> 32)));
-#else
-            const uint64_t tgt = div_small_u(v, T, 0, w, recip(w));   // < T < 2^32
-            const uint32_t t32 = (uint32_t)tgt;
-            const uint64_t cm = __ballot((lane < nch) & ((uint32_t)cwi <= t32) & (t32 < (uint32_t)(cwi >> 32)));
-#endif
-            if (!cm) break;
-            const int64_t cv0 = (int64_t)(__ffsll((unsigned long long)cm) - 1) * CI * 64;
+            const uint64_t cm = __ballot((lane < nch32) & le_p((uint32_t)cwi) & !le_p((uint32_t)(cwi >> 32)));
+            // the chunk's loads first (in bounds whatever the step: refused below if it is bad),
+            // then the stream window, then everything that can wait for them
+            const uint32_t src = cm ? (uint32_t)(__ffsll((unsigned long long)cm) - 1) : 0u;
+            const int32_t cv0 = (int32_t)(src * ci64);
             Vt xs[CIM];
             uint32_t ps[CIM];
 #pragma unroll
             for (int g = 0; g < CIM; g++) {
-                const int64_t vi = cv0 + g * 64 + lane, vc = vi < nvec ? vi : nvec - 1;
+                const int32_t vi = cv0 + g * 64 + lane, vc = vi < nv32 ? vi : nv32 - 1;
                 xs[g] = reinterpret_cast<const Vt *>(row)[vc];
                 ps[g] = pr[vc];
             }
-#if LAC_LEAN_PROD
-            __builtin_amdgcn_sched_barrier(0);                   // the division below, after the loads
-            const uint64_t tgt = div_small_u(v, T, 0, w, recip(w));   // < T < 2^32
+            const BitWin win = bit_window(mybits, mynbits, pos);
+            if (progress && (i & 7) == 0 && lane == 0)             // the helpers' pace (after the loads)
+                __hip_atomic_store(progress + b, i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // a step outside the lean case leaves at the end (a branch here would let the
+            // compiler sink the loads below it); until then its divisions run on safe values
+            const bool bad = (T == 0) | neg_u((uint64_t)(x - l)) | neg_u((uint64_t)(h - x)) |
+                             (ceil_map & neg_u(w - fthr)) | (cm == 0);
+            const uint64_t Ts = bad ? 1 : T, ws = bad ? 1 : w, vs = bad ? 0 : v;
+            const double iw = recip(ws);
+            const uint64_t tgt = div_small_u(vs, Ts, 0, ws, iw);   // < T < 2^32
             const uint32_t t32 = (uint32_t)tgt;
-#endif
             clk.mark(1);
             // in the loads' shadow: the 1-padded end's target
-            const uint64_t past = st.pos > mynbits ? st.pos - mynbits : 0;
+            const uint64_t past = pos > mynbits ? pos - mynbits : 0;
             const int u = past < (uint64_t)prec ? (int)past : prec;
-            const uint64_t vhi = v + ((1ull << u) - 1);
-            const uint64_t thi = vhi == v ? tgt : (vhi < w ? div_small_u(vhi, T, 0, w, recip(w)) : 0);
+            const uint64_t vhi = vs + ((1ull << u) - 1);
+            const bool vhi_in = neg_u(vhi - ws);                 // vhi < w
+            const uint64_t thi = u == 0 ? tgt : (vhi_in ? div_small_u(vhi, Ts, 0, ws, iw) : 0);
             clk.mark(2);
             // the iteration holding the target: the last whose first vector starts at or below it
             int gs = 0;
 #pragma unroll
             for (int g = 1; g < CIM; g++)
-                if (cv0 + g * 64 < nvec && (uint32_t)__builtin_amdgcn_readfirstlane((int)ps[g]) <= t32) gs = g;
+                if (cv0 + g * 64 < nv32 && (uint32_t)__builtin_amdgcn_readfirstlane((int)ps[g]) <= t32) gs = g;
             Vt xg = xs[0];
             uint32_t pg = ps[0];
 #pragma unroll
@@ -2186,14 +2279,13 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ pmf, i
                 xg = gs == g ? xs[g] : xg;
                 pg = gs == g ? ps[g] : pg;
             }
-            const bool real = cv0 + gs * 64 + lane < nvec;
+            const bool real = cv0 + gs * 64 + lane < nv32;
             uint32_t c[VEC];
             uint32_t acc = pg;
 #pragma unroll
             for (int j = 0; j < VEC; j++) { acc += real ? (uint32_t)vget<E, VEC>(xg, j) : 0u; c[j] = acc; }
             const uint64_t m2 = __ballot(real & (c[VEC - 1] > t32));
-            if (!m2) break;
-            const int L = __ffsll((unsigned long long)m2) - 1;
+            const int L = m2 ? __ffsll((unsigned long long)m2) - 1 : 0;
             uint32_t k = 0, lo = pg, hi = c[VEC - 1];
 #pragma unroll
             for (int j = VEC - 1; j >= 0; j--) {
@@ -2205,18 +2297,31 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ pmf, i
             for (int j = 0; j < VEC; j++) lo = c[j] <= t32 ? c[j] : lo;
             const uint64_t lo_c = (uint32_t)__builtin_amdgcn_readlane((int)lo, L);
             const uint64_t hi_c = (uint32_t)__builtin_amdgcn_readlane((int)hi, L);
-            const int64_t s = (cv0 + gs * 64 + L) * VEC + (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)k, L);
+            const int32_t sym = (cv0 + gs * 64 + L) * VEC + __builtin_amdgcn_readlane((int)k, L);
             clk.mark(3);
             uint64_t a, bb;
-            div_small_u2(lo_c, hi_c, w, ceil_map ? T - 1 : 0, T, iT, &a, &bb);
-            if (!((l + (int64_t)a) <= x && x <= l + (int64_t)bb - 1)) break;
+            div_small_u2(lo_c, hi_c, ws, ceil_map ? Ts - 1 : 0, Ts, bad ? 1.0 : iT, &a, &bb);
+            // (l + a <= x <= l + bb - 1: v in [a, bb))
+            if (bad || !m2 || neg_u(vs - a) || !neg_u(vs - bb)) break;
             clk.mark(4);
-            const bool det = vhi < w && thi < hi_c;
-            if (st.det && det) st.ndet++;
-            else st.det = 0;
-            decode_advance<true>(st, a, bb, win, mynbits, prec);
-            if (lane == (int)(i & 63)) sbuf = (int32_t)s;
-            if ((i & 63) == 63) sym_out[(t0 + i - 63 + lane) * B + b] = sbuf;
+            if (firstnd < 0 && !(vhi_in && neg_u(thi - hi_c))) firstnd = i;
+            // narrow + renormalise (decode_advance<true>)
+            int64_t nl = l + (int64_t)a, nh = l + (int64_t)bb - 1;
+            int kk;
+            uint64_t Ev;
+            renorm(nl, nh, prec, &kk, &Ev);
+            if (kk > 0) {
+                const BitWin wu{rfl_u64(win.w0), rfl_u64(win.w1)};
+                x = (int64_t)((((uint64_t)x - (Ev << (prec - kk))) << kk) | window_bits(wu, mynbits, pos, kk));
+                pos += (uint64_t)kk;
+            }
+            l = nl;
+            h = nh;
+            if (lane == (i & 63)) sbuf = sym;
+            if ((i & 63) == 63) {
+                *outv = sbuf;
+                outv += (int64_t)B32 * 64;
+            }
             clk.mark(5);
         }
     }
@@ -2226,8 +2331,20 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ pmf, i
         atomicAdd(&g_dec_phase[6], (unsigned long long)i);
     }
 #endif
-    if (lane < (int)(i & 63)) sym_out[(t0 + (i & ~(int64_t)63) + lane) * B + b] = sbuf;
+    if (lane < (i & 63)) *outv = sbuf;
+    if (progress && lane == 0)                                  // let the helpers go
+        __hip_atomic_store(progress + b, 1 << 30, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (lane == 0) {
+        // the counters of decode_symbol for the i steps done
+        if (st.det) {
+            st.ndet += firstnd < 0 ? i : firstnd;
+            st.det = firstnd < 0;
+        }
+        st.nsym += i;
+        st.l = l;
+        st.h = h;
+        st.x = x;
+        st.pos = pos;
         states[b] = st;
         resume[b] = t0 + i;
     }
@@ -3896,6 +4013,7 @@ struct lac_ctx {
     uint64_t *lchunk = nullptr;         //              [lean_steps * B][64] chunk bounds
     void *lmeta = nullptr;              //              [lean_steps * B] LeanMeta
     int64_t lean_steps = 0;             //              steps per launch the buffers hold
+    int32_t *dprogress = nullptr;       //              [B] decoder progress for the prefetch helpers
     float *q1m = nullptr;               //                [chunk_steps * B] row maxima
     uint64_t *pxch = nullptr;           // paired row stats (shape 19): [2 * cus] maximum words
     uint64_t *pack_off = nullptr;       // lac_pack_bits: [B] byte offsets of the streams
@@ -4115,6 +4233,12 @@ static int decode_stats_path(lac_ctx *c, const E *pmf, int64_t step_stride, int6
         }
         if (!c->dresume) HIPCHK(hipMalloc(&c->dresume, sizeof(int64_t) * c->B));
     }
+    // prefetching helper workgroups for the fewest streams (kLeanHelpers per stream, dealt
+    // to the stream's XCD)
+    const bool help = lean && LAC_LEAN_HELP && c->B <= kLeanHelpMaxStreams;
+    const int64_t B8 = (c->B + 7) & ~(int64_t)7;
+    const unsigned lean_blocks = (unsigned)(help ? B8 * (1 + kLeanHelpers) : c->B);
+    if (help && !c->dprogress) HIPCHK(hipMalloc(&c->dprogress, sizeof(int32_t) * c->B));
     for (int64_t t0 = 0; t0 < steps; t0 += cs) {
         const int64_t n = (steps - t0) < cs ? (steps - t0) : cs;
         const int64_t rows = n * c->B;
@@ -4125,10 +4249,12 @@ static int decode_stats_path(lac_ctx *c, const E *pmf, int64_t step_stride, int6
                 pmf, step_stride, stream_stride, c->B, rows, c->V, t0, c->q1chunks, (DecRowMeta *)c->dmeta,
                 (uint32_t *)c->lvpre, c->lchunk, (LeanMeta *)c->lmeta);
             CHECK_LAUNCH();
+            if (help) HIPCHK(hipMemsetAsync(c->dprogress, 0, sizeof(int32_t) * c->B, st));
 #define LAC_LEAN_K(CIM)                                                                                          \
-    k_decode_lean<E, VEC, CIM><<<(unsigned)c->B, 64, 0, st>>>(                                                 \
+    k_decode_lean<E, VEC, CIM><<<lean_blocks, 64, 0, st>>>(                                                    \
         pmf, step_stride, stream_stride, t0, n, c->V, c->prec, (const uint32_t *)c->lvpre, c->lchunk,          \
-        (const LeanMeta *)c->lmeta, c->dec, c->dbits, c->dstride, c->dnbits, out, c->B, c->mapping, c->dresume)
+        (const LeanMeta *)c->lmeta, c->dec, c->dbits, c->dstride, c->dnbits, out, c->B, c->mapping, c->dresume, \
+        help ? c->dprogress : nullptr)
             switch (CI) {
             case 1: LAC_LEAN_K(1); break;
             case 2: LAC_LEAN_K(2); break;
@@ -4708,6 +4834,7 @@ int lac_close(lac_ctx *c) {
     (void)hipFree(c->lvpre);
     (void)hipFree(c->lchunk);
     (void)hipFree(c->lmeta);
+    (void)hipFree(c->dprogress);
     (void)hipFree(c->q1m);
     (void)hipFree(c->pxch);
     (void)hipFree(c->pack_off);
