@@ -1156,13 +1156,16 @@ __device__ unsigned long long g_dec_phase[8];
 #endif
 
 // r < 0 for a wave-uniform int64.  (Forcing the test onto the scalar unit -- the high
-// word's sign through an opaque SGPR -- measured slower in both sequential decoders,
-// c2 1.29 -> 1.43 us/step, profiles/r04/lean/: the vector compare it replaces overlaps.)
+// word's sign through an opaque SGPR, or through readfirstlane -- measured slower in both
+// sequential decoders, c2 1.29 -> 1.43 / 1.50 us/step, profiles/r04/lean/: the vector
+// compare it replaces overlaps.)
 __device__ inline bool neg_u(uint64_t r) { return (int64_t)r < 0; }
 
 // div_small_fix for wave-uniform values (|r| < 3d < 2^53).
 __device__ inline uint64_t div_small_fix_u(uint64_t q, uint64_t n, uint64_t m, uint64_t add, uint64_t d) {
     uint64_t r = n * m + add - q * d;
+    // (corrections as a fixed count of selects instead of these loops, which are never
+    // entered past their first test: c2 1.29 -> 1.48 us/step, profiles/r04/lean/)
     while (neg_u(r)) { q -= 1; r += d; }
     for (;;) {
         const uint64_t t = r - d;
@@ -2101,9 +2104,15 @@ __global__ __launch_bounds__(256) void k_decode_seq(const E *__restrict__ pmf, i
 // They pace themselves by the decoder's progress (a relaxed agent-scope counter it sets
 // every 8 steps), never the other way round: results do not depend on them, and a
 // helper that sees no progress for ~10 ms gives up, so the grid always drains.
-constexpr int kLeanAhead = 8;                   // rows prefetched ahead of the decoder
-constexpr int kLeanHelpers = 16;                // helper waves per stream
-constexpr int kLeanHelpMaxStreams = 16;         // above: no helpers (L2: ~1.3 MB ahead per stream)
+#ifndef LAC_LEAN_AHEAD
+#define LAC_LEAN_AHEAD 16
+#endif
+#ifndef LAC_LEAN_HELPERS
+#define LAC_LEAN_HELPERS 16
+#endif
+constexpr int kLeanAhead = LAC_LEAN_AHEAD;      // rows prefetched ahead of the decoder
+constexpr int kLeanHelpers = LAC_LEAN_HELPERS;  // helper waves per stream
+constexpr int kLeanHelpMaxStreams = 16;         // above: no helpers (L2: ~2.6 MB ahead per stream)
 
 __device__ inline int32_t lean_progress(const int32_t *p) {
     return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));

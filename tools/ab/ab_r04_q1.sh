@@ -15,6 +15,6 @@ run() {   # run <tag> <variant> <cmd...>
     python3 -c "import json; d=json.loads(open('$o/${tag}_$v.json').read().strip().splitlines()[-1]); p=d['parity']['decode']; print('$tag $v', {k: round(1e3*x, 3) for k, x in p['kernel_ms_per_step_each'].items()}, 'rt', d['parity']['round_trip_all_streams'])"
 }
 for r in 1 2; do
-    for v in $VARS; do run c3_$r $v $B; done
+    [ -n "${NO_C3:-}" ] || for v in $VARS; do run c3_$r $v $B; done
     for v in $VARS; do run c2_$r $v $C2; done
 done
