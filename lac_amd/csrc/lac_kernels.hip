@@ -3809,16 +3809,19 @@ constexpr int kQ1WideSlotMaxVec = 512 * (kQ1WideR + kQ1WideL);
 // k_q1_decode: one wave per stream, sequential over a chunk of steps, from the
 // chunk totals of k_q1_stats: per step it finds the chunk holding
 // floor((x-l)*T/w), re-quantises only that chunk's logits and scans them to the
-// symbol, then renormalises as A_from_bin does (decode_advance).  (Loading all of
-// a chunk's groups at once instead of one per search round measured no faster at
-// c4, 4 / 8 groups per chunk: with 16 stream-waves per CU the step is bound by
-// their VALU issue, not by the re-read's latency -- profiles/r02/q1_pair_bf16/.)
+// symbol, then renormalises as A_from_bin does (decode_advance).  A chunk's groups
+// are loaded up to 4 at once and re-quantised one by one until the crossing (round 4:
+// c4 7.23 -> 6.89, Qwen2 7.28 -> 6.79 us/step, profiles/r04/q1dec/; round 2 had
+// re-quantised every loaded group, which measured no faster: with 16 stream-waves per
+// CU the step is bound by their issue).
 template <typename LT>
 __global__ LAC_DEC_BOUNDS void k_q1_decode(const LT *__restrict__ lg, int64_t step_stride, int64_t stream_stride,
                                            int64_t t0, int64_t nsteps, int64_t V, int prec, uint32_t xsh,
                                            int64_t G, const uint64_t *__restrict__ chunks,
                                            const float *__restrict__ mrow, DecState *states, const uint8_t *bits,
                                            uint64_t stride, const uint64_t *nbits, int32_t *sym_out, int64_t B) {
+    // (one shared table copy: 8 or 16 lane-interleaved copies against the gathers' bank
+    // conflicts measured no faster, profiles/r04/q1dec/)
     __shared__ uint32_t tab[LAC_Q1_TAB_SIZE];
     q1_load_tab(tab, xsh);
     constexpr int N = LogitN<LT>::N;
@@ -3887,10 +3890,22 @@ __global__ LAC_DEC_BOUNDS void k_q1_decode(const LT *__restrict__ lg, int64_t st
                 // runs in 32 bits and only the wave scan needs 64
                 uint64_t lo_c = cb, hi_c = ~0ull, cnt = 0;
                 bool found = false;
-                for (int64_t g = 0; g < G && !found; g++) {
+                // the chunk's groups, up to 4 loads in flight (clamped in-row indices), then
+                // re-quantised and scanned one by one until the crossing
+                for (int64_t g0 = 0; g0 < G && !found; g0 += 4) {
+                u32x4 xq[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int64_t vi = cv0 + (g0 + u) * 64 + lane;
+                    xq[u] = ld16(row, (g0 + u < G && vi < nvec) ? vi : nvec - 1, false);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int64_t g = g0 + u;
+                    if (found || g >= G) break;
                     const int64_t vi = cv0 + g * 64 + lane;
                     const bool valid = vi < nvec;
-                    const u32x4 xv = ld16(row, valid ? vi : nvec - 1, false);
+                    const u32x4 xv = xq[u];
                     uint32_t loc[N], ls = 0;
 #pragma unroll
                     for (int j = 0; j < N; j++) {
@@ -3923,6 +3938,7 @@ __global__ LAC_DEC_BOUNDS void k_q1_decode(const LT *__restrict__ lg, int64_t st
                         found = true;
                     }
                     cb += readlane_u64(in, 63);
+                }
                 }
                 if (!found) {
                     err = LAC_E_DECODE_RANGE;                  // corrupt state: tgt outside the chunk
