@@ -5,6 +5,8 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 o=gpurun_out/${1:-ab_q1big}; shift; mkdir -p $o
 VARS="${*:-cur head}"
+timeout -k 10 500 python3 -u -m pytest tests/test_gpu_logits.py tests/test_gpu_fuzz.py -m gpu -x -q -rf --timeout 120 --timeout-method thread -p no:cacheprovider > $o/tests.log 2>&1 || { tail -30 $o/tests.log; exit 1; }
+tail -1 $o/tests.log
 B="python3 bench.py --cpu-baseline off --steps 10 --warmup 5 --decode-reps 5 --input logits-bf16"
 run() {
     local tag=$1 v=$2; shift 2
@@ -15,4 +17,5 @@ run() {
 for r in 1 2; do
     for v in $VARS; do run c4_$r $v $B --vocab 128256; done
     for v in $VARS; do run qwen2_$r $v $B --vocab 151936; done
+    [ -n "${NO_L4:-}" ] || for v in $VARS; do run llama4_$r $v $B --vocab 202048; done
 done
