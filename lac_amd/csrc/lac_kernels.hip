@@ -3841,21 +3841,32 @@ __global__ LAC_DEC_BOUNDS void k_q1_decode(const LT *__restrict__ lg, int64_t st
     const bool small = prec <= 50;
     uint64_t next = nsteps > 0 ? chunks[b * 64 + lane] : 0;
     float mnext = nsteps > 0 ? mrow[b] : 0.f;
-    for (int64_t i = 0; i < nsteps; i++) {
+    // (as k_decode_lean) a 32-bit step counter, running row pointers, and the symbols
+    // collected one per lane and stored once per 64 steps
+    const int32_t n32 = (int32_t)nsteps;                        // (<= chunk_steps)
+    const LT *rowp = lg + t0 * step_stride + b * stream_stride;
+    int32_t *outv = sym_out + (t0 + lane) * B + b;              // lane j: step 64k + j
+    int32_t sbuf = -1;
+    int32_t i = 0;
+    for (; i < n32; i++) {
         dec_state_uniform(st);                                 // (the loop's phis are not seen as uniform)
-        const int64_t t = t0 + i, r = i * B + b;
+        const int64_t r = (int64_t)i * B + b;
         const uint64_t mine = next;
         const float mcur = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, mnext)));
-        if (i + 1 < nsteps) {                                  // prefetch: independent of the state
+        if (i + 1 < n32) {                                     // prefetch: independent of the state
             next = chunks[(r + B) * 64 + lane];
             mnext = mrow[r + B];
         }
-        int32_t *out = sym_out + t * B + b;
+        const LT *row = rowp;
+        rowp += step_stride;
         if (st.err) {
-            if (lane == 0) *out = -1;
+            if (lane == (i & 63)) sbuf = -1;
+            if ((i & 63) == 63) {
+                *outv = sbuf;
+                outv += B * 64;
+            }
             continue;
         }
-        const LT *row = lg + t * step_stride + b * stream_stride;
         const BitWin win = bit_window(mybits, mynbits, st.pos);    // in flight during the search
         const float c = q1_c(mcur);
         const uint64_t incl = wave_incl_scan_u64(mine);
@@ -3961,8 +3972,13 @@ __global__ LAC_DEC_BOUNDS void k_q1_decode(const LT *__restrict__ lg, int64_t st
             st.err = err;
             st.err_step = st.nsym;
         }
-        if (lane == 0) *out = err ? -1 : (int32_t)s;
+        if (lane == (i & 63)) sbuf = err ? -1 : (int32_t)s;
+        if ((i & 63) == 63) {
+            *outv = sbuf;
+            outv += B * 64;
+        }
     }
+    if (lane < (i & 63)) *outv = sbuf;
     if (lane == 0) states[b] = st;
 }
 
