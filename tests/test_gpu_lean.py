@@ -63,3 +63,27 @@ def test_lean_many_launch_chunks_and_ragged_vocab():
         c.decode_open()
         assert torch.equal(c.decode(pmf), sym), path
     c.close()
+
+
+@pytest.mark.parametrize("mapping", ["floor", "ceil"])
+def test_lean_mappings_agree_with_wave_path(mapping):
+    """The floor mapping (Predictor / ACSampler ranges, no fudge) and the ceil mapping
+    through the lean step give the wave kernel's symbols, at 1 and 5 streams (helpers on)."""
+    from lac_amd.batch import BatchCoder
+    rng = np.random.default_rng(11)
+    for B in (1, 5):
+        V, T, prec = 1000, 700, 36
+        pmf = rng.integers(1, 5000, size=(T, B, V)).astype(np.uint32)
+        sym = rng.integers(0, V, size=(T, B)).astype(np.int32)
+        c = BatchCoder(V, B, prec=prec, capacity_bits=T * (prec + 16) + 256, device=DEV)
+        c.set_mapping(mapping)
+        dp = torch.from_numpy(pmf.view(np.int32)).to(DEV)
+        c.encode_job(dp, torch.from_numpy(sym).to(DEV))
+        c.raise_on_error()
+        outs = []
+        for path in ("stats", "fused"):
+            c.set_decode_path(path)
+            c.decode_open()
+            outs.append(c.decode(dp).cpu().numpy())
+        c.close()
+        assert np.array_equal(outs[0], sym) and np.array_equal(outs[1], sym), (mapping, B)
