@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Mean per-dispatch counter values per kernel from tools/pmc_passes.sh output.
+"""Mean per-dispatch counter values per kernel from tools/sessions/pmc_passes.sh output.
 
     python3 tools/pmc_summary.py gpurun_out/<outdir> [kernel-substring]
 FETCH_SIZE is also shown as bytes x2 (gfx950 wide-read correction, MI355X_MICROARCH.md)."""
