@@ -2162,7 +2162,8 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ pmf, i
                                                     int prec, const uint32_t *__restrict__ vpre,
                                                     const uint64_t *__restrict__ lchunk,
                                                     const LeanMeta *__restrict__ lmeta, DecState *states,
-                                                    const uint8_t *bits, uint64_t stride, const uint64_t *nbits,
+                                                    const uint8_t *__restrict__ bits, uint64_t stride,
+                                                    const uint64_t *__restrict__ nbits,
                                                     int32_t *sym_out, int64_t B, int mapping,
                                                     int64_t *__restrict__ resume, int32_t *progress) {
     typedef typename VecT<E, VEC>::type Vt;
