@@ -3897,6 +3897,8 @@ __global__ LAC_DEC_BOUNDS void k_q1_decode(const LT *__restrict__ lg, int64_t st
                 const int src = __ffsll((unsigned long long)mask) - 1;
                 uint64_t cb = readlane_u64(ex, src);
                 const int64_t cv0 = (int64_t)src * G * 64;
+                // a chunk whose total is below 2^32 (nearly all) scans its groups in 32 bits
+                const bool narrow = readlane_u64(mine, src) < (1ull << 32);
                 // the crossing lane by ballot, as scan_chunk (entries <= tgt are a prefix);
                 // a lane's 8 (bf16) / 4 (f32) entries are <= 2^24 each, so its own prefix
                 // runs in 32 bits and only the wave scan needs 64
@@ -3928,7 +3930,7 @@ __global__ LAC_DEC_BOUNDS void k_q1_decode(const LT *__restrict__ lg, int64_t st
                         ls += valid ? q : 0u;
                         loc[j] = ls;
                     }
-                    const uint64_t in = wave_incl_scan_u64((uint64_t)ls);
+                    const uint64_t in = narrow ? (uint64_t)wave_incl_scan_u32(ls) : wave_incl_scan_u64((uint64_t)ls);
                     const uint64_t exb = cb + in - ls;
                     const uint64_t m = __ballot(exb + ls > tgt);
                     if (m) {
