@@ -87,3 +87,22 @@ def test_lean_mappings_agree_with_wave_path(mapping):
             outs.append(c.decode(dp).cpu().numpy())
         c.close()
         assert np.array_equal(outs[0], sym) and np.array_equal(outs[1], sym), (mapping, B)
+
+
+def test_lean_total_at_2_32_boundary():
+    """Rows with totals 2^32 - 1 (lean) and exactly 2^32 (k_decode_seq) interleaved in one
+    stream; the vector CDF wraps mod 2^32 only on the rows the lean step refuses."""
+    rng = np.random.default_rng(3)
+    V, B, T, prec = 1024, 2, 200, 48
+    base = np.full(V, (1 << 22), dtype=np.uint64)                # 1024 * 2^22 = 2^32
+    pmf = np.empty((T, B, V), dtype=np.uint32)
+    for t in range(T):
+        for b in range(B):
+            row = base.copy()
+            if (t + b) % 3 == 0:
+                row[rng.integers(V)] -= 1                            # 2^32 - 1: lean
+            pmf[t, b] = row.astype(np.uint32)
+    sym = rng.integers(0, V, size=(T, B)).astype(np.int32)
+    outs = _roundtrip(pmf, sym, prec)
+    for path, o in outs.items():
+        assert np.array_equal(o, sym), path
