@@ -2112,6 +2112,10 @@ __global__ __launch_bounds__(256) void k_decode_seq(const E *__restrict__ pmf, i
 #endif
 constexpr int kLeanAhead = LAC_LEAN_AHEAD;      // rows prefetched ahead of the decoder
 constexpr int kLeanHelpers = LAC_LEAN_HELPERS;  // helper waves per stream
+#ifndef LAC_LEAN_MAX_STREAMS
+#define LAC_LEAN_MAX_STREAMS 64
+#endif
+constexpr int64_t kLeanMaxStreams = LAC_LEAN_MAX_STREAMS;   // k_decode_lean up to this many streams
 constexpr int kLeanHelpMaxStreams = 16;         // above: no helpers (L2: ~2.6 MB ahead per stream)
 
 __device__ inline int32_t lean_progress(const int32_t *p) {
@@ -4255,7 +4259,12 @@ static int decode_stats_path(lac_ctx *c, const E *pmf, int64_t step_stride, int6
     // buffers hold up to 64 MB of vector CDFs, so its launches take at most that many steps
     const int64_t nvec = c->V / VEC, nit = (nvec + 63) / 64;
     const int64_t CI = nit ? (nit + 63) / 64 : 1;
-    const bool lean = LAC_LEAN && sizeof(E) == 4 && c->prec <= 50 && CI <= 4 && nvec > 0;   // (u64 tables: totals >= 2^32)
+    // (u64 tables: totals >= 2^32.)  Only for the fewest streams: the stats pass writes a
+    // quarter of the rows' bytes more (the vector CDF), which costs more than the shorter
+    // chain saves once enough streams run side by side (same box, V=32000: B=4 1.36 vs
+    // 2.66 us/step, 64 3.41 vs 3.96, 128 5.39 vs 5.26, 512 18.0 vs 13.3, 1024 34.1 vs 22.8;
+    // profiles/r04/lean/fewstreams/)
+    const bool lean = LAC_LEAN && sizeof(E) == 4 && c->prec <= 50 && CI <= 4 && nvec > 0 && c->B <= kLeanMaxStreams;
     int64_t cs = c->chunk_steps;
     if (lean) {
         const int64_t per = c->B * nvec * (int64_t)sizeof(uint32_t);
