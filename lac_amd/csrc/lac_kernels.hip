@@ -3819,14 +3819,18 @@ constexpr int kQ1WideSlotMaxVec = 512 * (kQ1WideR + kQ1WideL);
 // c4 7.23 -> 6.89, Qwen2 7.28 -> 6.79 us/step, profiles/r04/q1dec/; round 2 had
 // re-quantised every loaded group, which measured no faster: with 16 stream-waves per
 // CU the step is bound by their issue).
-template <typename LT>
+// G1: a chunk is one group (rows of <= 4096 vectors, e.g. the c3 shape): the group
+// search compiles to one straight-line pass instead of four unrolled copies.
+template <typename LT, bool G1 = false>
 __global__ LAC_DEC_BOUNDS void k_q1_decode(const LT *__restrict__ lg, int64_t step_stride, int64_t stream_stride,
                                            int64_t t0, int64_t nsteps, int64_t V, int prec, uint32_t xsh,
-                                           int64_t G, const uint64_t *__restrict__ chunks,
+                                           int64_t Garg, const uint64_t *__restrict__ chunks,
                                            const float *__restrict__ mrow, DecState *states, const uint8_t *bits,
                                            uint64_t stride, const uint64_t *nbits, int32_t *sym_out, int64_t B) {
     // (one shared table copy: 8 or 16 lane-interleaved copies against the gathers' bank
     // conflicts measured no faster, profiles/r04/q1dec/)
+    const int64_t G = G1 ? 1 : Garg;
+    constexpr int GPF = G1 ? 1 : 4;                             // group loads in flight
     __shared__ uint32_t tab[LAC_Q1_TAB_SIZE];
     q1_load_tab(tab, xsh);
     constexpr int N = LogitN<LT>::N;
@@ -3910,15 +3914,15 @@ __global__ LAC_DEC_BOUNDS void k_q1_decode(const LT *__restrict__ lg, int64_t st
                 bool found = false;
                 // the chunk's groups, up to 4 loads in flight (clamped in-row indices), then
                 // re-quantised and scanned one by one until the crossing
-                for (int64_t g0 = 0; g0 < G && !found; g0 += 4) {
-                u32x4 xq[4];
+                for (int64_t g0 = 0; g0 < G && !found; g0 += GPF) {
+                u32x4 xq[GPF];
 #pragma unroll
-                for (int u = 0; u < 4; u++) {
+                for (int u = 0; u < GPF; u++) {
                     const int64_t vi = cv0 + (g0 + u) * 64 + lane;
                     xq[u] = ld16(row, (g0 + u < G && vi < nvec) ? vi : nvec - 1, false);
                 }
 #pragma unroll
-                for (int u = 0; u < 4; u++) {
+                for (int u = 0; u < GPF; u++) {
                     const int64_t g = g0 + u;
                     if (found || g >= G) break;
                     const int64_t vi = cv0 + g * 64 + lane;
@@ -4808,9 +4812,14 @@ static int q1_decode(lac_ctx *c, const Q1Args &a0, int64_t steps, int32_t *out, 
         int rc = q1_stats<LT, true>(c, a, st);
         if (rc) return rc;
         ProfScope ps(c, KID_Q1_DECODE, st);
-        k_q1_decode<LT><<<blocks, 64 * kWavesPerBlock, 0, st>>>(
-            (const LT *)a.lg, a.ss, a.bs, t0, n, c->V, c->prec, a.xsh, q1_groups_per_chunk(nvec), c->q1chunks,
-            c->q1m, c->dec, c->dbits, c->dstride, c->dnbits, out, c->B);
+        if (q1_groups_per_chunk(nvec) == 1)
+            k_q1_decode<LT, true><<<blocks, 64 * kWavesPerBlock, 0, st>>>(
+                (const LT *)a.lg, a.ss, a.bs, t0, n, c->V, c->prec, a.xsh, 1, c->q1chunks, c->q1m, c->dec, c->dbits,
+                c->dstride, c->dnbits, out, c->B);
+        else
+            k_q1_decode<LT><<<blocks, 64 * kWavesPerBlock, 0, st>>>(
+                (const LT *)a.lg, a.ss, a.bs, t0, n, c->V, c->prec, a.xsh, q1_groups_per_chunk(nvec), c->q1chunks,
+                c->q1m, c->dec, c->dbits, c->dstride, c->dnbits, out, c->B);
         CHECK_LAUNCH();
     }
     return LAC_OK;
