@@ -3819,9 +3819,10 @@ constexpr int kQ1WideSlotMaxVec = 512 * (kQ1WideR + kQ1WideL);
 // c4 7.23 -> 6.89, Qwen2 7.28 -> 6.79 us/step, profiles/r04/q1dec/; round 2 had
 // re-quantised every loaded group, which measured no faster: with 16 stream-waves per
 // CU the step is bound by their issue).
-// G1: a chunk is one group (rows of <= 4096 vectors, e.g. the c3 shape): the group
-// search compiles to one straight-line pass instead of four unrolled copies.
-template <typename LT, bool G1 = false>
+// GC: the groups per chunk when known at compile time (1..4; 0 = G at run time): one
+// group (rows of <= 4096 vectors, the c3 shape) compiles to one straight-line pass
+// instead of four unrolled copies inside a loop.
+template <typename LT, int GC = 0>
 __global__ LAC_DEC_BOUNDS void k_q1_decode(const LT *__restrict__ lg, int64_t step_stride, int64_t stream_stride,
                                            int64_t t0, int64_t nsteps, int64_t V, int prec, uint32_t xsh,
                                            int64_t Garg, const uint64_t *__restrict__ chunks,
@@ -3829,8 +3830,8 @@ __global__ LAC_DEC_BOUNDS void k_q1_decode(const LT *__restrict__ lg, int64_t st
                                            uint64_t stride, const uint64_t *nbits, int32_t *sym_out, int64_t B) {
     // (one shared table copy: 8 or 16 lane-interleaved copies against the gathers' bank
     // conflicts measured no faster, profiles/r04/q1dec/)
-    const int64_t G = G1 ? 1 : Garg;
-    constexpr int GPF = G1 ? 1 : 4;                             // group loads in flight
+    const int64_t G = GC ? GC : Garg;
+    constexpr int GPF = GC ? GC : 4;                            // group loads in flight
     __shared__ uint32_t tab[LAC_Q1_TAB_SIZE];
     q1_load_tab(tab, xsh);
     constexpr int N = LogitN<LT>::N;
@@ -4812,14 +4813,19 @@ static int q1_decode(lac_ctx *c, const Q1Args &a0, int64_t steps, int32_t *out, 
         int rc = q1_stats<LT, true>(c, a, st);
         if (rc) return rc;
         ProfScope ps(c, KID_Q1_DECODE, st);
-        if (q1_groups_per_chunk(nvec) == 1)
-            k_q1_decode<LT, true><<<blocks, 64 * kWavesPerBlock, 0, st>>>(
-                (const LT *)a.lg, a.ss, a.bs, t0, n, c->V, c->prec, a.xsh, 1, c->q1chunks, c->q1m, c->dec, c->dbits,
-                c->dstride, c->dnbits, out, c->B);
-        else
-            k_q1_decode<LT><<<blocks, 64 * kWavesPerBlock, 0, st>>>(
-                (const LT *)a.lg, a.ss, a.bs, t0, n, c->V, c->prec, a.xsh, q1_groups_per_chunk(nvec), c->q1chunks,
-                c->q1m, c->dec, c->dbits, c->dstride, c->dnbits, out, c->B);
+        const int64_t G = q1_groups_per_chunk(nvec);
+#define LAC_Q1_DEC(GC)                                                                                            \
+    k_q1_decode<LT, GC><<<blocks, 64 * kWavesPerBlock, 0, st>>>((const LT *)a.lg, a.ss, a.bs, t0, n, c->V, c->prec, \
+                                                               a.xsh, G, c->q1chunks, c->q1m, c->dec, c->dbits,    \
+                                                               c->dstride, c->dnbits, out, c->B)
+        switch (G) {
+        case 1: LAC_Q1_DEC(1); break;
+        case 2: LAC_Q1_DEC(2); break;
+        case 3: LAC_Q1_DEC(3); break;
+        case 4: LAC_Q1_DEC(4); break;
+        default: LAC_Q1_DEC(0); break;
+        }
+#undef LAC_Q1_DEC
         CHECK_LAUNCH();
     }
     return LAC_OK;
