@@ -3819,7 +3819,7 @@ constexpr int kQ1WideSlotMaxVec = 512 * (kQ1WideR + kQ1WideL);
 // c4 7.23 -> 6.89, Qwen2 7.28 -> 6.79 us/step, profiles/r04/q1dec/; round 2 had
 // re-quantised every loaded group, which measured no faster: with 16 stream-waves per
 // CU the step is bound by their issue).
-// GC: the groups per chunk when known at compile time (1..4; 0 = G at run time): one
+// GC: the groups per chunk when known at compile time (1..8; 0 = G at run time): one
 // group (rows of <= 4096 vectors, the c3 shape) compiles to one straight-line pass
 // instead of four unrolled copies inside a loop.
 template <typename LT, int GC = 0>
@@ -4823,6 +4823,10 @@ static int q1_decode(lac_ctx *c, const Q1Args &a0, int64_t steps, int32_t *out, 
         case 2: LAC_Q1_DEC(2); break;
         case 3: LAC_Q1_DEC(3); break;
         case 4: LAC_Q1_DEC(4); break;
+        case 5: LAC_Q1_DEC(5); break;
+        case 6: LAC_Q1_DEC(6); break;
+        case 7: LAC_Q1_DEC(7); break;
+        case 8: LAC_Q1_DEC(8); break;
         default: LAC_Q1_DEC(0); break;
         }
 #undef LAC_Q1_DEC
