@@ -3822,7 +3822,7 @@ constexpr int kQ1WideSlotMaxVec = 512 * (kQ1WideR + kQ1WideL);
 // GC: the groups per chunk when known at compile time (1..8; 0 = G at run time): one
 // group (rows of <= 4096 vectors, the c3 shape) compiles to one straight-line pass
 // instead of four unrolled copies inside a loop.
-template <typename LT, int GC = 0>
+template <typename LT, int GC = 0, bool SMALL = true>
 __global__ LAC_DEC_BOUNDS void k_q1_decode(const LT *__restrict__ lg, int64_t step_stride, int64_t stream_stride,
                                            int64_t t0, int64_t nsteps, int64_t V, int prec, uint32_t xsh,
                                            int64_t Garg, const uint64_t *__restrict__ chunks,
@@ -3848,7 +3848,7 @@ __global__ LAC_DEC_BOUNDS void k_q1_decode(const LT *__restrict__ lg, int64_t st
     const uint8_t *mybits = bits + b * stride;
     const uint64_t mynbits = rfl_u64(nbits[b]);
     const int64_t nvec = V / N;
-    const bool small = prec <= 50;
+    const bool small = SMALL;                                   // (the host passes prec <= 50)
     uint64_t next = nsteps > 0 ? chunks[b * 64 + lane] : 0;
     float mnext = nsteps > 0 ? mrow[b] : 0.f;
     // (as k_decode_lean) a 32-bit step counter, running row pointers, and the symbols
@@ -4818,7 +4818,12 @@ static int q1_decode(lac_ctx *c, const Q1Args &a0, int64_t steps, int32_t *out, 
     k_q1_decode<LT, GC><<<blocks, 64 * kWavesPerBlock, 0, st>>>((const LT *)a.lg, a.ss, a.bs, t0, n, c->V, c->prec, \
                                                                a.xsh, G, c->q1chunks, c->q1m, c->dec, c->dbits,    \
                                                                c->dstride, c->dnbits, out, c->B)
-        switch (G) {
+        // prec > 50 (quotients past div_small's range): the general form, 128-bit divisions
+        if (c->prec > 50)
+            k_q1_decode<LT, 0, false><<<blocks, 64 * kWavesPerBlock, 0, st>>>(
+                (const LT *)a.lg, a.ss, a.bs, t0, n, c->V, c->prec, a.xsh, G, c->q1chunks, c->q1m, c->dec, c->dbits,
+                c->dstride, c->dnbits, out, c->B);
+        else switch (G) {
         case 1: LAC_Q1_DEC(1); break;
         case 2: LAC_Q1_DEC(2); break;
         case 3: LAC_Q1_DEC(3); break;

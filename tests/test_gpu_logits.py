@@ -85,6 +85,8 @@ CASES = [
     (65536, 6, 3, 48, "bf16"),             # (8,16) shape
     (24, 5, 50, 24, "f32"),
     (4096, 2048, 3, 48, "bf16"),
+    (1000, 16, 20, 56, "bf16"),            # prec > 50: k_q1_decode's 128-bit division form
+    (32000, 8, 6, 60, "f32"),
 ]
 
 
