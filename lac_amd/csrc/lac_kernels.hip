@@ -1945,10 +1945,26 @@ __global__ __launch_bounds__(256) void k_dec_stats(const E *__restrict__ pmf, in
     int64_t chunk = 0, left = CI;
     uint32_t run = 0;                                          // LEAN: the row's sum so far, mod 2^32
     uint32_t *vp = LEAN ? vpre + r * nvec : nullptr;
+    // LEAN: a group's vpre values are stored after the next group's loads are issued, so
+    // the in-order wait for those loads never waits on these stores (B=64: 3.41 -> 3.35 us
+    // per step; the pass stays ~1.5x the plain one, bound by its per-iteration scans)
+    uint32_t pv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int64_t pg = -1;
+    auto store_pending = [&]() {
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int64_t vi = (pg * 8 + u) * 64 + lane;
+            if (vi < nvec) vp[vi] = pv[u];
+        }
+    };
     for (int64_t g = 0; g < ngrp; g++) {
         typename VecT<E, VEC>::type x[8];
 #pragma unroll
         for (int u = 0; u < 8; u++) x[u] = load_vec_or0<E, VEC>(row, (g * 8 + u) * 64 + lane, nvec);
+        if constexpr (LEAN) {
+            __builtin_amdgcn_sched_barrier(0);
+            if (pg >= 0) store_pending();
+        }
         uint64_t s8[8];
 #pragma unroll
         for (int u = 0; u < 8; u++) {
@@ -1965,11 +1981,11 @@ __global__ __launch_bounds__(256) void k_dec_stats(const E *__restrict__ pmf, in
         if constexpr (LEAN) {
 #pragma unroll
             for (int u = 0; u < 8; u++) {
-                const int64_t vi = (g * 8 + u) * 64 + lane;
                 const uint32_t in = wave_incl_scan_u32((uint32_t)s8[u]);
-                if (vi < nvec) vp[vi] = run + in - (uint32_t)s8[u];
+                pv[u] = run + in - (uint32_t)s8[u];
                 run += (uint32_t)__builtin_amdgcn_readlane((int)in, 63);
             }
+            pg = g;
         }
         const uint64_t tot = wave_sum8_u64<W>(s8, ovf);       // lane l: iteration g*8 + (l & 7)
 #pragma unroll
@@ -1979,6 +1995,9 @@ __global__ __launch_bounds__(256) void k_dec_stats(const E *__restrict__ pmf, in
             if (lane == chunk) mine = add_ovf<W>(mine, v, ovf);
             if (--left == 0) { chunk++; left = CI; }
         }
+    }
+    if constexpr (LEAN) {
+        if (pg >= 0) store_pending();
     }
     uint64_t minp;
     if constexpr (sizeof(E) == 8) minp = wave_min_u64(mn) + 1;
