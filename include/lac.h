@@ -78,30 +78,28 @@ enum {                       /* lac_set_option */
                                       STATS, BLOCK = see LAC_PATH_STATS / LAC_PATH_BLOCK;
                                       AUTO = FUSED from 2048 streams, BLOCK at 5/8 CUs .. CUs streams
                                       (160-256 on MI355X) and from 1536, else STATS */
-    LAC_OPT_Q1_SHAPE = 6,          /* logits path row-stats shape: 0 = auto (default), 1..7 = (waves per
+    LAC_OPT_Q1_SHAPE = 6,          /* logits path row-stats shape: 0 = auto (default), 1..4 / 6 = (waves per
                                       row, vectors/thread, rolling prefetch) (1,4,n) (2,8,n) (4,8,n)
-                                      (8,8,n) (8,16,n) (8,8,y) (8,4,y), 8 = tiles of (8,8,n),
-                                      9 = 16-wave (16,16,n), 10 = tiles of 9, 11 = (16,8,y),
-                                      12 = (16,8,n), 13 / 14 = tiles of (8,8) / (16,8) with a
+                                      (8,8,n) / (8,8,y), 8 = tiles of (8,8,n), 10 = tiles of a
+                                      16-wave (16,16,n) block, 14 = tiles of (16,8) with a
                                       tile-walking prefetch, 15 = 16-wave, 8 vectors/thread in
                                       registers + 8 in LDS (rows <= 16384 vectors; 16 table copies
                                       when the row fits a trimmed last slot, <= 16064 vectors),
-                                      16 = 15 with 8 table copies always, 17 / 18 = the same
-                                      register + LDS form with 4 rows of <= 4096 / 2 rows of
-                                      <= 8192 vectors per 16-wave block, 19 / 20 / 21 = row
-                                      groups: a row of > 16384 vectors in 2..16 segments, one
-                                      per row slot of 1 / 2 / 4 rows per 16-wave block (the
-                                      forms of 15 / 18 / 17; slots are numbered across the
-                                      blocks of an XCD, so a segment count need not divide
-                                      the blocks); AUTO picks the form that fills its slots
-                                      best (f32 V = 128256: 2 slots of 1 row per block),
-                                      22 = one row of <= 20480 vectors per 8-wave block,
-                                      whole in registers (AUTO for 16385..20480 vectors:
-                                      bf16 V = 151936), 23 = groups of such blocks (AUTO
-                                      where the slot form has several rows per block:
-                                      bf16 V = 262144, f32 V = 151936); identical results,
-                                      only speed
-                                      differs */
+                                      17 / 18 = the same register + LDS form with 4 rows of
+                                      <= 4096 / 2 rows of <= 8192 vectors per 16-wave block,
+                                      19 / 20 / 21 = row groups: a row of > 16384 vectors in
+                                      2..16 segments, one per row slot of 1 / 2 / 4 rows per
+                                      16-wave block (the forms of 15 / 18 / 17; slots are
+                                      numbered across the blocks of an XCD, so a segment count
+                                      need not divide the blocks); AUTO picks the form that
+                                      fills its slots best (f32 V = 128256: 2 slots of 1 row
+                                      per block), 22 = one row of <= 20480 vectors per 8-wave
+                                      block, whole in registers (+ LDS slots up to 26112),
+                                      23 = groups of such blocks (AUTO where the slot form has
+                                      several rows per block: bf16 V = 262144, f32 V = 151936);
+                                      5, 7, 9, 11, 12, 13 and 16 are retired (AUTO never took
+                                      them) and refused with LAC_E_ARG; identical results,
+                                      only speed differs */
     LAC_OPT_DECODE_FINE = 7,       /* one-wave decode (FUSED path): 1 = one total per 64 vectors of
                                       the row, so only 1 KB is re-read after the search (default,
                                       rows <= 131072 u32 / 65536 u64 entries); 0 = <= 64 chunk totals */

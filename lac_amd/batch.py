@@ -448,10 +448,12 @@ class BatchCoder:
 
     def set_q1_shape(self, shape: int):
         """Logits row-stats block shape (include/lac.h LAC_OPT_Q1_SHAPE; identical
-        results, only speed differs): 0 auto, 1..18 forced single-block forms,
-        19 / 20 / 21 row groups -- a row of > 16384 vectors in 2..16 segments, one
-        per row slot of 1 / 2 / 4 rows per 16-wave block --, 22 one row of <= 20480
-        vectors whole in the registers of one 8-wave block, 23 groups of such blocks."""
+        results, only speed differs): 0 auto, 1..4 / 6 / 8 / 10 / 14 / 15 / 17 / 18
+        forced single-block forms, 19 / 20 / 21 row groups -- a row of > 16384
+        vectors in 2..16 segments, one per row slot of 1 / 2 / 4 rows per 16-wave
+        block --, 22 one row of <= 26112 vectors in the registers (+ LDS slots) of
+        one 8-wave block, 23 groups of such blocks.  The retired shapes 5, 7, 9, 11,
+        12, 13 and 16 (never chosen by AUTO) raise LacError (LAC_E_ARG)."""
         check(self.lib.lac_set_option(self.ctx, _lib.LAC_OPT_Q1_SHAPE, int(shape)))
 
     def q1_k(self):

@@ -4654,8 +4654,8 @@ static int q1_wide_group_kernel(lac_ctx *c, const Q1Args &a, hipStream_t st, con
 }
 
 // The register + LDS-slot shapes (k_q1_stats_rl), by rows per block:
-//   15 = one row of <= 16384 vectors (16 table copies when <= 16064: trimmed last slot), 16 = the same with 8
-//   copies always, 17 = four rows of <= 4096 vectors (4 waves each), 18 = two rows of <= 8192 (8 waves each).
+//   15 = one row of <= 16384 vectors (16 table copies when <= 16064: trimmed last slot, else 8),
+//   17 = four rows of <= 4096 vectors (4 waves each), 18 = two rows of <= 8192 (8 waves each).
 // A trimmed last slot (whole waves only) makes room for 16 table copies where the LDS allows it.
 template <typename LT, bool DEC>
 static int q1_stats_rl_launch(lac_ctx *c, const Q1Args &a, hipStream_t st, int shape) {
@@ -4663,8 +4663,6 @@ static int q1_stats_rl_launch(lac_ctx *c, const Q1Args &a, hipStream_t st, int s
     switch (shape) {
     case 15:
         if (nvec <= kRLTrimMaxVec) return q1_rl_kernel<LT, DEC, 16, kRLLastTrim, 1024>(c, a, st);
-        return q1_rl_kernel<LT, DEC, kRLRep, 1024, 1024>(c, a, st);
-    case 16:
         return q1_rl_kernel<LT, DEC, kRLRep, 1024, 1024>(c, a, st);
     case 17:                                       // LDS: 4 x 31 KB of slots + 16 copies (encode) / 8 (decode)
         if (nvec <= 15 * 256 + 192) return q1_rl_kernel<LT, DEC, DEC ? 8 : 16, 192, 256>(c, a, st);
@@ -4680,11 +4678,19 @@ static int q1_stats_rl_launch(lac_ctx *c, const Q1Args &a, hipStream_t st, int s
 // in registers (measured on MI355X, c3 shape: encode bf16 (8,8,y) 0.75 ms vs
 // (8,8,n) 0.79 ms; decode (8,8,n) 70 M sym/s vs 46 M for the spilling (8,8,y)),
 // else tiles of (8, 8); LAC_OPT_Q1_SHAPE forces one for both directions (tuning;
-// identical results).  Shapes 9-12 are one 16-wave block per CU: 9 = (16,16,n),
-// 10 = tiles of 9, 11 = (16,8,y), 12 = (16,8,n); 13 / 14 = tiles of (8,8) / (16,8)
-// with a rolling prefetch that walks the tiles (pass 1 up, pass 2 down, then the
-// next row's first tile).
+// identical results).  10 = tiles of a 16-wave (16,16,n) block per CU, 14 = tiles of
+// (16,8) with a rolling prefetch that walks the tiles (pass 1 up, pass 2 down, then
+// the next row's first tile).
+//
+// Round 4 retired the shapes AUTO never reaches (5, 7, 9, 11, 12, 13, 16): each vocabulary
+// range resolves to one of 1..4 / 6 (rows <= 4096 vectors), 17 / 18 (<= 8192), 15
+// (<= 16384), 22 (<= 26112), 19..21 / 23 (longer) or the tiled fallbacks 8 / 10 / 14,
+// and a forced retired number is refused (LAC_E_ARG) instead of running a form no
+// default configuration exercises.  Their measurements stay in DESIGN.md section 5b.
 static const int kQ1Shapes[][3] = {{1, 4, 0}, {2, 8, 0}, {4, 8, 0}, {8, 8, 0}, {8, 16, 0}, {8, 8, 1}, {8, 4, 1}};
+static bool q1_shape_live(int sh) {
+    return sh >= 0 && sh <= 23 && sh != 5 && sh != 7 && sh != 9 && sh != 11 && sh != 12 && sh != 13 && sh != 16;
+}
 
 template <typename LT, bool DEC>
 static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
@@ -4692,7 +4698,7 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
     int sh = c->q1_shape;
     auto holds = [&](int i) { return nvec <= 64 * kQ1Shapes[i - 1][0] * kQ1Shapes[i - 1][1]; };
     if (sh == 0) {                     // decode: the prefetching (8,8) spills around the multi-sum
-        static const int enc_order[] = {1, 2, 3, 6, 5}, dec_order[] = {1, 2, 3, 4, 5};
+        static const int enc_order[] = {1, 2, 3, 6}, dec_order[] = {1, 2, 3, 4};
         // several rows per 16-wave block in registers + LDS slots (shapes 17 / 18; same-box,
         // profiles/r02/q1_rl_rows/): rows of 4097..8192 vectors in both directions (bf16
         // V = 65536 encode 1.48 -> 1.31 ms, f32 c3 1.241 -> 1.200 ms = 87 % of peak, decode
@@ -4702,11 +4708,6 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
         else if (!DEC && sizeof(LT) == 4 && nvec > 2048 && nvec <= 4096) sh = 17;
         for (int i : DEC ? dec_order : enc_order) {
             if (sh) break;
-            // f32 rows of 4097..8192 vectors: one 16-wave block per CU with rolling
-            // prefetch, (16,8,y) = shape 11, before (8,16,n) (c3 f32: encode 1.33 vs
-            // 1.39 ms; decode, once the buffer-form loads removed its spills, 45.0 vs
-            // 40.9 M sym/s end to end, profiles/r02/q1_dec_shapes/)
-            if (sizeof(LT) == 4 && i == 5 && nvec <= 64 * 16 * 8) { sh = 11; break; }
             if (holds(i)) { sh = i; break; }
         }
         // rows of 8193..16384 vectors: registers + LDS slots (shape 15; same-box, bf16
@@ -4751,17 +4752,13 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
         }
         // measured at V = 128256 f32: encode tiles of (16,8) with the tile-rolling
         // prefetch 1.98 ms vs 2.18 for tiles of (8,8) (shape 13, its (8,8) form: 2.20)
-        if (sh == 0) sh = nvec <= 64 * 16 * 16 ? 9 : (DEC ? 10 : (sizeof(LT) == 4 ? 14 : 8));
+        // (rows of > 16384 vectors that no group form takes)
+        if (sh == 0) sh = DEC ? 10 : (sizeof(LT) == 4 ? 14 : 8);
     }
-    // one 16-wave block per CU (LDS: one table copy), 16 vectors per thread: a bf16 row
-    // of up to 131072 entries in registers (c4's V = 128256) -- one pass, no re-read
-    if (sh == 9 && nvec <= 64 * 16 * 16) return q1_stats_launch<LT, 16, 16, DEC, false, false, 16>(c, a, st);
     if (sh == 10) return q1_stats_launch<LT, 16, 16, DEC, true, false, 16>(c, a, st);   // tiles of 16384
-    if (sh == 11 && nvec <= 64 * 16 * 8) return q1_stats_launch<LT, 16, 8, DEC, false, true, 16>(c, a, st);
-    if (sh == 12 && nvec <= 64 * 16 * 8) return q1_stats_launch<LT, 16, 8, DEC, false, false, 16>(c, a, st);
-    // registers + LDS slots (q1_stats_rl_launch): 15 / 16 one row of <= 16384 vectors per
+    // registers + LDS slots (q1_stats_rl_launch): 15 one row of <= 16384 vectors per
     // block, 17 four rows of <= 4096, 18 two rows of <= 8192
-    if ((sh == 15 || sh == 16) && nvec <= 16384) return q1_stats_rl_launch<LT, DEC>(c, a, st, sh);
+    if (sh == 15 && nvec <= 16384) return q1_stats_rl_launch<LT, DEC>(c, a, st, sh);
     if (sh == 17 && nvec <= 4096) return q1_stats_rl_launch<LT, DEC>(c, a, st, 17);
     if (sh == 18 && nvec <= 8192) return q1_stats_rl_launch<LT, DEC>(c, a, st, 18);
     Q1Group grp;
@@ -4769,21 +4766,18 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
         return q1_stats_group_launch<LT, DEC>(c, a, st, grp);
     if (sh == 22 && nvec <= kQ1WideSlotMaxVec) return q1_wide_launch<LT, DEC>(c, a, st);
     if (sh == 23 && q1_wide_group(c, nvec, &grp)) return q1_wide_group_kernel<LT, DEC>(c, a, st, grp);
-    if (sh == 13) return q1_stats_launch<LT, 8, 8, DEC, true, true>(c, a, st);         // tiles of (8,8,y)
     if (sh == 14) return q1_stats_launch<LT, 16, 8, DEC, true, true, 16>(c, a, st);    // tiles of (16,8,y)
     if (sh == 8) return q1_stats_launch<LT, 8, 8, DEC, true, false>(c, a, st);      // tiles of 4096 vectors
-    // shapes 9, 11, 12, 15..19 with a row too long for them, and 1..7 likewise (kQ1Shapes
-    // describes 1..7 only: a forced 11 / 12 used to index past it)
-    if (sh > 7 || !holds(sh))
+    // shapes 15, 17..23 with a row too long for them, and 1..4 / 6 likewise (kQ1Shapes
+    // describes 1..7 only; lac_set_option refuses the retired shapes)
+    if (sh > 7 || !q1_shape_live(sh) || !holds(sh))
         return fail(LAC_E_ARG, "q1 shape %d does not hold a row of %lld vectors", sh, (long long)nvec);
     switch (sh) {
     case 1: return q1_stats_launch<LT, 1, 4, DEC, false, false>(c, a, st);
     case 2: return q1_stats_launch<LT, 2, 8, DEC, false, false>(c, a, st);
     case 3: return q1_stats_launch<LT, 4, 8, DEC, false, false>(c, a, st);
     case 4: return q1_stats_launch<LT, 8, 8, DEC, false, false>(c, a, st);
-    case 5: return q1_stats_launch<LT, 8, 16, DEC, false, false>(c, a, st);
-    case 6: return q1_stats_launch<LT, 8, 8, DEC, false, true>(c, a, st);
-    default: return q1_stats_launch<LT, 8, 4, DEC, false, true>(c, a, st);
+    default: return q1_stats_launch<LT, 8, 8, DEC, false, true>(c, a, st);   // 6
     }
 }
 
@@ -4993,7 +4987,7 @@ int lac_set_option(lac_ctx *c, int option, int64_t value) {
         c->fine_decode = (int)value;
         return LAC_OK;
     case LAC_OPT_Q1_SHAPE:
-        if (value < 0 || value > 23) return fail(LAC_E_ARG, "bad q1 shape");
+        if (!q1_shape_live((int)value) || value != (int)value) return fail(LAC_E_ARG, "bad or retired q1 shape");
         c->q1_shape = (int)value;
         return LAC_OK;
     case LAC_OPT_MAPPING:

@@ -269,9 +269,9 @@ def test_every_q1_shape_gives_the_same_bits(dtype, V):
     want, wn = c.to_bytes()
     ran = 0
     for sh in range(1, 24):
-        c.set_q1_shape(sh)
         try:
-            c.encode_logits_job(dl, sym)
+            c.set_q1_shape(sh)                # retired shapes are refused here
+            c.encode_logits_job(dl, sym)      # and shapes that cannot hold the row here
         except LacError:
             continue
         got, gn = c.to_bytes()
@@ -319,14 +319,16 @@ def test_paired_row_stats_many_rows(dtype, V, B, steps):
 
 
 def test_q1_shape_option_range():
-    """LAC_OPT_Q1_SHAPE takes 0 (AUTO) .. 23; anything else is refused with LAC_E_ARG."""
+    """LAC_OPT_Q1_SHAPE takes 0 (AUTO) and the live shapes of 1 .. 23; anything else,
+    the retired shapes included (5, 7, 9, 11, 12, 13, 16: AUTO never took them), is
+    refused with LAC_E_ARG."""
     from lac_amd._lib import LacError, LAC_E_ARG
     c = _coder(1024, 4, 40)
-    for bad in (-1, 24, 99):
+    for bad in (-1, 5, 7, 9, 11, 12, 13, 16, 24, 99, 1 << 32 | 1):
         with pytest.raises(LacError) as e:
             c.set_q1_shape(bad)
         assert e.value.code == LAC_E_ARG
-    for ok in (0, 19, 20, 21, 22, 23):
+    for ok in (0, 1, 2, 3, 4, 6, 8, 10, 14, 15, 17, 18, 19, 20, 21, 22, 23):
         c.set_q1_shape(ok)
     c.close()
 

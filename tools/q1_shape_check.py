@@ -22,9 +22,9 @@ sym = torch.from_numpy(_sample(pmf, 5)).to("cuda:0")
 from oracle import oracle as coracle  # noqa: E402
 out, nb, _, rc = coracle.encode_batch(pmf, sym.cpu().numpy(), prec, nthreads=8)
 want = [out[b, :(int(nb[b]) + 7) // 8].tobytes() for b in range(B)]
-for sh in range(0, 16):
-    c.set_q1_shape(sh)
+for sh in range(0, 24):
     try:
+        c.set_q1_shape(sh)
         c.encode_logits_job(dl, sym)
     except LacError as e:
         print(sh, "refused", e)
