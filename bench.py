@@ -103,6 +103,21 @@ def main():
                     help="pmf rows (BASELINE c3, default) or raw logits quantised in-kernel (q1, SURVEY §8(f)1)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher around us: start one rank per GPU (torch.distributed.run as a child
+        # process, before any GPU call here) and relay rank 0's line
+        import torch
+        from lac_amd import launch
+        try:
+            launch.check_devices(args.gpus, os.environ.get("LAC_DIST_BACKEND", "nccl"), torch.cuda.device_count())
+        except launch.LaunchError as e:
+            log(f"bench.py: {e}")
+            sys.exit(2)
+        sys.exit(launch.relay(args.gpus, os.path.abspath(__file__), sys.argv[1:]))
+    if "WORLD_SIZE" in os.environ and args.gpus != int(os.environ["WORLD_SIZE"]) and args.gpus != 1:
+        log(f"bench.py: --gpus {args.gpus} but the launcher started {os.environ['WORLD_SIZE']} ranks")
+        sys.exit(2)
+
     import ctypes as C
 
     import numpy as np
@@ -287,46 +302,52 @@ def main():
     if gatherer:
         parity["gather_ok"] = gather_ok
         parity["gather"] = gather_info
+    # every rank checks its own streams against the CPU oracle (bit-exact bytes and bit
+    # counts); rank 0 then times the oracle on its sample for cpu_baseline
+    from oracle import oracle as coracle
+    S = B if (args.cpu_streams <= 0 or args.cpu_streams > B) else args.cpu_streams
+    if logits_in:
+        S = min(S, 512) if args.cpu_streams <= 0 else S          # q1 oracle is per-row, single-threaded
+        host = pmf[:, :S, :].contiguous()
+        host = host.view(torch.int16).cpu().numpy().view(np.uint16) if ebytes == 2 else host.cpu().numpy()
+    else:
+        host = pmf[:, :S, :].cpu().numpy()
+        host = host.view(np.uint32) if args.pmf_bits == 32 else host.view(np.uint64)
+    hsym = sym[:, :S].cpu().numpy()
+    nthreads = args.cpu_threads if args.cpu_threads > 0 else host_cores()
+    c0 = time.perf_counter()
+    tabs = coracle.q1_quantize(host, P) if logits_in else host
+    out, onb, ost, orc = coracle.encode_batch(tabs, hsym, P, nthreads=nthreads)
+    c1 = time.perf_counter()
+    exact = orc == 0 and rc == 0 and all(
+        int(onb[b]) == int(nbits[b]) and out[b, :(int(onb[b]) + 7) // 8].tobytes() == data[b] for b in range(S))
+    if dist:
+        ok = torch.tensor([1 if exact else 0], device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        exact = bool(ok.item())
+    parity.update({"oracle_streams_checked": S * world, "oracle_ranks_checked": world,
+                   "bit_exact_vs_oracle": bool(exact)})
     if rank == 0:
-        from oracle import oracle as coracle
-        S = B if (args.cpu_streams <= 0 or args.cpu_streams > B) else args.cpu_streams
-        if world > 1:
-            S = min(S, 256)
-        if logits_in:
-            S = min(S, 512) if args.cpu_streams <= 0 else S          # q1 oracle is per-row, single-threaded
-            host = pmf[:, :S, :].contiguous()
-            host = host.view(torch.int16).cpu().numpy().view(np.uint16) if ebytes == 2 else host.cpu().numpy()
-        else:
-            host = pmf[:, :S, :].cpu().numpy()
-            host = host.view(np.uint32) if args.pmf_bits == 32 else host.view(np.uint64)
-        hsym = sym[:, :S].cpu().numpy()
-        nthreads = args.cpu_threads if args.cpu_threads > 0 else host_cores()
-        # cpu_baseline: repeat the same bounded sample until >= --cpu-seconds of CPU
-        # work (the first repetition is also the parity check)
-        reps = 0
-        c0 = time.perf_counter()
-        while True:
-            tabs = coracle.q1_quantize(host, P) if logits_in else host
-            res = coracle.encode_batch(tabs, hsym, P, nthreads=nthreads)
-            if reps == 0:
-                out, onb, ost, orc = res
-            reps += 1
-            c1 = time.perf_counter()
-            if world > 1 or args.cpu_baseline != "on" or c1 - c0 >= args.cpu_seconds:
-                break
-        exact = orc == 0 and rc == 0 and all(
-            int(onb[b]) == int(nbits[b]) and out[b, :(int(onb[b]) + 7) // 8].tobytes() == data[b] for b in range(S))
-        parity.update({"oracle_streams_checked": S, "bit_exact_vs_oracle": bool(exact)})
-        if world == 1 and args.cpu_baseline == "on":
+        if args.cpu_baseline == "on":
+            # cpu_baseline: repeat the same bounded sample until >= --cpu-seconds of CPU
+            # work (the first repetition above was the parity check); other ranks wait
+            reps = 1
+            while c1 - c0 < args.cpu_seconds:
+                tabs = coracle.q1_quantize(host, P) if logits_in else host
+                coracle.encode_batch(tabs, hsym, P, nthreads=nthreads)
+                reps += 1
+                c1 = time.perf_counter()
             what = "q1 quantise (1 thread) + encode" if logits_in else "encode"
             cpu = {"value": reps * S * T / (c1 - c0), "unit": "symbols/s", "cores": nthreads, "kind": "port",
-                   "sample": f"C oracle (oracle/lac_oracle.c) {what} on {S} streams x {T} symbols of the same "
-                             f"inputs, repeated {reps}x, {nthreads} threads, {c1 - c0:.1f}s",
+                   "sample": f"C oracle (oracle/lac_oracle.c) {what} on rank 0's first {S} streams x {T} symbols "
+                             f"of the same inputs, repeated {reps}x, {nthreads} threads, {c1 - c0:.1f}s",
                    "cores_rule": f"nproc semantics: {len(os.sched_getaffinity(0))} CPUs in this process's affinity "
                                  f"mask, OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', 'unset')}, "
                                  f"os.cpu_count()={os.cpu_count()}"}
         avg_bits = float(np.mean(nbits.astype(np.float64))) / T if nbits is not None else None
         parity["bits_per_symbol"] = avg_bits
+    if dist:
+        dist.barrier()                                     # ranks wait out rank 0's baseline
 
     if rank == 0:
         kid = 6 if cnt[6] else (4 if cnt[4] else 0)        # q1_stats, encode_fused, else row_stats
@@ -358,7 +379,12 @@ def main():
             "config": cfg,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-                         "traffic": read_traffic(cfg, kname), "kernel": kname,
+                         "traffic": read_traffic(cfg, kname),
+                         "traffic_source": "not measured in this run: HBM bytes per launch of this kernel from "
+                                           "the committed profiles/pmc_traffic.json (a separate rocprofv3 --pmc "
+                                           "FETCH_SIZE pass of the same config, x2 gfx950 wide-read correction, "
+                                           "tools/pmc_traffic.py); null when no entry matches the config",
+                         "kernel": kname,
                          "kernel_ms_per_launch": rs_launch_ms, "launches": int(cnt[kid]),
                          "bytes_per_launch": alg_bytes,
                          "kernel_ms_per_step": {n: ms[i] / args.steps for n, i in

@@ -202,7 +202,11 @@ int lac_copy_nbits_dev(lac_ctx *ctx, uint64_t *dst_dev, void *stream);
  * bytes(group_bits(bits())), arith_code.py:401-420) for b = 0, 1, ...; *len_dev
  * (device uint64) receives the total length.  dst_dev holds at least
  * streams * (hdr_bytes + 8 * ceil(capacity_bits / 64)) bytes.  Two small launches,
- * asynchronous on `stream`: the multi-GPU gather's payload (lac_amd.dist). */
+ * asynchronous on `stream`: the multi-GPU gather's payload (lac_amd.dist).
+ * LAC_E_ARG for hdr_bytes = 2 when the context's streams can hold 65536 bits or more
+ * (8 * 8 * ceil(capacity_bits / 64) >= 65536: the count would not fit); LAC_E_STATE
+ * unless the last encode call finished the streams (lac_encode_job,
+ * lac_encode_logits_job, lac_encode_finish) and no decode is open. */
 int lac_pack_bits(lac_ctx *ctx, uint8_t *dst_dev, int hdr_bytes, uint64_t *len_dev, void *stream);
 
 /* Synchronise and copy each stream's coder registers l, h (A_to_bin.l/.h,
@@ -222,8 +226,11 @@ int lac_flush_digits(lac_ctx *ctx, int8_t *digits_host, int32_t *count_host, voi
  * [2][streams][cap_words] uint64 (plane A, then plane C; cap_words =
  * ceil(capacity_bits / 64)).  set refuses (LAC_E_ARG, nothing copied) register sets no
  * encoder reaches: l outside [0, 2^(prec+1)), h < l, h - l >= 2^prec, L beyond the
- * capacity, nflush outside [-1, 8] (streams with err set are copied as they are);
- * get refuses a decoding context (LAC_E_STATE).
+ * capacity, nflush outside [-1, 8] (streams with err set are copied as they are), and
+ * planes_host == NULL while a stream has bits written (L > 0: its output words would
+ * be whatever the context held); get and set refuse a decoding context (LAC_E_STATE;
+ * lac_encode_reset first).  A restored context is not finished: lac_pack_bits needs a
+ * lac_encode_finish first.
  * Synchronise `stream`. */
 typedef struct lac_enc_state {
     int64_t l, h;

@@ -286,6 +286,9 @@ class BatchCoder:
         (include/lac.h lac_pack_bits: a header of bit counts, ``hdr_bytes`` = 2 or 4 each,
         then each stream's bytes back to back); ``length`` (a one-element 8-byte integer
         device tensor) receives the packed length.  Asynchronous; no host sync."""
+        if hdr_bytes not in (2, 4) or (hdr_bytes == 2 and self.bits_stride() * 8 >= 1 << 16):
+            raise ValueError(f"hdr_bytes={hdr_bytes}: 2-byte headers need streams of < 65536 bits "
+                             f"(this coder's hold {self.bits_stride() * 8}), else 4")
         need = self.streams * (hdr_bytes + self.bits_stride())
         if out.dtype != _torch().uint8 or not out.is_contiguous() or out.numel() < need or out.device != self.device:
             raise ValueError(f"out must be a contiguous uint8 device tensor of >= {need} bytes on {self.device}")

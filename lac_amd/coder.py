@@ -175,7 +175,7 @@ def _row_of(predictor):
                         "needs CDFPredictor/ProbPredictor-style predictors")
     a = _cdf_array(d)
     if a is not None and a.size:
-        if a.dtype.kind == "i" and a[0] < 0:
+        if a.dtype.kind == "i" and bool((a < 0).any()):     # before the uint64 cast, which would wrap
             raise ValueError("dist is not monotone non-decreasing")
         a = a.astype(np.uint64, copy=False)
         if a.size > 1 and bool((a[1:] < a[:-1]).any()):
@@ -1223,23 +1223,29 @@ def measure_compress(comp, inp, print_every_out=100, print_every_inp=100, save_b
     bit is appended to ``save_bits``.  A progress line ("n -> entropy  bits/tok",
     carriage-return terminated) is printed as each input arrives while the
     output count is a multiple of ``print_every_inp`` (the reference tests the
-    output count there, :409) and after every ``print_every_out`` output bits."""
+    output count there, :409) and after every ``print_every_out`` output bits.
+    The coder reads its input in chunks ahead of the bits it yields, so the
+    output count stands still while a chunk is read: the input side prints at
+    most once per output count (the reference, whose bits interleave with its
+    inputs, prints on each input only while the count sits at a multiple)."""
     if save_bits is None:
         save_bits = []
     n_in = n_out = 0
     last = None
+    printed_at = None                                   # output count of the last input-side line
 
     def progress():
         info = comp.total_encoded_entropy
         print(n_in, "->", info, "   ", info / n_in, " bits/tok ", inp_cb(last), end="        \r")
 
     def inputs():
-        nonlocal n_in, last
+        nonlocal n_in, last, printed_at
         for v in inp:
             yield v
             last = v
             n_in += 1
-            if n_out % print_every_inp == 0:
+            if n_out % print_every_inp == 0 and n_out != printed_at:
+                printed_at = n_out
                 progress()
 
     def outputs(bits):

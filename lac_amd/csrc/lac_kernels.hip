@@ -4059,6 +4059,7 @@ struct lac_ctx {
     uint64_t dstride = 0;
     const uint64_t *dnbits = nullptr;
     int mode = 0;                       // 0 encode, 1 decode
+    int finished = 0;                   // nbits / planeA hold finished streams (a job, lac_encode_finish)
     int path = LAC_PATH_AUTO;           // encode kernel path (lac_set_option)
     int64_t fused_min_streams = 2048;   // AUTO: fused kernel from this many streams
     int64_t chunk_steps = 64;           // split path: steps per row-stats launch
@@ -4937,6 +4938,7 @@ int lac_encode_reset(lac_ctx *c, void *stream) {
     if (!c) return fail(LAC_E_ARG, "ctx is NULL");
     HIPCHK(hipSetDevice(c->device));
     c->mode = 0;
+    c->finished = 0;
     k_enc_reset<<<(unsigned)((c->B + 255) / 256), 256, 0, S(stream)>>>(c->enc, c->B, c->prec);
     CHECK_LAUNCH();
     return LAC_OK;
@@ -4954,13 +4956,17 @@ int lac_encode_rebase(lac_ctx *c, void *stream) {
 int lac_encode(lac_ctx *c, const void *pmf_dev, int64_t step_stride, int64_t stream_stride, const int32_t *sym_dev,
                int64_t steps, uint64_t *trace_dev, void *stream) {
     if (c && c->mode != 0) return fail(LAC_E_STATE, "context is decoding; call lac_encode_reset first");
-    return encode_dispatch(c, pmf_dev, step_stride, stream_stride, sym_dev, steps, trace_dev, stream, 0);
+    const int rc = encode_dispatch(c, pmf_dev, step_stride, stream_stride, sym_dev, steps, trace_dev, stream, 0);
+    if (rc == LAC_OK && steps > 0) c->finished = 0;
+    return rc;
 }
 
 int lac_encode_job(lac_ctx *c, const void *pmf_dev, int64_t step_stride, int64_t stream_stride,
                    const int32_t *sym_dev, int64_t steps, uint64_t *trace_dev, void *stream) {
-    return encode_dispatch(c, pmf_dev, step_stride, stream_stride, sym_dev, steps, trace_dev, stream,
-                           kReset | kFinish);
+    const int rc = encode_dispatch(c, pmf_dev, step_stride, stream_stride, sym_dev, steps, trace_dev, stream,
+                                   kReset | kFinish);
+    if (rc == LAC_OK) c->finished = 1;
+    return rc;
 }
 
 int lac_set_option(lac_ctx *c, int option, int64_t value) {
@@ -5008,6 +5014,7 @@ int lac_encode_finish(lac_ctx *c, void *stream) {
     if (c->mode != 0) return fail(LAC_E_STATE, "context is decoding");
     HIPCHK(hipSetDevice(c->device));
     ProfScope ps(c, KID_FINISH, S(stream));
+    c->finished = 1;
     k_finish<<<(unsigned)((c->B + 255) / 256), 256, 0, S(stream)>>>(c->enc, c->planeA, c->planeC, c->cap_words, c->B,
                                                                    c->prec, c->nbits, c->term);
     CHECK_LAUNCH();
@@ -5078,6 +5085,11 @@ int lac_copy_bits_dev(lac_ctx *c, uint8_t *dst, uint64_t dst_stride, void *strea
 
 int lac_pack_bits(lac_ctx *c, uint8_t *dst, int hdr_bytes, uint64_t *len_dev, void *stream) {
     if (!c || !dst || !len_dev || (hdr_bytes != 2 && hdr_bytes != 4)) return fail(LAC_E_ARG, "bad argument");
+    if (hdr_bytes == 2 && c->cap_words * 64 >= 65536)
+        return fail(LAC_E_ARG, "a 2-byte header holds bit counts below 65536; this context's streams hold up to "
+                               "%llu bits: use 4", (unsigned long long)(c->cap_words * 64));
+    if (c->mode != 0) return fail(LAC_E_STATE, "context is decoding");
+    if (!c->finished) return fail(LAC_E_STATE, "no finished encode to pack (lac_encode_job or lac_encode_finish)");
     HIPCHK(hipSetDevice(c->device));
     if (!c->pack_off) HIPCHK(hipMalloc(&c->pack_off, sizeof(uint64_t) * (c->B > 0 ? c->B : 1)));
     k_pack_scan<<<1, 1024, 0, S(stream)>>>(c->nbits, c->B, hdr_bytes, c->pack_off, dst, len_dev);
@@ -5130,10 +5142,14 @@ int lac_encode_get_state(lac_ctx *c, lac_enc_state *host_out, uint64_t *planes_h
 
 int lac_encode_set_state(lac_ctx *c, const lac_enc_state *host_in, const uint64_t *planes_host, void *stream) {
     if (!c || !host_in) return fail(LAC_E_ARG, "NULL argument");
+    if (c->mode != 0) return fail(LAC_E_STATE, "context is decoding; call lac_encode_reset first");
     const int64_t D = (int64_t)1 << c->prec;
     for (int64_t b = 0; b < c->B; b++) {
         const lac_enc_state &q = host_in[b];
         if (q.err) continue;
+        if (q.L > 0 && !planes_host)
+            return fail(LAC_E_ARG, "stream %lld has %lld bits written: its planes must be restored too",
+                        (long long)b, (long long)q.L);
         if (q.l < 0 || q.l >= 2 * D || q.h < q.l || q.h - q.l >= D || q.L > c->cap_words * 64 || q.nsym < 0 ||
             q.nflush < -1 || q.nflush > 8)
             return fail(LAC_E_ARG, "stream %lld: encoder registers out of range", (long long)b);
@@ -5145,7 +5161,7 @@ int lac_encode_set_state(lac_ctx *c, const lac_enc_state *host_in, const uint64_
         HIPCHK(hipMemcpyAsync(c->planeA, planes_host, n, hipMemcpyHostToDevice, S(stream)));
         HIPCHK(hipMemcpyAsync(c->planeC, planes_host + c->cap_words * c->B, n, hipMemcpyHostToDevice, S(stream)));
     }
-    c->mode = 0;
+    c->finished = 0;
     HIPCHK(hipStreamSynchronize(S(stream)));
     return LAC_OK;
 }
@@ -5251,14 +5267,19 @@ static int logits_encode(lac_ctx *c, const void *logits_dev, int logit_type, int
 int lac_encode_logits_job(lac_ctx *c, const void *logits_dev, int logit_type, int64_t step_stride,
                           int64_t stream_stride, const int32_t *sym_dev, int64_t steps, uint64_t *trace_dev,
                           void *stream) {
-    return logits_encode(c, logits_dev, logit_type, step_stride, stream_stride, sym_dev, steps, trace_dev, stream,
-                         kReset | kFinish);
+    const int rc = logits_encode(c, logits_dev, logit_type, step_stride, stream_stride, sym_dev, steps, trace_dev,
+                                 stream, kReset | kFinish);
+    if (rc == LAC_OK) c->finished = 1;
+    return rc;
 }
 
 int lac_encode_logits(lac_ctx *c, const void *logits_dev, int logit_type, int64_t step_stride,
                       int64_t stream_stride, const int32_t *sym_dev, int64_t steps, uint64_t *trace_dev,
                       void *stream) {
-    return logits_encode(c, logits_dev, logit_type, step_stride, stream_stride, sym_dev, steps, trace_dev, stream, 0);
+    const int rc = logits_encode(c, logits_dev, logit_type, step_stride, stream_stride, sym_dev, steps, trace_dev,
+                                 stream, 0);
+    if (rc == LAC_OK && steps > 0) c->finished = 0;
+    return rc;
 }
 
 int lac_decode_logits_steps(lac_ctx *c, const void *logits_dev, int logit_type, int64_t step_stride,

@@ -250,7 +250,7 @@ class BitstreamGatherer:
         if self.gloo:
             _all_gather(self.meta[i], mine.cpu(), self.group, self.world)
             st["meta"] = self.meta[i].view(self.world, self.META).tolist()
-            st["payload"] = payload.cpu()
+            st["payload"] = payload[:st["meta"][self.rank][0]].cpu()    # the packed bytes only
             self.state[i] = st
             return i
         ev = torch.cuda.Event()

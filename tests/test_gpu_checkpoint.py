@@ -3,6 +3,8 @@ BatchCoder.checkpoint / restore): a job stopped after any encode call continues
 bit for bit -- in a fresh context or in the same one after more symbols were
 coded (rollback).  The one-shot encode_job output is the comparison; it equals
 the oracle in test_gpu_parity.py."""
+import ctypes as C
+
 import numpy as np
 import pytest
 
@@ -87,7 +89,40 @@ def test_checkpoint_refusals(dev):
             c.restore({**ck, "planes": ck["planes"][:, :, :-1]})
         with pytest.raises(ValueError):
             c.restore({**ck, "prec": 31})
+        # registers with bits written but no planes: refused (the context's words would be kept)
+        st = np.ascontiguousarray(ck["state"])
+        assert int(st["L"].max()) > 0
+        rc = c.lib.lac_encode_set_state(c.ctx, st.ctypes.data_as(C.c_void_p), None, c._stream)
+        assert rc != 0
         c.finish()
         c.decode_open()
         with pytest.raises(LacError):
             c.checkpoint()
+        with pytest.raises(LacError):                          # no restore into an open decode
+            c.restore(ck)
+
+
+def test_pack_bits_refusals(dev):
+    """lac_pack_bits packs finished streams only, and only with a header wide enough
+    for the context's capacity (include/lac.h)."""
+    from lac_amd._lib import LacError
+    from lac_amd.batch import BatchCoder
+    V, B, T = 300, 8, 3
+    pmf, sym = _batch(dev, 5, T, B, V)
+    length = torch.zeros(1, dtype=torch.int64, device=dev)
+    with BatchCoder(V, B, prec=48, capacity_bits=70000, device=dev) as c:   # >= 65536 bits per stream
+        out = torch.empty(B * (4 + c.bits_stride()), dtype=torch.uint8, device=dev)
+        c.encode(pmf, sym)
+        with pytest.raises(LacError):                          # not finished
+            c.pack_bits(out, 4, length)
+        c.finish()
+        with pytest.raises(ValueError):                        # 2-byte counts cannot hold 65536+
+            c.pack_bits(out, 2, length)
+        rc = c.lib.lac_pack_bits(c.ctx, C.c_void_p(out.data_ptr()), 2, C.c_void_p(length.data_ptr()), c._stream)
+        assert rc != 0
+        c.pack_bits(out, 4, length)
+        torch.cuda.synchronize()
+        assert int(length.item()) == B * 4 + int(((c.nbits_tensor() + 7) // 8).sum())
+        c.decode_open()
+        with pytest.raises(LacError):                          # decoding
+            c.pack_bits(out, 4, length)
