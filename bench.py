@@ -99,6 +99,7 @@ def main():
     ap.add_argument("--gather", action="store_true",
                     help="run the bitstream gather (lac_amd.dist.BitstreamGatherer) even on one rank: a "
                          "one-rank RCCL group, the gather inside the timed region, parity.gather_ok")
+    ap.add_argument("--gather-batch", type=int, default=8, help="jobs per bitstream exchange (the gatherer's batch)")
     ap.add_argument("--input", default="pmf", choices=("pmf", "logits-bf16", "logits-f32"),
                     help="pmf rows (BASELINE c3, default) or raw logits quantised in-kernel (q1, SURVEY §8(f)1)")
     args = ap.parse_args()
@@ -177,8 +178,8 @@ def main():
         coder.set_block_waves(args.block_waves)
 
     # N > 1: each job's bitstreams go to rank 0 over RCCL, packed and sized to the
-    # payload, asynchronously (overlapping the next job's encode), double-buffered
-    gatherer = BitstreamGatherer(coder) if (world > 1 or args.gather) else None
+    # payload, --gather-batch jobs per exchange, overlapping the next jobs' encodes
+    gatherer = BitstreamGatherer(coder, batch=args.gather_batch) if (world > 1 or args.gather) else None
 
     def job():
         if logits_in:
@@ -190,6 +191,8 @@ def main():
 
     for _ in range(args.warmup):
         job()
+    if gatherer:
+        gatherer.drain()                                   # the timed region holds its own jobs' gathers
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -235,7 +238,8 @@ def main():
         jobs = max(gatherer.jobs, 1)
         gather_info = {"to_rank": 0, "link_bytes_per_job": gatherer.bytes_sent / jobs,
                        "payload_bytes_per_job": gatherer.payload_bytes / jobs,
-                       "header_bytes_per_stream": gatherer.hdr}
+                       "header_bytes_per_stream": gatherer.hdr, "jobs_per_exchange": gatherer.batch,
+                       "host_meta_bytes_per_job": gatherer.meta_bytes / jobs}
     rc, err, err_step = coder.status()
     data, nbits = coder.to_bytes() if rc == 0 else ([], None)
     decode = coder.decode_logits if logits_in else coder.decode
@@ -395,6 +399,8 @@ def main():
             "parity": parity,
         }
         print(json.dumps(line), flush=True)
+    if gatherer:
+        gatherer.close()
     coder.close()
     if dist:
         dist.barrier()

@@ -209,6 +209,25 @@ int lac_copy_nbits_dev(lac_ctx *ctx, uint64_t *dst_dev, void *stream);
  * lac_encode_logits_job, lac_encode_finish) and no decode is open. */
 int lac_pack_bits(lac_ctx *ctx, uint8_t *dst_dev, int hdr_bytes, uint64_t *len_dev, void *stream);
 
+/* lac_pack_bits appending to a buffer of several jobs (the gatherer's per-batch
+ * outbox, lac_amd.dist.BitstreamGatherer): the packed job is written at byte offset
+ * *base_dev of dst_dev (0 when base_dev is NULL; device memory, read by the kernel,
+ * so jobs chain without a host round trip), *end_dev (device) receives base + the
+ * packed length, and *len_out, when not NULL, the packed length -- len_out may be
+ * host memory from lac_host_alloc (its device address), which the host reads once
+ * the launch has completed, with no copy.  A job that would pass dst_bytes writes
+ * nothing: *end_dev = base and *len_out = UINT64_MAX.  Same refusals as
+ * lac_pack_bits. */
+int lac_pack_bits_at(lac_ctx *ctx, uint8_t *dst_dev, uint64_t dst_bytes, int hdr_bytes, const uint64_t *base_dev,
+                     uint64_t *end_dev, uint64_t *len_out, void *stream);
+
+/* Pinned host memory mapped into the device's address space, coherent (kernels'
+ * stores are visible to the host when the launch completes), zero-filled:
+ * *host_out is the host address, *dev_out the address kernels use.  For the few
+ * words the host reads back per job (lac_pack_bits_at's len_out). */
+int lac_host_alloc(uint64_t bytes, void **host_out, void **dev_out);
+int lac_host_free(void *host);
+
 /* Synchronise and copy each stream's coder registers l, h (A_to_bin.l/.h,
  * arith_code.py:161-162); either pointer may be NULL. */
 int lac_encoder_registers(lac_ctx *ctx, int64_t *l_host, int64_t *h_host, void *stream);

@@ -298,6 +298,26 @@ class BatchCoder:
                                      C.c_void_p(length.data_ptr()), self._stream))
         return out, length
 
+    def pack_bits_at(self, out, hdr_bytes, base, end, len_out=None):
+        """pack_bits appended at byte offset ``base[0]`` of ``out`` (include/lac.h
+        lac_pack_bits_at): ``base`` / ``end`` are one-element 8-byte integer device
+        tensors (``base`` may be None: offset 0), ``end`` receives base + the packed
+        length; ``len_out`` is None or a device address (int) of 8 bytes -- e.g. from
+        lac_host_alloc -- for the packed length.  Asynchronous; no host sync."""
+        if hdr_bytes not in (2, 4) or (hdr_bytes == 2 and self.bits_stride() * 8 >= 1 << 16):
+            raise ValueError(f"hdr_bytes={hdr_bytes}: 2-byte headers need streams of < 65536 bits "
+                             f"(this coder's hold {self.bits_stride() * 8}), else 4")
+        if out.dtype != _torch().uint8 or not out.is_contiguous() or out.device != self.device:
+            raise ValueError(f"out must be a contiguous uint8 device tensor on {self.device}")
+        for t in (base, end):
+            if t is not None and (t.numel() < 1 or t.element_size() != 8 or t.device != self.device):
+                raise ValueError("base / end must be 8-byte integer tensors on the coder's device")
+        check(self.lib.lac_pack_bits_at(self.ctx, C.c_void_p(out.data_ptr()), out.numel(), int(hdr_bytes),
+                                        None if base is None else C.c_void_p(base.data_ptr()),
+                                        C.c_void_p(end.data_ptr()),
+                                        None if len_out is None else C.c_void_p(int(len_out)), self._stream))
+        return out
+
     def nbits_tensor(self):
         """Per-stream bit counts as a fresh int64 device tensor (asynchronous copy)."""
         torch = _torch()

@@ -808,46 +808,71 @@ __global__ __launch_bounds__(256) void k_finish(EncState *states, uint64_t *plan
 // trace (A_to_bin.step / run in lac_amd/coder.py) so a stream of any length
 // fits a fixed capacity; the packed output of lac_encode_finish then holds
 // only the tail, but the flush digits are exact.
-// lac_pack_bits: the streams' byte offsets (an exclusive scan of ceil(nbits / 8) behind
-// the header, one 1024-thread block: thread t sums a contiguous run of streams, the
-// block scans the 1024 run sums) and the header of bit counts; then one wave per
-// stream copies its packed bytes (planeA, big-endian, after k_finish).
-__global__ __launch_bounds__(1024) void k_pack_scan(const uint64_t *__restrict__ nbits, int64_t B, int hdr,
-                                                    uint64_t *__restrict__ off, uint8_t *__restrict__ dst,
-                                                    uint64_t *__restrict__ len) {
-    __shared__ uint64_t part[1024];
-    const int t = threadIdx.x;
-    const int64_t per = (B + 1023) / 1024, b0 = t * per, b1 = b0 + per < B ? b0 + per : B;
-    uint64_t sum = 0;
-    for (int64_t b = b0; b < b1; b++) sum += (nbits[b] + 7) >> 3;
-    part[t] = sum;
+// lac_pack_bits(_at), one launch: streams of 1024 per workgroup, one per thread.
+// Every workgroup first sums the byte counts ceil(nbits / 8) of all streams before
+// its own (its 1024 threads stride over them, L2-hot; a DPP wave scan and 16 wave
+// sums per workgroup), then scans its own, so no workgroup waits on another.  Each
+// thread writes its stream's header entry (bit count, `hdr` bytes little endian) and
+// copies its packed bytes (planeA, big-endian bytes, after k_finish) behind the header,
+// all placed at byte `base` of dst (*base_in, 0 when NULL).  *end_out = base + the
+// packed length and *len_out (when not NULL: device or host-mapped memory) = the
+// length, from workgroup 0.  A job that would pass dst_bytes writes nothing:
+// *end_out = base, *len_out = ~0.  (Round 4 used a one-workgroup scan launch and a
+// copy launch: 7 + 4 us plus a dispatch gap per job, profiles/r05/gather/.)
+__device__ inline uint64_t block_excl_sum1024(uint64_t v, uint64_t *wsum, uint64_t &total) {
+    const int w = threadIdx.x >> 6;
+    const uint64_t inc = wave_incl_scan_u64(v);
+    if ((threadIdx.x & 63) == 63) wsum[w] = inc;
     __syncthreads();
-    for (int d = 1; d < 1024; d <<= 1) {                       // Hillis-Steele inclusive scan
-        const uint64_t v = t >= d ? part[t - d] : 0;
-        __syncthreads();
-        part[t] += v;
-        __syncthreads();
+    uint64_t before = 0;
+    total = 0;
+    for (int i = 0; i < 16; i++) {
+        const uint64_t x = wsum[i];
+        before += i < w ? x : 0;
+        total += x;
     }
-    uint64_t o = (uint64_t)hdr * (uint64_t)B + part[t] - sum;
-    for (int64_t b = b0; b < b1; b++) {
-        const uint64_t n = nbits[b];
-        off[b] = o;
-        o += (n + 7) >> 3;
-        for (int i = 0; i < hdr; i++) dst[b * hdr + i] = (uint8_t)(n >> (8 * i));
-    }
-    if (t == 1023) *len = (uint64_t)hdr * (uint64_t)B + part[1023];
+    __syncthreads();
+    return before + inc - v;
 }
 
-__global__ __launch_bounds__(256) void k_pack_copy(const uint64_t *__restrict__ planeA, uint64_t cap_words,
-                                                   const uint64_t *__restrict__ nbits,
-                                                   const uint64_t *__restrict__ off, int64_t B,
-                                                   uint8_t *__restrict__ dst) {
-    const int64_t b = (int64_t)blockIdx.x * 4 + wave_in_block();
-    if (b >= B) return;
-    const uint64_t n = (nbits[b] + 7) >> 3;
-    const uint8_t *src = reinterpret_cast<const uint8_t *>(planeA + (uint64_t)b * cap_words);
-    uint8_t *d = dst + off[b];
-    for (uint64_t i = lane_id(); i < n; i += 64) d[i] = src[i];
+__global__ __launch_bounds__(1024) void k_pack(const uint64_t *__restrict__ planeA, uint64_t cap_words,
+                                               const uint64_t *__restrict__ nbits, int64_t B, int hdr,
+                                               uint8_t *__restrict__ dst, uint64_t dst_bytes,
+                                               const uint64_t *__restrict__ base_in, uint64_t *__restrict__ end_out,
+                                               uint64_t *__restrict__ len_out) {
+    __shared__ uint64_t wsum[16];
+    const int t = threadIdx.x;
+    const int64_t first = (int64_t)blockIdx.x * 1024, b = first + t;
+    const uint64_t base = base_in ? *base_in : 0;
+    // bytes of every stream before this workgroup's, and of all streams (the fit test)
+    uint64_t pre = 0, all = 0;
+    for (int64_t k = t; k < B; k += 1024) {
+        const uint64_t n = (nbits[k] + 7) >> 3;
+        pre += k < first ? n : 0;
+        all += n;
+    }
+    uint64_t tp, ta;
+    (void)block_excl_sum1024(pre, wsum, tp);
+    (void)block_excl_sum1024(all, wsum, ta);
+    const uint64_t nb = b < B ? nbits[b] : 0, n = (nb + 7) >> 3;
+    uint64_t tb;
+    const uint64_t excl = block_excl_sum1024(n, wsum, tb);
+    const uint64_t total = (uint64_t)hdr * (uint64_t)B + ta;
+    const bool fits = base <= dst_bytes && total <= dst_bytes - base;
+    if (blockIdx.x == 0 && t == 0) {
+        *end_out = fits ? base + total : base;
+        if (len_out) *len_out = fits ? total : ~0ull;
+    }
+    if (!fits || b >= B) return;
+    uint8_t *h = dst + base + (uint64_t)b * hdr;
+    for (int i = 0; i < hdr; i++) h[i] = (uint8_t)(nb >> (8 * i));
+    const uint64_t *src = planeA + (uint64_t)b * cap_words;
+    uint8_t *d = dst + base + (uint64_t)hdr * (uint64_t)B + tp + excl;
+    for (uint64_t wi = 0; wi * 8 < n; wi++) {
+        const uint64_t v = src[wi];
+        const uint64_t m = n - wi * 8 < 8 ? n - wi * 8 : 8;
+        for (uint64_t k = 0; k < m; k++) d[wi * 8 + k] = (uint8_t)(v >> (8 * k));
+    }
 }
 
 __global__ void k_enc_rebase(EncState *states, int64_t B) {
@@ -2871,15 +2896,45 @@ __global__ __launch_bounds__(64 * NWB, LAC_Q1_MINW) void k_q1_stats(const LT *__
                     __builtin_amdgcn_sched_barrier(0);         // keep the load after vector j's use
                 }
             };
+            // DEC with 8 vectors: wave_multi_sum32<8>'s butterfly runs as the sums appear
+            // (vectors in the order 0 4 2 6 1 5 3 7, each halving step once both inputs
+            // exist: <= 3 live sums instead of 8, as k_q1_stats_rl) -- with all 8 live
+            // the rolling prefetch spilled at the 128-VGPR cap, so the decode form ran
+            // without it (bf16 c3 decode stats 46-49 vs encode 41 us per step)
+            constexpr bool STREAM = DEC && R == 8;
+            auto pair_halve = [&](int k) {
+                if constexpr (STREAM) {
+                    if (k == 4) sv[0] = halve_pair<0>(sv[0], sv[4]);
+                    if (k == 6) { sv[2] = halve_pair<0>(sv[2], sv[6]); sv[0] = halve_pair<1>(sv[0], sv[2]); }
+                    if (k == 5) sv[1] = halve_pair<0>(sv[1], sv[5]);
+                    if (k == 7) {
+                        sv[3] = halve_pair<0>(sv[3], sv[7]);
+                        sv[1] = halve_pair<1>(sv[1], sv[3]);
+                        sv[0] = halve_pair<2>(sv[0], sv[1]);
+                    }
+                }
+            };
             if (fast) {                                        // row-uniform branch, outside the vector loop
 #pragma unroll
-                for (int j = 0; j < R; j++) { take(j, q1_vec_sum<LT>(x[j], c, true, tabr, loff)); roll(j); }
+                for (int q = 0; q < R; q++) {
+                    const int j = STREAM ? kHalveOrder[q] : q;
+                    take(j, q1_vec_sum<LT>(x[j], c, true, tabr, loff));
+                    pair_halve(j);
+                    roll(j);
+                }
             } else {
 #pragma unroll
-                for (int j = 0; j < R; j++) { take(j, q1_vec_sum<LT>(x[j], c, false, tabr, loff)); roll(j); }
+                for (int q = 0; q < R; q++) {
+                    const int j = STREAM ? kHalveOrder[q] : q;
+                    take(j, q1_vec_sum<LT>(x[j], c, false, tabr, loff));
+                    pair_halve(j);
+                    roll(j);
+                }
             }
             if (DEC) {
-                const uint64_t gsum = wave_multi_sum32<R>(sv);    // group total of index q_index(lane)
+                uint64_t gsum;                                 // group total of index q_index(lane)
+                if constexpr (STREAM) gsum = wave_multi_sum32_tail8(sv[0]);
+                else gsum = wave_multi_sum32<R>(sv);
                 if (lane < R) {
                     const int grp = tile * RW * R + wg + RW * q_index<R>(lane);
                     if (grp * 64 < nvec) atomicAdd(&bins[g][grp / (int)G], (unsigned long long)gsum);
@@ -4089,7 +4144,6 @@ struct lac_ctx {
     int32_t *dprogress = nullptr;       //              [B] decoder progress for the prefetch helpers
     float *q1m = nullptr;               //                [chunk_steps * B] row maxima
     uint64_t *pxch = nullptr;           // paired row stats (shape 19): [2 * cus] maximum words
-    uint64_t *pack_off = nullptr;       // lac_pack_bits: [B] byte offsets of the streams
     int64_t xch_abort = -1;             // word of pxch holding the last row-group launch's abort flag
     // live kernel timing (lac_profile_enable): hipEvent pairs around launches
     bool prof = false;
@@ -4698,8 +4752,11 @@ static int q1_stats(lac_ctx *c, const Q1Args &a, hipStream_t st) {
     const int64_t nvec = c->V / LogitN<LT>::N;
     int sh = c->q1_shape;
     auto holds = [&](int i) { return nvec <= 64 * kQ1Shapes[i - 1][0] * kQ1Shapes[i - 1][1]; };
-    if (sh == 0) {                     // decode: the prefetching (8,8) spills around the multi-sum
-        static const int enc_order[] = {1, 2, 3, 6}, dec_order[] = {1, 2, 3, 4};
+    if (sh == 0) {
+        // both directions take the prefetching (8,8) form 6 at 2049..4096 vectors: its decode
+        // form spilled around the 8-way multi-sum (4 instead, no prefetch) until round 5
+        // streamed the butterfly (127 VGPRs, no spills; profiles/r05/q1dec_pf/)
+        static const int enc_order[] = {1, 2, 3, 6}, dec_order[] = {1, 2, 3, 6};
         // several rows per 16-wave block in registers + LDS slots (shapes 17 / 18; same-box,
         // profiles/r02/q1_rl_rows/): rows of 4097..8192 vectors in both directions (bf16
         // V = 65536 encode 1.48 -> 1.31 ms, f32 c3 1.241 -> 1.200 ms = 87 % of peak, decode
@@ -4928,7 +4985,6 @@ int lac_close(lac_ctx *c) {
     (void)hipFree(c->dprogress);
     (void)hipFree(c->q1m);
     (void)hipFree(c->pxch);
-    (void)hipFree(c->pack_off);
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
     delete c;
     return LAC_OK;
@@ -5083,22 +5139,45 @@ int lac_copy_bits_dev(lac_ctx *c, uint8_t *dst, uint64_t dst_stride, void *strea
     return LAC_OK;
 }
 
-int lac_pack_bits(lac_ctx *c, uint8_t *dst, int hdr_bytes, uint64_t *len_dev, void *stream) {
-    if (!c || !dst || !len_dev || (hdr_bytes != 2 && hdr_bytes != 4)) return fail(LAC_E_ARG, "bad argument");
+int lac_pack_bits_at(lac_ctx *c, uint8_t *dst, uint64_t dst_bytes, int hdr_bytes, const uint64_t *base_dev,
+                     uint64_t *end_dev, uint64_t *len_out, void *stream) {
+    if (!c || !dst || !end_dev || (hdr_bytes != 2 && hdr_bytes != 4)) return fail(LAC_E_ARG, "bad argument");
     if (hdr_bytes == 2 && c->cap_words * 64 >= 65536)
         return fail(LAC_E_ARG, "a 2-byte header holds bit counts below 65536; this context's streams hold up to "
                                "%llu bits: use 4", (unsigned long long)(c->cap_words * 64));
     if (c->mode != 0) return fail(LAC_E_STATE, "context is decoding");
     if (!c->finished) return fail(LAC_E_STATE, "no finished encode to pack (lac_encode_job or lac_encode_finish)");
     HIPCHK(hipSetDevice(c->device));
-    if (!c->pack_off) HIPCHK(hipMalloc(&c->pack_off, sizeof(uint64_t) * (c->B > 0 ? c->B : 1)));
-    k_pack_scan<<<1, 1024, 0, S(stream)>>>(c->nbits, c->B, hdr_bytes, c->pack_off, dst, len_dev);
+    const unsigned blocks = (unsigned)((c->B + 1023) / 1024);
+    k_pack<<<blocks > 0 ? blocks : 1, 1024, 0, S(stream)>>>(c->planeA, c->cap_words, c->nbits, c->B, hdr_bytes, dst,
+                                                            dst_bytes, base_dev, end_dev, len_out);
     CHECK_LAUNCH();
-    if (c->B > 0) {
-        k_pack_copy<<<(unsigned)((c->B + 3) / 4), 256, 0, S(stream)>>>(c->planeA, c->cap_words, c->nbits, c->pack_off,
-                                                                       c->B, dst);
-        CHECK_LAUNCH();
+    return LAC_OK;
+}
+
+int lac_pack_bits(lac_ctx *c, uint8_t *dst, int hdr_bytes, uint64_t *len_dev, void *stream) {
+    if (!len_dev) return fail(LAC_E_ARG, "bad argument");
+    return lac_pack_bits_at(c, dst, ~0ull, hdr_bytes, nullptr, len_dev, nullptr, stream);
+}
+
+int lac_host_alloc(uint64_t bytes, void **host_out, void **dev_out) {
+    if (!host_out || !dev_out || bytes == 0) return fail(LAC_E_ARG, "bad argument");
+    void *h = nullptr;
+    HIPCHK(hipHostMalloc(&h, bytes, hipHostMallocMapped | hipHostMallocCoherent));
+    void *d = nullptr;
+    const hipError_t e = hipHostGetDevicePointer(&d, h, 0);
+    if (e != hipSuccess) {
+        (void)hipHostFree(h);
+        return fail(LAC_E_HIP, "hipHostGetDevicePointer: %s", hipGetErrorString(e));
     }
+    memset(h, 0, bytes);
+    *host_out = h;
+    *dev_out = d;
+    return LAC_OK;
+}
+
+int lac_host_free(void *host) {
+    if (host) HIPCHK(hipHostFree(host));
     return LAC_OK;
 }
 

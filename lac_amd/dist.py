@@ -13,6 +13,8 @@ over xGMI; with ``gloo`` (tests) they are CPU tensors.
 """
 from __future__ import annotations
 
+import collections
+
 
 def shard_range(total_streams: int, rank: int, world: int):
     """Contiguous block of streams owned by ``rank``."""
@@ -152,197 +154,277 @@ def unpack_bitstreams(payload, streams, width, hdr_bytes):
     return out, nb
 
 
+class HostWords:
+    """``n`` int64 words of pinned host memory mapped into the device (liblac's
+    lac_host_alloc, coherent): kernels write them at ``dev_addr(i)``, the host reads
+    ``self[i]`` once the writing launch has completed -- no copy launch."""
+
+    def __init__(self, lib, n):
+        import ctypes as C
+        self.lib, self.n = lib, int(n)
+        h, d = C.c_void_p(), C.c_void_p()
+        from ._lib import check
+        check(lib.lac_host_alloc(8 * self.n, C.byref(h), C.byref(d)))
+        self._h, self._d = h.value, d.value
+        self.words = (C.c_uint64 * self.n).from_address(self._h)
+
+    def dev_addr(self, i):
+        return self._d + 8 * int(i)
+
+    def __getitem__(self, i):
+        return int(self.words[i])
+
+    def close(self):
+        if self._h:
+            self.lib.lac_host_free(self._h)
+            self._h = self._d = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class BitstreamGatherer:
     """Bitstreams of back-to-back compression jobs gathered to one rank, sized to
-    the payload, with no host synchronisation on the GPU's path.
+    the payload, in batches of jobs (the path's one exchange).
 
-    Per job, on every rank (``submit``): the coder's streams are packed on the
-    device into a header of bit counts (2 bytes per stream when the coder's
-    capacity is below 2^16 bits, else 4) plus the streams' bytes back to back
-    (``pack_bitstreams``), and four int64 -- the packed length, the rank's stream
-    count, its slot width and header size -- are all-gathered, asynchronously.
-    Ranks may hold different numbers of streams (uneven shards).  Under nccl the
-    sizes reach the host through a pinned copy on a side stream, so the host
-    waits only for this job's packing, never for the next job's encode, which it
-    has already enqueued.  At the next ``submit`` (or ``drain``) every rank sends
-    exactly its packed bytes to ``root`` and the root receives them (one grouped
-    send/recv batch on the side stream: RCCL over xGMI), ordered after the
-    packing only.  Under nccl the root's own share takes the same batch as a send
-    to itself (``self_p2p``; NCCL group semantics), so a one-rank job runs every
-    line of the RCCL path; gloo has no self-pair, the root copies its share.
-    xGMI carries the payload, the header and 32 bytes per rank -- not a
-    worst-case slot per stream, and not to every rank.
+    Per job (``submit``), on every rank, one small launch pair on the caller's stream
+    packs the coder's finished streams (lac_pack_bits_at: a header of bit counts,
+    2 bytes per stream when the coder's capacity is below 2^16 bits, else 4, then
+    the streams' bytes back to back) and APPENDS them to the current *outbox*, a
+    device buffer of ``batch`` jobs; the kernel itself chains the offset (the previous
+    job's end, in device memory) and writes the job's packed length into pinned,
+    device-mapped host memory.  Nothing else touches the GPU per job: no copy, no
+    collective, no cross-stream wait.
 
-    On the root, ``last`` describes the last finished job (``last_job`` its
-    number, counting from 1) and ``last_unpacked()`` returns its streams as
-    (bits [sum of streams, width], nbits).  A job is finished when its slot is
-    reused (``depth`` jobs later) or by ``drain``.  ``bytes_sent`` /
-    ``payload_bytes`` count what crossed the links and the encoded bytes
-    themselves (bench.py reports both).
+    Per batch, at the ``submit`` after it filled (the next job's encode is already
+    enqueued, so the GPU stays busy while the host works): the host waits for the
+    batch's last pack (which precedes that encode), reads the lengths from the mapped
+    words, exchanges them with every rank over a gloo group on the host (``meta``:
+    job count, streams, slot width, header size and each job's length, per rank; no
+    GPU work), and posts one grouped send/recv batch: every rank sends exactly its
+    packed bytes to ``root``, which receives them (RCCL over xGMI under nccl; the
+    root's own share as a send to itself in the same batch, ``self_p2p``, so a
+    one-rank group runs every line of the path; gloo has no self-pair, the root
+    copies its share).  ``depth`` outboxes rotate: before an outbox is refilled, the
+    caller's stream waits for its batch's sends/receives (long finished by then).
+    One RCCL launch per batch instead of a pack, an all-gather, two copies and a
+    send/recv per job with cross-stream waits between them (the round-4 form cost
+    ~80 us per 1.2 ms job at world 1: every one of those sat in the encode's
+    hardware queue, profiles/r05/gather/).
 
-    Under ``gloo`` (CPU tests, one-GPU rehearsals) the same deferred exchange runs
-    on host tensors; only the streams, events and pinned copies are nccl's.
+    On the root, ``last`` describes the last finished batch (``finished_jobs`` its
+    job numbers, counting from 1; ``last_job`` the newest) and ``last_unpacked(job)``
+    returns one of its jobs' streams as (bits [sum of streams, width], nbits).  A
+    batch is finished when its outbox is reused (``depth`` batches later) or by
+    ``drain``.  ``bytes_sent`` / ``payload_bytes`` count what crossed the links (the
+    other ranks' packed jobs) and the encoded bytes themselves; ``meta_bytes`` what
+    the host exchange carried.
+
+    Under ``gloo`` (CPU tests, one-GPU rehearsals) the same batches run on host
+    tensors; only the device-mapped lengths and RCCL are nccl's.
     """
 
-    META = 4                                                 # int64 per rank: L, streams, width, hdr
+    META = 4                                                 # int64 per rank ahead of the lengths
 
-    def __init__(self, coder, group=None, depth: int = 2, root: int = 0, self_p2p=None):
+    def __init__(self, coder, group=None, batch: int = 8, depth: int = 2, root: int = 0, self_p2p=None):
         import torch
         import torch.distributed as dist
-        self.coder, self.group, self.depth, self.root = coder, group, max(1, int(depth)), int(root)
+        self.coder, self.group, self.root = coder, group, int(root)
+        self.batch, self.depth = max(1, int(batch)), max(1, int(depth))
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.gloo = dist.get_backend(group) == "gloo"
         self.self_p2p = (not self.gloo) if self_p2p is None else bool(self_p2p)
+        # sizes travel between hosts, never through the GPU: the group itself under
+        # gloo, else a gloo group over the same ranks (created collectively, once)
+        if self.gloo:
+            self.meta_group = group
+        else:
+            ranks = dist.get_process_group_ranks(group) if group is not None else list(range(self.world))
+            self.meta_group = dist.new_group(ranks=ranks, backend="gloo")
         self.width = coder.bits_stride()                      # cap_words * 8 bytes per stream
         self.hdr = 2 if self.width * 8 < (1 << 16) else 4
         B, dev = coder.streams, coder.device
-        self.B = B
-        self.cap = B * self.hdr + B * self.width + 1
-        self.io_dev = torch.device("cpu") if self.gloo else torch.device(dev)
-        # per slot the packed payload (a BatchCoder packs its planes directly, lac_pack_bits)
-        # or, for other coders, the copies pack_bitstreams works from
-        if hasattr(coder, "pack_bits"):
-            self.packed = [(torch.empty(self.cap, dtype=torch.uint8, device=dev),
-                            torch.tensor([0, B, self.width, self.hdr], dtype=torch.int64, device=dev))
-                           for _ in range(self.depth)]
-            self.slots = None
-        else:
-            self.packed = None
-            self.slots = [(torch.empty((B, self.width), dtype=torch.uint8, device=dev),
-                           torch.empty((B,), dtype=torch.int64, device=dev)) for _ in range(self.depth)]
-        # root: per slot and rank a receive buffer, (re)sized to the largest payload seen
+        self.B, self.device = B, torch.device(dev)
+        self.job_cap = B * self.hdr + B * self.width
+        self.box_cap = self.batch * self.job_cap
+        self.cuda = self.device.type == "cuda"
+        self.native = hasattr(coder, "pack_bits_at") and self.cuda
+        self.io_dev = torch.device("cpu") if self.gloo else self.device
+        self.boxes = []
+        for _ in range(self.depth):
+            bx = {"buf": torch.empty(max(self.box_cap, 1), dtype=torch.uint8, device=self.device),
+                  "jobs": [], "lens": None, "ends": None, "ev": None, "works": None, "meta": None, "seq": 0}
+            if self.native:
+                bx["ends"] = torch.zeros(self.batch, dtype=torch.int64, device=self.device)
+                bx["lens"] = HostWords(coder.lib, self.batch)
+            else:
+                bx["lens"] = [0] * self.batch
+            self.boxes.append(bx)
+        # root: per outbox and rank a receive buffer, (re)sized to the largest batch seen
         self.recv = [[None] * self.world if self.rank == self.root else None for _ in range(self.depth)]
-        self.meta = [torch.empty(self.world * self.META, dtype=torch.int64, device=self.io_dev)
-                     for _ in range(self.depth)]
-        self.meta_host = [torch.empty(self.world * self.META, dtype=torch.int64).pin_memory()
-                          if not self.gloo and torch.cuda.is_available()
-                          else torch.empty(self.world * self.META, dtype=torch.int64) for _ in range(self.depth)]
-        self._shape_meta = torch.tensor([B, self.width, self.hdr], dtype=torch.int64, device=dev)
-        self.state = [None] * self.depth                        # per slot: dict of the job in flight
-        self.side = torch.cuda.Stream(device=dev) if not self.gloo else None
+        self.side = torch.cuda.Stream(device=self.device) if self.cuda and not self.gloo else None
+        self.cur = 0
+        self.pending = None
+        self.seq = 0
         self.k = 0
         self.last = None
         self.last_job = 0
+        self.finished_jobs = []
+        self.recent = collections.deque(maxlen=self.depth)       # root: finished batches still held
         self.bytes_sent = 0
         self.payload_bytes = 0
+        self.meta_bytes = 0
         self.jobs = 0
 
     # -- per job
     def submit(self):
-        """Queue the coder's current output for the root; returns the job's slot."""
+        """Append the coder's current (finished) output to the current batch; returns
+        the job's number (counting from 1)."""
         import torch
-        import torch.distributed as dist
-        i = self.k % self.depth
         self.k += 1
-        self._finish(i)                                         # slot i's previous job, if any
-        self._send_pending()                                    # the jobs queued since: their exact sends
-        if self.packed is not None:                              # BatchCoder: one pack on the device,
-            payload, mine = self.packed[i]                       # its length straight into the sizes row
-            self.coder.pack_bits(payload, self.hdr, mine[:1])    # (on the caller's stream)
+        if self.pending is not None:                             # a full batch: exchange it now
+            i, self.pending = self.pending, None
+            self._post(i)
+        i = self.cur
+        bx = self.boxes[i]
+        if bx["works"] is not None:
+            self._finish(i)                                      # its previous batch, before packing over it
+        n = len(bx["jobs"])
+        if self.native:                                          # one pack on the device, chained offsets
+            self.coder.pack_bits_at(bx["buf"], self.hdr, None if n == 0 else bx["ends"][n - 1:n],
+                                    bx["ends"][n:n + 1], bx["lens"].dev_addr(n))
         else:                                                    # any coder with the copy accessors
-            bits, nbits = self.slots[i]
+            bits = torch.empty((self.B, self.width), dtype=torch.uint8, device=self.device)
+            nbits = torch.empty((self.B,), dtype=torch.int64, device=self.device)
             self.coder.copy_bits_into(bits)
             self.coder.copy_nbits_into(nbits)
             payload, L = pack_bitstreams(bits, nbits, self.hdr)
-            mine = torch.cat([L.to(torch.int64).reshape(1), self._shape_meta])
-        st = {"payload": payload, "job": self.k}
-        if self.gloo:
-            _all_gather(self.meta[i], mine.cpu(), self.group, self.world)
-            st["meta"] = self.meta[i].view(self.world, self.META).tolist()
-            st["payload"] = payload[:st["meta"][self.rank][0]].cpu()    # the packed bytes only
-            self.state[i] = st
-            return i
-        ev = torch.cuda.Event()
-        ev.record()                                             # packing done (caller's stream)
-        work = dist.all_gather_into_tensor(self.meta[i], mine, group=self.group, async_op=True)
-        with torch.cuda.stream(self.side):
-            self.side.wait_event(ev)
-            work.wait()                                         # the side stream waits for the sizes
-            self.meta_host[i].copy_(self.meta[i], non_blocking=True)
-            st["meta_ready"] = torch.cuda.Event()
-            st["meta_ready"].record(self.side)
-        st["packed"] = ev
-        self.state[i] = st
-        return i
+            L = int(L)
+            off = sum(bx["lens"][:n])
+            bx["buf"][off:off + L].copy_(payload[:L])
+            bx["lens"][n] = L
+        bx["jobs"].append(self.k)
+        if len(bx["jobs"]) == self.batch:
+            self._close_box(i)
+            self.pending = i                                     # posted at the next submit (or drain)
+        return self.k
 
-    def _send_pending(self):
-        """Post the sends of every queued job, oldest first (point-to-point order
-        must match between each rank and the root)."""
-        for _, i in sorted((st["job"], i) for i, st in enumerate(self.state) if st is not None):
-            self._send(i)
+    def _close_box(self, i):
+        import torch
+        bx = self.boxes[i]
+        if self.cuda:
+            bx["ev"] = torch.cuda.Event()
+            bx["ev"].record()                                    # the box's last pack (caller's stream)
+        self.cur = (i + 1) % self.depth
 
     def _recv_buffer(self, i, r, n):
         import torch
         buf = self.recv[i][r]
         if buf is None or buf.numel() < n:
-            buf = self.recv[i][r] = torch.empty(max(n, self.cap), dtype=torch.uint8, device=self.io_dev)
+            buf = self.recv[i][r] = torch.empty(max(n, self.job_cap), dtype=torch.uint8, device=self.io_dev)
         return buf
 
-    def _send(self, i):
-        """Post job i's exact-size send (every rank) / receives (root), once its
-        sizes are on the host."""
+    def _post(self, i):
+        """Box i's exchange: sizes over the host, then one grouped send/recv batch."""
         import torch
         import torch.distributed as dist
-        st = self.state[i]
-        if st is None or "works" in st:
-            return
-        if "meta" not in st:
-            st["meta_ready"].synchronize()                      # this job's packing + size gather only
-            st["meta"] = self.meta_host[i].view(self.world, self.META).tolist()
-        lens = [m[0] for m in st["meta"]]
+        bx = self.boxes[i]
+        if bx["ev"] is not None:
+            bx["ev"].synchronize()                               # its last pack only (not the next encode)
+        n = len(bx["jobs"])
+        lens = [bx["lens"][j] for j in range(n)]
+        if any(v >= 1 << 63 for v in lens):
+            raise RuntimeError("a packed job did not fit its outbox slot")
+        mine = torch.zeros(self.META + self.batch, dtype=torch.int64)
+        mine[:self.META] = torch.tensor([n, self.B, self.width, self.hdr])
+        mine[self.META:self.META + n] = torch.tensor(lens, dtype=torch.int64)
+        meta = torch.empty((self.world, self.META + self.batch), dtype=torch.int64)
+        _all_gather(meta.view(-1), mine, self.meta_group, self.world)
+        rows = meta.tolist()
+        if any(row[0] != n for row in rows):
+            raise RuntimeError(f"ranks disagree on the batch's job count: {[row[0] for row in rows]}")
+        tot = [sum(row[self.META:self.META + n]) for row in rows]
         ops = []
         if self.rank == self.root:
             for r in range(self.world):
                 if r != self.root or self.self_p2p:
-                    ops.append(dist.P2POp(dist.irecv, self._recv_buffer(i, r, lens[r])[:lens[r]], r,
-                                          group=self.group))
+                    ops.append(dist.P2POp(dist.irecv, self._recv_buffer(i, r, tot[r])[:tot[r]], r, group=self.group))
         if self.rank != self.root or self.self_p2p:
-            ops.append(dist.P2POp(dist.isend, st["payload"][:lens[self.rank]], self.root, group=self.group))
-        ctx = torch.cuda.stream(self.side) if not self.gloo else _nullctx()
+            src = bx["buf"][:tot[self.rank]]
+            if self.gloo and src.is_cuda:
+                src = src.cpu()
+            ops.append(dist.P2POp(dist.isend, src, self.root, group=self.group))
+        ctx = torch.cuda.stream(self.side) if self.side is not None else _nullctx()
         with ctx:
-            if not self.gloo:
-                self.side.wait_event(st["packed"])
-            st["works"] = dist.batch_isend_irecv(ops) if ops else []
-        if self.rank == self.root and not self.self_p2p:        # the root's own share: a local copy
-            buf = self._recv_buffer(i, self.root, lens[self.root])
-            buf[:lens[self.root]].copy_(st["payload"][:lens[self.root]], non_blocking=True)
-        self.bytes_sent += sum(lens) - lens[self.root] + 8 * self.META * self.world
-        self.payload_bytes += sum(lens) - sum(m[1] * m[3] for m in st["meta"])
-        self.jobs += 1
+            bx["works"] = dist.batch_isend_irecv(ops) if ops else []
+        if self.rank == self.root and not self.self_p2p:         # the root's own share: a local copy
+            buf = self._recv_buffer(i, self.root, tot[self.root])
+            buf[:tot[self.root]].copy_(bx["buf"][:tot[self.root]], non_blocking=True)
+        bx["meta"] = rows
+        self.seq += 1
+        bx["seq"] = self.seq
+        self.bytes_sent += sum(tot) - tot[self.root]
+        self.payload_bytes += sum(tot) - sum(row[0] * row[1] * row[3] for row in rows)
+        self.meta_bytes += meta.numel() * 8
+        self.jobs += n
 
     def _finish(self, i):
-        import torch
-        st = self.state[i]
-        if st is None:
+        bx = self.boxes[i]
+        if bx["works"] is None:
             return
-        self._send_pending()                                    # older jobs first, then this one
-        # the caller's stream waits for this job's sends and receives only (its payload
-        # slot is about to be reused; the root's received bytes are then visible) -- not
-        # for the whole side stream, which already holds later jobs' size exchanges: that
-        # wait cost ~60 us of cross-queue hops per job (profiles/r04/gather/)
-        for w in st["works"]:
+        # the caller's stream waits for this batch's sends / receives only (its outbox is
+        # about to be refilled; the root's received bytes are then visible)
+        for w in bx["works"]:
             w.wait()
         if self.rank == self.root:
-            self.last = [(self.recv[i][r], m[0], m[1], m[2], m[3]) for r, m in enumerate(st["meta"])]
-            self.last_job = st["job"]
-        self.state[i] = None
+            self.last = {"jobs": list(bx["jobs"]), "meta": bx["meta"], "bufs": list(self.recv[i])}
+            self.recent.append(self.last)
+            self.finished_jobs = [j for b in self.recent for j in b["jobs"]]
+            self.last_job = bx["jobs"][-1]
+        bx.update(jobs=[], works=None, ev=None, meta=None)
 
     def drain(self):
-        """Complete every job in flight (the caller's stream waits for them)."""
-        self._send_pending()
-        for _, j in sorted((st["job"], j) for j, st in enumerate(self.state) if st is not None):
+        """Exchange every job submitted so far and complete every batch in flight (the
+        caller's stream waits for them)."""
+        if self.pending is not None:
+            i, self.pending = self.pending, None
+            self._post(i)
+        i = self.cur
+        if self.boxes[i]["jobs"] and self.boxes[i]["works"] is None:   # a part-filled batch
+            self._close_box(i)
+            self._post(i)
+        for _, j in sorted((bx["seq"], j) for j, bx in enumerate(self.boxes) if bx["works"] is not None):
             self._finish(j)
         return self.last
 
-    def last_unpacked(self):
-        """Root: the last finished job's streams, rank by rank, as (bits [streams,
-        width], nbits [streams]) with width the widest rank's slot."""
+    def last_unpacked(self, job=None):
+        """Root: one job of the finished batches still held (``finished_jobs``; default
+        the newest), rank by rank, as (bits [streams, width], nbits [streams]) with width
+        the widest rank's slot.  A batch's bytes stay until its outbox is exchanged
+        again, so read them after the ``submit`` / ``drain`` that finished it."""
         import torch
-        parts = [unpack_bitstreams(p[:n], b, w, h) for p, n, b, w, h in self.last]
+        job = self.last_job if job is None else job
+        last = next((b for b in self.recent if job in b["jobs"]), None)
+        if last is None:
+            raise KeyError(f"job {job} is not among the finished batches held ({self.finished_jobs})")
+        q = last["jobs"].index(job)
+        parts = []
+        for r, row in enumerate(last["meta"]):
+            off = sum(row[self.META:self.META + q])
+            L = row[self.META + q]
+            parts.append(unpack_bitstreams(last["bufs"][r][off:off + L], row[1], row[2], row[3]))
         W = max(p[0].shape[1] for p in parts)
         bits = [torch.nn.functional.pad(p[0], (0, W - p[0].shape[1])) for p in parts]
         return torch.cat(bits), torch.cat([p[1] for p in parts])
+
+    def close(self):
+        for bx in self.boxes:
+            if isinstance(bx["lens"], HostWords):
+                bx["lens"].close()
 
 
 class _nullctx:

@@ -92,34 +92,41 @@ class _FakeCoder:
         out.copy_(self.nbits)
 
 
-def _gatherer_worker(rank, world, port, q, shards, stride, jobs, depth):
+def _record(g, seen):
+    """Root: every job of the batches finished since the last call, once."""
+    for j in g.finished_jobs:
+        if not seen or j > seen[-1][0]:
+            b, n = g.last_unpacked(j)
+            seen.append((j, b.tolist(), n.tolist()))
+
+
+def _gatherer_worker(rank, world, port, q, shards, stride, jobs, batch, depth):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     coder = _FakeCoder(shards[rank], stride, rank)
-    g = BitstreamGatherer(coder, depth=depth)
-    seen = []
-    for j in range(1, jobs + 1):                         # more jobs than slots: slots are reused
+    g = BitstreamGatherer(coder, batch=batch, depth=depth)
+    seen, when = [], []
+    for j in range(1, jobs + 1):                         # more batches than outboxes: outboxes are reused
         coder.new_job(j)
         g.submit()
-        if rank == 0 and g.last is not None:
-            b, n = g.last_unpacked()
-            seen.append((g.last_job, b.tolist(), n.tolist()))
+        if rank == 0:
+            _record(g, seen)
+            when.append(g.last_job)
     g.drain()
     if rank == 0:
-        b, n = g.last_unpacked()
-        seen.append((g.last_job, b.tolist(), n.tolist()))
-    q.put((rank, seen, g.bytes_sent, g.payload_bytes, g.jobs, g.hdr))
+        _record(g, seen)
+    q.put((rank, seen, g.bytes_sent, g.payload_bytes, g.jobs, g.hdr, when))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def _run_gatherer(shards, stride, jobs, depth=2):
+def _run_gatherer(shards, stride, jobs, batch=2, depth=2):
     world = len(shards)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_gatherer_worker, args=(r, world, port, q, shards, stride, jobs, depth))
+    ps = [ctx.Process(target=_gatherer_worker, args=(r, world, port, q, shards, stride, jobs, batch, depth))
           for r in range(world)]
     for p in ps:
         p.start()
@@ -130,12 +137,16 @@ def _run_gatherer(shards, stride, jobs, depth=2):
     return res
 
 
-def _check_root(res, shards, stride, jobs, depth=2):
-    """The root saw every job exactly when its slot came round (job j after
-    submitting job j + depth) and once more for the last job after drain(); each
-    holds every rank's streams, bytes and bit counts, exactly."""
-    seen = res[0][0]
-    assert [s[0] for s in seen] == list(range(1, jobs - depth + 1)) + [jobs]
+def _check_root(res, shards, stride, jobs, batch=2, depth=2):
+    """The root saw every job exactly once, batch by batch: a batch of `batch` jobs is
+    exchanged at the submit after it filled and finished when its outbox comes round
+    again (`depth` batches later) or at drain(); each job holds every rank's
+    streams, bytes and bit counts, exactly."""
+    seen, when = res[0][0], res[0][5]
+    assert [s[0] for s in seen] == list(range(1, jobs + 1))
+    for k, last in enumerate(when, start=1):             # after submitting job k: job k's batch
+        done = max(0, (k - 1) // batch - depth + 1)      # reuses an outbox, finishing the batch
+        assert last == done * batch, (k, last)           # that held it depth batches earlier
     for j, bits, nbits in seen:
         want = [_FakeCoder.job_data(shards[r], stride, r, j) for r in range(len(shards))]
         assert nbits == [int(x) for _, n in want for x in n]
@@ -145,23 +156,24 @@ def _check_root(res, shards, stride, jobs, depth=2):
             assert got[:nb] == row[:nb] and not any(got[nb:])   # exactly the stream's bytes
 
 
-def test_bitstream_gatherer_gloo_world2():
-    """Jobs through the payload-sized gather to rank 0: the root holds every
+@pytest.mark.parametrize("batch,depth", [(1, 2), (2, 2), (8, 2)])
+def test_bitstream_gatherer_gloo_world2(batch, depth):
+    """Jobs through the payload-sized, batched gather to rank 0: the root holds every
     stream's bytes and bit count, exactly; 2-byte headers (capacity < 2^16 bits)."""
-    res = _run_gatherer([3, 3], 24, 5)
-    _check_root(res, [3, 3], 24, 5)
+    res = _run_gatherer([3, 3], 24, 5, batch, depth)
+    _check_root(res, [3, 3], 24, 5, batch, depth)
     assert res[0][4] == 2
 
 
-@pytest.mark.parametrize("shards,jobs,depth", [([3, 0, 5, 2], 7, 2), ([1, 2, 2, 2, 2, 2, 2, 2], 6, 3),
-                                               ([4096 // 8] * 8, 3, 2)])
-def test_bitstream_gatherer_gloo_world4_world8_uneven(shards, jobs, depth):
+@pytest.mark.parametrize("shards,jobs,batch,depth", [([3, 0, 5, 2], 7, 2, 2), ([1, 2, 2, 2, 2, 2, 2, 2], 6, 1, 3),
+                                                     ([4096 // 8] * 8, 5, 2, 2), ([1, 2, 2, 2, 2, 2, 2, 2], 7, 3, 2)])
+def test_bitstream_gatherer_gloo_world4_world8_uneven(shards, jobs, batch, depth):
     """World 4 and 8 (the c5 node), uneven shards (one rank with no streams, 15
-    streams over 8 ranks), more jobs than slots at depth 2 and 3: seven senders,
-    the root's receive order, slot reuse -- the deferred path RCCL takes, minus
-    its streams and events."""
-    res = _run_gatherer(shards, 40, jobs, depth)
-    _check_root(res, shards, 40, jobs, depth)
+    streams over 8 ranks), more batches than outboxes at depth 2 and 3, part-filled
+    last batches: seven senders, the root's receive order, outbox reuse -- the path
+    RCCL takes, minus its streams and device-mapped lengths."""
+    res = _run_gatherer(shards, 40, jobs, batch, depth)
+    _check_root(res, shards, 40, jobs, batch, depth)
 
 
 def test_bitstream_gatherer_long_job_sized_to_payload():
@@ -169,8 +181,8 @@ def test_bitstream_gatherer_long_job_sized_to_payload():
     links per job stays within 1.2x the encoded bytes, where
     the fixed-width slots of round 2 moved the whole capacity to every rank."""
     stride = (4096 * 50 + 256) // 8
-    res = _run_gatherer([6, 6], stride, 3)
-    _check_root(res, [6, 6], stride, 3)
+    res = _run_gatherer([6, 6], stride, 3, 2, 2)
+    _check_root(res, [6, 6], stride, 3, 2, 2)
     sent = res[0][1]                                    # (every rank counts the whole job)
     payload = res[0][2]
     assert res[0][4] == 4 and payload > 0 and sent <= 1.2 * payload, (sent, payload)

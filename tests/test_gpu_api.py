@@ -371,11 +371,25 @@ def test_llama_ac_bits_match_reference_fixture(case):
     from fake_llm import FakeLlama
     from lac_amd.coder import AC, group_bits
     from lac_amd.llm import Llama_AC
-    llm = FakeLlama(case["vocab"], case["n_ctx"], case["seed"])
+    llm = FakeLlama(case["vocab"], case["n_ctx"], case["seed"], scale=case.get("scale", 3.0))
     ac = AC(Llama_AC(llm), case["prec"])
     bits = list(ac.to_bin.bits(case["tokens"]))
     assert len(bits) == case["exact_L"] and bytes(group_bits(iter(bits))).hex() == case["exact_bytes"]
     assert list(ac.from_bin.run(bits, stop=0, n=len(case["tokens"]))) == case["tokens"]
+
+
+@pytest.mark.parametrize("case", load_golden("llama_cases.json")["refuse"], ids=lambda c: c["name"])
+def test_llama_ac_refuses_rows_whose_fudge_decision_differs(case):
+    """Rows where the reference's minp (0: zero CDF steps) and the table's smallest
+    positive entry (>= 2^12) give different fudged_dist decisions at some width
+    (tests/golden/llama_cases.json "refuse"): the GPU coder raises ValueError instead
+    of coding bits that differ from the reference's."""
+    from fake_llm import HeadLlama
+    from lac_amd.coder import AC
+    from lac_amd.llm import Llama_AC
+    ac = AC(Llama_AC(HeadLlama(case["vocab"], case["n_ctx"], case["heads"], case["floor"])), case["prec"])
+    with pytest.raises(ValueError, match="minp"):
+        list(ac.to_bin.bits(case["tokens"]))
 
 
 def _static_case(V=300, n=10000, seed=7):

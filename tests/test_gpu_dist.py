@@ -3,8 +3,9 @@ the GPU, with a real BatchCoder: a one-rank nccl group (RCCL refuses two ranks
 on one GPU -- "Duplicate GPU detected", tools/nccl_probe.py -- and the pool's
 boxes have one MI355X).  Under nccl the root's own share is a P2P send to
 itself in the same batch as every other rank's, so this runs every line of the
-nccl path: the asynchronous all-gather of the sizes, the side stream and its
-events, the pinned copy, batch_isend_irecv, and slot reuse at depth 2 and 3.
+nccl path: packing into batched outboxes with device-chained offsets and lengths
+in device-mapped host words, the sizes over the host (gloo), the side stream,
+batch_isend_irecv, and outbox reuse at depth 2 and 3.
 The multi-rank ordering is covered by the gloo world-2/4/8 tests (test_dist.py),
 which take the same deferred path."""
 import numpy as np
@@ -34,26 +35,32 @@ def _job(coder, j, T, B, V):
     return coder.bits_tensor().clone(), coder.nbits_tensor().clone(), pmf, sym
 
 
-@pytest.mark.parametrize("depth,jobs", [(2, 5), (3, 7)])
-def test_rccl_gatherer_world1_real_coder(nccl_world1, depth, jobs):
+@pytest.mark.parametrize("batch,depth,jobs", [(1, 2, 5), (2, 2, 7), (3, 3, 11), (8, 2, 5)])
+def test_rccl_gatherer_world1_real_coder(nccl_world1, batch, depth, jobs):
     from lac_amd.batch import BatchCoder
     from lac_amd.dist import BitstreamGatherer
     V, B, T = 1000, 96, 10
     coder = BatchCoder(V, B, prec=48, capacity_bits=T * 50 + 256, device=nccl_world1)
-    g = BitstreamGatherer(coder, depth=depth)
-    assert not g.gloo and g.self_p2p
-    made, seen = [], []
+    g = BitstreamGatherer(coder, batch=batch, depth=depth)
+    assert not g.gloo and g.self_p2p and g.native
+    made, seen, when = [], [], []
+
+    def record():
+        for j in g.finished_jobs:
+            if not seen or j > seen[-1][0]:
+                b, n = g.last_unpacked(j)
+                seen.append((j, b.clone(), n.clone()))
     for j in range(jobs):
         bits, nbits, _, _ = _job(coder, j, T, B, V)
         made.append((bits, nbits))
         g.submit()                                   # the next job's encode is enqueued behind it
-        if g.last is not None:
-            b, n = g.last_unpacked()
-            seen.append((g.last_job, b.clone(), n.clone()))
+        record()
+        when.append(g.last_job)
     g.drain()
-    b, n = g.last_unpacked()
-    seen.append((g.last_job, b, n))
-    assert [s[0] for s in seen] == list(range(1, jobs - depth + 1)) + [jobs]
+    record()
+    assert [s[0] for s in seen] == list(range(1, jobs + 1))
+    for k, last in enumerate(when, start=1):
+        assert last == max(0, (k - 1) // batch - depth + 1) * batch, (k, last)
     for j, b, n in seen:
         want_b, want_n = made[j - 1]
         assert torch.equal(n, want_n)
@@ -61,6 +68,38 @@ def test_rccl_gatherer_world1_real_coder(nccl_world1, depth, jobs):
         for r in range(B):
             assert torch.equal(b[r, :nb[r]], want_b[r, :nb[r]]) and not b[r, nb[r]:].any()
     assert g.jobs == jobs and g.payload_bytes > 0
+    g.close()
+    coder.close()
+
+
+def test_pack_bits_at_chains_jobs(nccl_world1):
+    """lac_pack_bits_at appends jobs back to back through device-held offsets and writes
+    each length into device-mapped host words (lac_host_alloc); a job that does not
+    fit writes nothing and reports UINT64_MAX."""
+    from lac_amd.batch import BatchCoder
+    from lac_amd.dist import HostWords, pack_bitstreams
+    V, B, T = 1000, 77, 6
+    coder = BatchCoder(V, B, prec=48, capacity_bits=T * 50 + 256, device=nccl_world1)
+    words = HostWords(coder.lib, 4)
+    ends = torch.zeros(4, dtype=torch.int64, device=nccl_world1)
+    cap = 3 * B * (2 + coder.bits_stride())
+    out = torch.full((cap,), 0xCD, dtype=torch.uint8, device=nccl_world1)
+    want = []
+    for k in range(3):
+        bits, nbits, _, _ = _job(coder, 40 + k, T, B, V)
+        p, L = pack_bitstreams(bits, nbits, 2)
+        want.append(p[:int(L)].clone())
+        coder.pack_bits_at(out, 2, None if k == 0 else ends[k - 1:k], ends[k:k + 1], words.dev_addr(k))
+    torch.cuda.synchronize()
+    lens = [words[k] for k in range(3)]
+    assert lens == [w.numel() for w in want]
+    assert ends[:3].tolist() == [sum(lens[:k + 1]) for k in range(3)]
+    assert torch.equal(out[:sum(lens)], torch.cat(want))
+    small = torch.zeros(10, dtype=torch.uint8, device=nccl_world1)
+    coder.pack_bits_at(small, 2, None, ends[3:4], words.dev_addr(3))
+    torch.cuda.synchronize()
+    assert words[3] == (1 << 64) - 1 and int(ends[3]) == 0 and not small.any()
+    words.close()
     coder.close()
 
 

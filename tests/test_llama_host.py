@@ -12,19 +12,28 @@ import numpy as np
 import pytest
 
 from conftest import load_golden
-from fake_llm import FakeLlama
+from fake_llm import FakeLlama, HeadLlama
 
 CASES = load_golden("llama_cases.json")["cases"]
+REFUSE = load_golden("llama_cases.json")["refuse"]
+
+
+def _llm(case):
+    if "heads" in case:
+        return HeadLlama(case["vocab"], case["n_ctx"], case["heads"], case["floor"])
+    return FakeLlama(case["vocab"], case["n_ctx"], case["seed"], scale=case.get("scale", 3.0))
 
 
 def _sha(b):
     return hashlib.sha256(b).hexdigest()
 
 
-@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+@pytest.mark.parametrize("case", CASES + REFUSE, ids=[c["name"] for c in CASES + REFUSE])
 def test_llama_ac_tables_match_reference(case):
+    """Logits, int64 CDFs, minp (zeros included: the peaky cases' rows have zero CDF
+    steps and minp 0) and window, step by step, equal the reference adapter's."""
     from lac_amd.llm import Llama_AC, quantise_logits
-    llm = FakeLlama(case["vocab"], case["n_ctx"], case["seed"])
+    llm = _llm(case)
     p = Llama_AC(llm)
     for i, (t, want) in enumerate(zip(case["tokens"], case["steps"])):
         logits = np.asarray(llm._scores[-1], dtype=np.float32)
@@ -36,15 +45,59 @@ def test_llama_ac_tables_match_reference(case):
         if "cdf" in want:
             assert [int(x) for x in cdf] == want["cdf"], i
         p.accept(t)
-    assert max(s["window"] for s in case["steps"]) == case["n_ctx"] - 1     # the window wrapped
+    assert max(s["window"] for s in case["steps"]) == min(case["n_ctx"] - 1, len(case["tokens"]))
+
+
+def test_peaky_cases_have_zero_steps():
+    """The fixture covers the reference's always-fudged branch: rows whose float64
+    cumsum absorbed entries (zero CDF steps), so Llama_AC.minp == 0 and
+    fudged_dist fudges at every width (arith_code.py:84)."""
+    peaky = [c for c in CASES if c.get("scale", 3.0) >= 12]
+    assert len(peaky) == 2 and {c["vocab"] for c in peaky} == {1000, 32000}
+    for c in peaky:
+        assert c["zero_step_rows"] == len(c["tokens"]) and all(s["minp"] == 0 for s in c["steps"])
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_fudge_decisions_agree_on_reference_rows(case):
+    """Every recorded row's declared minp (the reference's) and its smallest positive
+    entry give the same fudge decision at every width: the build codes them."""
+    from lac_amd.coder import fudge_decisions_agree
+    from lac_amd.llm import Llama_AC
+    p = Llama_AC(_llm(case))
+    for t, want in zip(case["tokens"], case["steps"]):
+        r = p.pmf_row()
+        assert p.minp == want["minp"]
+        assert fudge_decisions_agree(int(r.sum(dtype=object)), p.minp, int(r[r > 0].min()), case["prec"])
+        p.accept(t)
+
+
+@pytest.mark.parametrize("case", REFUSE, ids=[c["name"] for c in REFUSE])
+def test_refusal_rows(case):
+    """Rows with zero steps whose every positive entry is >= 2^12 (HeadLlama): the
+    reference (minp 0) fudges at every width, the table's smallest positive entry
+    would not at the widest -- the build refuses the first such row rather than code
+    it differently (lac_amd.coder.fudge_decisions_agree)."""
+    from lac_amd.coder import fudge_decisions_agree
+    from lac_amd.llm import Llama_AC
+    p = Llama_AC(_llm(case))
+    k = case["refuse_at_step"]
+    for i, t in enumerate(case["tokens"][:k + 1]):
+        r = p.pmf_row()
+        assert int(r[r > 0].min()) == case["min_positive"][i] >= 1 << 12
+        agree = fudge_decisions_agree(int(r.sum(dtype=object)), p.minp, int(r[r > 0].min()), case["prec"])
+        assert agree == (i != k), i
+        p.accept(t)
 
 
 @pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
 def test_oracle_exact_bits_on_reference_tables(case):
-    """The oracle, on the CDFs this adapter yields, gives the reference's exact-int bits."""
+    """The oracle, on the CDFs this adapter yields, gives the reference's exact-int bits
+    (on the peaky cases the oracle's minp is the smallest positive entry, which fudges
+    wherever the reference's minp 0 does: the test above)."""
     from lac_amd.llm import Llama_AC
     from oracle import restate
-    p = Llama_AC(FakeLlama(case["vocab"], case["n_ctx"], case["seed"]))
+    p = Llama_AC(_llm(case))
     rows = []
     for t in case["tokens"]:
         rows.append([int(x) for x in p.pmf_row()])
