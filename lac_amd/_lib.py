@@ -55,6 +55,8 @@ PROTOTYPES = [
     ("lac_copy_nbits_dev", _i, [_vp, _vp, _vp]),
     ("lac_pack_bits", _i, [_vp, _vp, C.c_int, _vp, _vp]),
     ("lac_pack_bits_at", _i, [_vp, _vp, _u64, C.c_int, _vp, _vp, _vp, _vp]),
+    ("lac_pack_jobs", _i, [C.c_int, _vp, _u64, _vp, _i64, _i64, _u64, _vp, _u64, C.c_int, _vp, _vp, _vp, _vp]),
+    ("lac_set_output", _i, [_vp, _vp, _vp]),
     ("lac_host_alloc", _i, [_u64, C.POINTER(_vp), C.POINTER(_vp)]),
     ("lac_host_free", _i, [_vp]),
     ("lac_encode_get_state", _i, [_vp, _vp, _vp, _vp]),

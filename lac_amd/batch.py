@@ -318,6 +318,25 @@ class BatchCoder:
                                         None if len_out is None else C.c_void_p(int(len_out)), self._stream))
         return out
 
+    def set_output(self, planes=None, nbits=None):
+        """Direct later encodes' output (plane A and the bit counts, include/lac.h
+        lac_set_output) into caller-owned device tensors: ``planes`` of >= streams *
+        cap_words + 1 int64 (``output_words()``), ``nbits`` of streams int64; None, None
+        restores the coder's own.  The tensors are kept referenced while in use."""
+        if (planes is None) != (nbits is None):
+            raise ValueError("planes and nbits: both or neither")
+        if planes is not None:
+            for t, n in ((planes, self.output_words()), (nbits, self.streams)):
+                if t.element_size() != 8 or not t.is_contiguous() or t.numel() < n or t.device != self.device:
+                    raise ValueError(f"output buffers: contiguous 8-byte tensors of >= {n} elements on {self.device}")
+        check(self.lib.lac_set_output(self.ctx, None if planes is None else C.c_void_p(planes.data_ptr()),
+                                      None if nbits is None else C.c_void_p(nbits.data_ptr())))
+        self._output = (planes, nbits)
+
+    def output_words(self):
+        """uint64 words of one job's plane A (set_output): streams * cap_words + 1."""
+        return self.streams * (self.bits_stride() // 8) + 1
+
     def nbits_tensor(self):
         """Per-stream bit counts as a fresh int64 device tensor (asynchronous copy)."""
         torch = _torch()

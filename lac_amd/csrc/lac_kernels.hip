@@ -808,17 +808,20 @@ __global__ __launch_bounds__(256) void k_finish(EncState *states, uint64_t *plan
 // trace (A_to_bin.step / run in lac_amd/coder.py) so a stream of any length
 // fits a fixed capacity; the packed output of lac_encode_finish then holds
 // only the tail, but the flush digits are exact.
-// lac_pack_bits(_at), one launch: streams of 1024 per workgroup, one per thread.
-// Every workgroup first sums the byte counts ceil(nbits / 8) of all streams before
-// its own (its 1024 threads stride over them, L2-hot; a DPP wave scan and 16 wave
-// sums per workgroup), then scans its own, so no workgroup waits on another.  Each
-// thread writes its stream's header entry (bit count, `hdr` bytes little endian) and
-// copies its packed bytes (planeA, big-endian bytes, after k_finish) behind the header,
-// all placed at byte `base` of dst (*base_in, 0 when NULL).  *end_out = base + the
-// packed length and *len_out (when not NULL: device or host-mapped memory) = the
-// length, from workgroup 0.  A job that would pass dst_bytes writes nothing:
-// *end_out = base, *len_out = ~0.  (Round 4 used a one-workgroup scan launch and a
-// copy launch: 7 + 4 us plus a dispatch gap per job, profiles/r05/gather/.)
+// lac_pack_jobs / lac_pack_bits(_at): one launch packs `jobs` finished jobs back to back
+// (job j's plane A at planeA + j * pstride words, its bit counts at nbits + j * B).
+// Workgroup (x, j) holds streams [1024 x, 1024 x + 1024) of job j, one per thread.  Each
+// workgroup first sums the byte counts ceil(nbits / 8) of everything before its own
+// streams -- the earlier jobs (plus their headers) and its job's earlier streams --
+// striding over them with its 1024 threads (L2-hot; a DPP wave scan and 16 wave sums
+// per workgroup), then scans its own, so no workgroup waits on another.  Each thread
+// writes its stream's header entry (bit count, `hdr` bytes little endian) and copies
+// its packed bytes (plane A holds big-endian bytes after k_finish) behind its job's
+// header, everything placed from byte `base` of dst (*base_in, 0 when NULL).
+// ends[j] = the end of job j and lens[j] (when not NULL: device or host-mapped memory)
+// its packed length.  A job that would pass dst_bytes writes nothing: ends[j] = its
+// start, lens[j] = ~0.  (Round 4 packed one job with a one-workgroup scan launch and a
+// copy launch: 7 + 4 us plus a dispatch gap, on the encode's stream, per job.)
 __device__ inline uint64_t block_excl_sum1024(uint64_t v, uint64_t *wsum, uint64_t &total) {
     const int w = threadIdx.x >> 6;
     const uint64_t inc = wave_incl_scan_u64(v);
@@ -835,41 +838,54 @@ __device__ inline uint64_t block_excl_sum1024(uint64_t v, uint64_t *wsum, uint64
     return before + inc - v;
 }
 
-__global__ __launch_bounds__(1024) void k_pack(const uint64_t *__restrict__ planeA, uint64_t cap_words,
-                                               const uint64_t *__restrict__ nbits, int64_t B, int hdr,
-                                               uint8_t *__restrict__ dst, uint64_t dst_bytes,
-                                               const uint64_t *__restrict__ base_in, uint64_t *__restrict__ end_out,
-                                               uint64_t *__restrict__ len_out) {
+__global__ __launch_bounds__(1024) void k_pack(const uint64_t *__restrict__ planes, uint64_t pstride,
+                                               uint64_t cap_words, const uint64_t *__restrict__ nbits_all,
+                                               int64_t B, int hdr, uint8_t *__restrict__ dst, uint64_t dst_bytes,
+                                               const uint64_t *__restrict__ base_in, uint64_t *__restrict__ ends,
+                                               uint64_t *__restrict__ lens) {
     __shared__ uint64_t wsum[16];
     const int t = threadIdx.x;
-    const int64_t first = (int64_t)blockIdx.x * 1024, b = first + t;
-    const uint64_t base = base_in ? *base_in : 0;
-    // bytes of every stream before this workgroup's, and of all streams (the fit test)
-    uint64_t pre = 0, all = 0;
-    for (int64_t k = t; k < B; k += 1024) {
-        const uint64_t n = (nbits[k] + 7) >> 3;
-        pre += k < first ? n : 0;
-        all += n;
+    const int64_t job = blockIdx.y, first = (int64_t)blockIdx.x * 1024, b = first + t;
+    const uint64_t *nbits = nbits_all + job * B;
+    const uint64_t *planeA = planes + job * pstride;
+    // this thread's stream first: its count and first 4 words are in flight while the
+    // workgroup sums the byte counts (plane A was written by the encode's waves on any
+    // XCD, so these are L2 misses)
+    const uint64_t nb = b < B ? nbits[b] : 0, n = (nb + 7) >> 3, nw = (n + 7) >> 3;
+    const uint64_t *src = planeA + (uint64_t)(b < B ? b : 0) * cap_words;
+    uint64_t w4[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) w4[i] = (uint64_t)i < nw ? src[i] : 0;
+    const uint64_t base0 = base_in ? *base_in : 0;
+    // bytes of the earlier jobs' streams, of this job's streams before this workgroup's,
+    // and of all this job's streams (the fit test)
+    uint64_t pj = 0, pw = 0, all = 0;
+    for (int64_t k = t; k < (job + 1) * B; k += 1024) {
+        const uint64_t m = (nbits_all[k] + 7) >> 3;
+        const int64_t kj = k / B, kb = k - kj * B;
+        pj += kj < job ? m : 0;
+        pw += kj == job && kb < first ? m : 0;
+        all += kj == job ? m : 0;
     }
-    uint64_t tp, ta;
-    (void)block_excl_sum1024(pre, wsum, tp);
+    uint64_t tj, tw, ta, tb;
+    (void)block_excl_sum1024(pj, wsum, tj);
+    (void)block_excl_sum1024(pw, wsum, tw);
     (void)block_excl_sum1024(all, wsum, ta);
-    const uint64_t nb = b < B ? nbits[b] : 0, n = (nb + 7) >> 3;
-    uint64_t tb;
     const uint64_t excl = block_excl_sum1024(n, wsum, tb);
-    const uint64_t total = (uint64_t)hdr * (uint64_t)B + ta;
-    const bool fits = base <= dst_bytes && total <= dst_bytes - base;
+    const uint64_t hB = (uint64_t)hdr * (uint64_t)B, total = hB + ta;
+    const uint64_t start = base0 + (uint64_t)job * hB + tj;      // job j: after the earlier jobs
+    const uint64_t before_ws = tw;
+    const bool fits = start <= dst_bytes && total <= dst_bytes - start;
     if (blockIdx.x == 0 && t == 0) {
-        *end_out = fits ? base + total : base;
-        if (len_out) *len_out = fits ? total : ~0ull;
+        ends[job] = fits ? start + total : start;
+        if (lens) lens[job] = fits ? total : ~0ull;
     }
     if (!fits || b >= B) return;
-    uint8_t *h = dst + base + (uint64_t)b * hdr;
+    uint8_t *h = dst + start + (uint64_t)b * hdr;
     for (int i = 0; i < hdr; i++) h[i] = (uint8_t)(nb >> (8 * i));
-    const uint64_t *src = planeA + (uint64_t)b * cap_words;
-    uint8_t *d = dst + base + (uint64_t)hdr * (uint64_t)B + tp + excl;
-    for (uint64_t wi = 0; wi * 8 < n; wi++) {
-        const uint64_t v = src[wi];
+    uint8_t *d = dst + start + hB + before_ws + excl;
+    for (uint64_t wi = 0; wi < nw; wi++) {
+        const uint64_t v = wi >= 4 ? src[wi] : wi == 0 ? w4[0] : wi == 1 ? w4[1] : wi == 2 ? w4[2] : w4[3];
         const uint64_t m = n - wi * 8 < 8 ? n - wi * 8 : 8;
         for (uint64_t k = 0; k < m; k++) d[wi * 8 + k] = (uint8_t)(v >> (8 * k));
     }
@@ -4110,6 +4126,7 @@ struct lac_ctx {
     DecState *dec = nullptr;
     TailState *tail = nullptr;          // decoder tail in the reference frame (lac_decode_tail_*)
     uint64_t *planeA = nullptr, *planeC = nullptr, *nbits = nullptr;
+    uint64_t *own_planeA = nullptr, *own_nbits = nullptr;   // planeA / nbits unless lac_set_output redirects them
     const uint8_t *dbits = nullptr;
     uint64_t dstride = 0;
     const uint64_t *dnbits = nullptr;
@@ -4951,6 +4968,8 @@ int lac_open(int device, int prec, int64_t vocab, int64_t streams, int pmf_bits,
     e = e ? e : hipMalloc(&c->planeC, sizeof(uint64_t) * (c->cap_words * streams + 1));
     e = e ? e : hipMalloc(&c->nbits, sizeof(uint64_t) * streams);
     e = e ? e : hipMemset(c->nbits, 0, sizeof(uint64_t) * streams);
+    c->own_planeA = c->planeA;
+    c->own_nbits = c->nbits;
     if (e != hipSuccess) {
         lac_close(c);
         return fail(LAC_E_HIP, "device allocation: %s", hipGetErrorString(e));
@@ -4973,9 +4992,9 @@ int lac_close(lac_ctx *c) {
     (void)hipFree(c->enc);
     (void)hipFree(c->dec);
     (void)hipFree(c->tail);
-    (void)hipFree(c->planeA);
+    (void)hipFree(c->own_planeA ? c->own_planeA : c->planeA);
     (void)hipFree(c->planeC);
-    (void)hipFree(c->nbits);
+    (void)hipFree(c->own_nbits ? c->own_nbits : c->nbits);
     (void)hipFree(c->q1chunks);
     (void)hipFree(c->dmeta);
     (void)hipFree(c->dresume);
@@ -5139,19 +5158,41 @@ int lac_copy_bits_dev(lac_ctx *c, uint8_t *dst, uint64_t dst_stride, void *strea
     return LAC_OK;
 }
 
+int lac_pack_jobs(int device, const uint64_t *planeA_dev, uint64_t plane_stride, const uint64_t *nbits_dev,
+                  int64_t jobs, int64_t streams, uint64_t cap_words, uint8_t *dst, uint64_t dst_bytes, int hdr_bytes,
+                  const uint64_t *base_dev, uint64_t *ends_dev, uint64_t *lens_out, void *stream) {
+    if (!dst || !ends_dev || streams < 0 || jobs < 1 || jobs > 65535 ||
+        (streams > 0 && (!planeA_dev || !nbits_dev)) || (hdr_bytes != 2 && hdr_bytes != 4) ||
+        (jobs > 1 && plane_stride < (uint64_t)streams * cap_words))
+        return fail(LAC_E_ARG, "bad argument");
+    if (hdr_bytes == 2 && cap_words * 64 >= 65536)
+        return fail(LAC_E_ARG, "a 2-byte header holds bit counts below 65536; these streams hold up to "
+                               "%llu bits: use 4", (unsigned long long)(cap_words * 64));
+    HIPCHK(hipSetDevice(device));
+    const unsigned bx = (unsigned)((streams + 1023) / 1024);
+    k_pack<<<dim3(bx > 0 ? bx : 1, (unsigned)jobs), 1024, 0, S(stream)>>>(
+        planeA_dev, plane_stride, cap_words, nbits_dev, streams, hdr_bytes, dst, dst_bytes, base_dev, ends_dev,
+        lens_out);
+    CHECK_LAUNCH();
+    return LAC_OK;
+}
+
 int lac_pack_bits_at(lac_ctx *c, uint8_t *dst, uint64_t dst_bytes, int hdr_bytes, const uint64_t *base_dev,
                      uint64_t *end_dev, uint64_t *len_out, void *stream) {
-    if (!c || !dst || !end_dev || (hdr_bytes != 2 && hdr_bytes != 4)) return fail(LAC_E_ARG, "bad argument");
-    if (hdr_bytes == 2 && c->cap_words * 64 >= 65536)
-        return fail(LAC_E_ARG, "a 2-byte header holds bit counts below 65536; this context's streams hold up to "
-                               "%llu bits: use 4", (unsigned long long)(c->cap_words * 64));
+    if (!c) return fail(LAC_E_ARG, "ctx is NULL");
     if (c->mode != 0) return fail(LAC_E_STATE, "context is decoding");
     if (!c->finished) return fail(LAC_E_STATE, "no finished encode to pack (lac_encode_job or lac_encode_finish)");
-    HIPCHK(hipSetDevice(c->device));
-    const unsigned blocks = (unsigned)((c->B + 1023) / 1024);
-    k_pack<<<blocks > 0 ? blocks : 1, 1024, 0, S(stream)>>>(c->planeA, c->cap_words, c->nbits, c->B, hdr_bytes, dst,
-                                                            dst_bytes, base_dev, end_dev, len_out);
-    CHECK_LAUNCH();
+    return lac_pack_jobs(c->device, c->planeA, 0, c->nbits, 1, c->B, c->cap_words, dst, dst_bytes, hdr_bytes,
+                         base_dev, end_dev, len_out, stream);
+}
+
+int lac_set_output(lac_ctx *c, uint64_t *planeA_dev, uint64_t *nbits_dev) {
+    if (!c) return fail(LAC_E_ARG, "ctx is NULL");
+    if (!planeA_dev != !nbits_dev) return fail(LAC_E_ARG, "planeA_dev and nbits_dev: both or neither");
+    if ((uintptr_t)planeA_dev % 8 || (uintptr_t)nbits_dev % 8) return fail(LAC_E_ARG, "buffers must be 8-byte aligned");
+    c->planeA = planeA_dev ? planeA_dev : c->own_planeA;
+    c->nbits = nbits_dev ? nbits_dev : c->own_nbits;
+    c->finished = 0;
     return LAC_OK;
 }
 

@@ -14,6 +14,8 @@ over xGMI; with ``gloo`` (tests) they are CPU tensors.
 from __future__ import annotations
 
 import collections
+import os
+import time
 
 
 def shard_range(total_streams: int, rank: int, world: int):
@@ -190,50 +192,59 @@ class BitstreamGatherer:
     """Bitstreams of back-to-back compression jobs gathered to one rank, sized to
     the payload, in batches of jobs (the path's one exchange).
 
-    Per job (``submit``), on every rank, one small launch pair on the caller's stream
-    packs the coder's finished streams (lac_pack_bits_at: a header of bit counts,
-    2 bytes per stream when the coder's capacity is below 2^16 bits, else 4, then
-    the streams' bytes back to back) and APPENDS them to the current *outbox*, a
-    device buffer of ``batch`` jobs; the kernel itself chains the offset (the previous
-    job's end, in device memory) and writes the job's packed length into pinned,
-    device-mapped host memory.  Nothing else touches the GPU per job: no copy, no
-    collective, no cross-stream wait.
+    Nothing runs on the encode's stream per job.  A BatchCoder encodes each job
+    straight into a job *slot* (plane A + bit counts, ``BatchCoder.set_output``;
+    ``batch`` slots per *box*, ``depth`` boxes in rotation), so a job's output needs
+    no copy.  When a box fills, a side stream -- once the batch's last encode is done
+    -- packs its jobs back to back into the box's outbox (one ``lac_pack_jobs`` launch
+    per batch: per job a header of bit counts, 2 bytes per stream when the coder's capacity is
+    below 2^16 bits, else 4, then each stream's bytes; the kernel chains the offsets in
+    device memory and writes each job's packed length into pinned, device-mapped host
+    words), concurrently with the next encodes.  ``lag`` jobs later (the same job
+    count on every rank, so the host exchange below is a well-ordered collective), the
+    host waits for the pack, reads the lengths, exchanges them with every rank over a gloo group (job
+    count, streams, slot width, header size and each job's length per rank; no GPU
+    work) and posts one grouped send/recv batch on the side stream: every rank sends
+    exactly its packed bytes to ``root``, which receives them (RCCL over xGMI under
+    nccl; the root's own share as a send to itself in the same batch, ``self_p2p``, so
+    a one-rank group runs every line of the path; gloo has no self-pair, the root
+    copies its share).  A box is refilled only after its pack (the encode's stream
+    waits for that event, long past) and its exchange (the side stream waits).
 
-    Per batch, at the ``submit`` after it filled (the next job's encode is already
-    enqueued, so the GPU stays busy while the host works): the host waits for the
-    batch's last pack (which precedes that encode), reads the lengths from the mapped
-    words, exchanges them with every rank over a gloo group on the host (``meta``:
-    job count, streams, slot width, header size and each job's length, per rank; no
-    GPU work), and posts one grouped send/recv batch: every rank sends exactly its
-    packed bytes to ``root``, which receives them (RCCL over xGMI under nccl; the
-    root's own share as a send to itself in the same batch, ``self_p2p``, so a
-    one-rank group runs every line of the path; gloo has no self-pair, the root
-    copies its share).  ``depth`` outboxes rotate: before an outbox is refilled, the
-    caller's stream waits for its batch's sends/receives (long finished by then).
-    One RCCL launch per batch instead of a pack, an all-gather, two copies and a
-    send/recv per job with cross-stream waits between them (the round-4 form cost
-    ~80 us per 1.2 ms job at world 1: every one of those sat in the encode's
-    hardware queue, profiles/r05/gather/).
+    The round-4 form put a pack, a size all-gather, two copies and a send/recv on the
+    encode's hardware queue per job, with cross-stream waits between them: ~80 us per
+    1.2 ms job at world 1; packing per job on the encode's stream still cost ~16 us
+    (profiles/r05/gather/).
 
-    On the root, ``last`` describes the last finished batch (``finished_jobs`` its
-    job numbers, counting from 1; ``last_job`` the newest) and ``last_unpacked(job)``
-    returns one of its jobs' streams as (bits [sum of streams, width], nbits).  A
-    batch is finished when its outbox is reused (``depth`` batches later) or by
-    ``drain``.  ``bytes_sent`` / ``payload_bytes`` count what crossed the links (the
-    other ranks' packed jobs) and the encoded bytes themselves; ``meta_bytes`` what
-    the host exchange carried.
+    On the root, ``finished_jobs`` lists the jobs of the finished batches still held
+    (``last_job`` the newest) and ``last_unpacked(job)`` returns one of them as (bits
+    [sum of streams, width], nbits).  A batch is finished when its box is refilled or
+    by ``drain``; after ``drain`` the coder presents its last job's output again (its
+    slot) and later jobs continue the rotation (the next job's output is then moved to
+    its place: one copy per drain).  ``bytes_sent`` / ``payload_bytes``
+    count what crossed the links (the other ranks' packed jobs) and the encoded bytes
+    themselves; ``meta_bytes`` what the host exchange carried.
 
-    Under ``gloo`` (CPU tests, one-GPU rehearsals) the same batches run on host
-    tensors; only the device-mapped lengths and RCCL are nccl's.
+    Coders without ``set_output`` (tests' CPU stand-ins) are copied and packed on the
+    host side at ``submit``; under ``gloo`` (CPU tests, one-GPU rehearsals) the sends
+    move host copies.
     """
 
     META = 4                                                 # int64 per rank ahead of the lengths
 
-    def __init__(self, coder, group=None, batch: int = 8, depth: int = 2, root: int = 0, self_p2p=None):
+    def __init__(self, coder, group=None, batch: int = 8, depth: int = 3, root: int = 0, self_p2p=None,
+                 lag=None):
         import torch
         import torch.distributed as dist
         self.coder, self.group, self.root = coder, group, int(root)
-        self.batch, self.depth = max(1, int(batch)), max(1, int(depth))
+        self.batch, self.depth = max(1, int(batch)), max(2, int(depth))
+        # a batch is exchanged `lag` jobs after it closed (default: one batch later).  The
+        # host waits there for the batch's pack, i.e. until the GPU has reached that
+        # batch's last job; the host, which runs ahead, then still has `lag` jobs queued
+        # behind it -- a lag of 2 left ~2.4 ms of queued work, and the host's exchange
+        # (sizes over gloo, posting the sends) sometimes took longer: the GPU idled
+        # (LAC_GATHER_TRACE, profiles/r05/gather/)
+        self.lag = self.batch if lag is None else max(1, int(lag))
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.gloo = dist.get_backend(group) == "gloo"
@@ -252,23 +263,34 @@ class BitstreamGatherer:
         self.job_cap = B * self.hdr + B * self.width
         self.box_cap = self.batch * self.job_cap
         self.cuda = self.device.type == "cuda"
-        self.native = hasattr(coder, "pack_bits_at") and self.cuda
+        self.native = hasattr(coder, "set_output") and self.cuda
         self.io_dev = torch.device("cpu") if self.gloo else self.device
+        # the side stream at high priority: a hardware queue of its own, so its packs and
+        # waits never sit between two encodes in the encode's queue (at the default
+        # priority it shared that queue: profiles/r05/gather/)
+        self.side = torch.cuda.Stream(device=self.device, priority=-1) if self.cuda else None
         self.boxes = []
         for _ in range(self.depth):
             bx = {"buf": torch.empty(max(self.box_cap, 1), dtype=torch.uint8, device=self.device),
-                  "jobs": [], "lens": None, "ends": None, "ev": None, "works": None, "meta": None, "seq": 0}
+                  "jobs": [], "lens": [0] * self.batch, "ends": None, "ev": None, "works": None, "meta": None,
+                  "seq": 0, "closed": False}
             if self.native:
                 bx["ends"] = torch.zeros(self.batch, dtype=torch.int64, device=self.device)
                 bx["lens"] = HostWords(coder.lib, self.batch)
-            else:
-                bx["lens"] = [0] * self.batch
             self.boxes.append(bx)
-        # root: per outbox and rank a receive buffer, (re)sized to the largest batch seen
+        self.slots = None
+        if self.native:                                          # per box: [job] plane A rows, bit counts
+            self.words = coder.output_words()
+            self.slots = [(torch.empty((self.batch, self.words), dtype=torch.int64, device=self.device),
+                           torch.zeros((self.batch, B), dtype=torch.int64, device=self.device))
+                          for _ in range(self.depth)]
+            coder.set_output(*self._slot(0, 0))
+        # root: per box and rank a receive buffer, (re)sized to the largest batch seen
         self.recv = [[None] * self.world if self.rank == self.root else None for _ in range(self.depth)]
-        self.side = torch.cuda.Stream(device=self.device) if self.cuda and not self.gloo else None
+        self.queue = collections.deque()                         # (box, job count it is exchanged at)
         self.cur = 0
-        self.pending = None
+        self.resume = None                                       # after drain: the slot the coder shows
+        self.last_slot = None                                    # where the last job's output lives
         self.seq = 0
         self.k = 0
         self.last = None
@@ -279,24 +301,35 @@ class BitstreamGatherer:
         self.payload_bytes = 0
         self.meta_bytes = 0
         self.jobs = 0
+        # LAC_GATHER_TRACE=<file>: host timestamps of every submit / exchange phase (JSON
+        # lines at close), to attribute host waits (tools/sessions, profiles/r05/gather/)
+        self.trace_path = os.environ.get("LAC_GATHER_TRACE")
+        self.trace = [] if self.trace_path else None
+
+    def _t(self, what, *extra):
+        if self.trace is not None:
+            self.trace.append((time.perf_counter(), self.k, what, *extra))
 
     # -- per job
     def submit(self):
-        """Append the coder's current (finished) output to the current batch; returns
-        the job's number (counting from 1)."""
+        """Record the coder's just-finished job (counting from 1) in the current batch;
+        exchanges whatever batch is due; points the coder at the next job's slot."""
         import torch
         self.k += 1
-        if self.pending is not None:                             # a full batch: exchange it now
-            i, self.pending = self.pending, None
-            self._post(i)
+        self._t("submit")
         i = self.cur
         bx = self.boxes[i]
-        if bx["works"] is not None:
-            self._finish(i)                                      # its previous batch, before packing over it
+        if not self.native and bx["closed"]:
+            self._prepare(i)
         n = len(bx["jobs"])
-        if self.native:                                          # one pack on the device, chained offsets
-            self.coder.pack_bits_at(bx["buf"], self.hdr, None if n == 0 else bx["ends"][n - 1:n],
-                                    bx["ends"][n:n + 1], bx["lens"].dev_addr(n))
+        if self.native:
+            if self.resume is not None:                          # the job went to the slot drain() showed:
+                li, ln = self.resume                             # move it into place (once per drain)
+                if (li, ln) != (i, n):
+                    for dst, src in zip(self._slot(i, n), self._slot(li, ln)):
+                        dst.copy_(src)
+                self.resume = None
+            self.last_slot = (i, n)
         else:                                                    # any coder with the copy accessors
             bits = torch.empty((self.B, self.width), dtype=torch.uint8, device=self.device)
             nbits = torch.empty((self.B,), dtype=torch.int64, device=self.device)
@@ -308,18 +341,65 @@ class BitstreamGatherer:
             bx["buf"][off:off + L].copy_(payload[:L])
             bx["lens"][n] = L
         bx["jobs"].append(self.k)
+        # due exchanges first: the sends are posted from the side stream, and RCCL's
+        # stream then waits for everything queued there -- posted after the new box's
+        # pack, a send waited for that pack (behind this job's encode) and held the next
+        # encode in its hardware queue (87 us, profiles/r05/gather/)
+        while self.queue and self.queue[0][1] <= self.k:
+            self._post(self.queue.popleft()[0])
         if len(bx["jobs"]) == self.batch:
             self._close_box(i)
-            self.pending = i                                     # posted at the next submit (or drain)
+        if self.native:
+            self._next_output()
         return self.k
 
     def _close_box(self, i):
+        """Box i holds its last job: pack it on the side stream, due for exchange ``lag``
+        jobs from now."""
         import torch
         bx = self.boxes[i]
-        if self.cuda:
+        if self.native:
+            import ctypes as C
+            from ._lib import check
+            done = torch.cuda.Event()
+            done.record()                                        # the batch's last encode (caller's stream)
+            self.side.wait_event(done)
+            planes, nbits = self.slots[i]
+            check(self.coder.lib.lac_pack_jobs(self.device.index or 0, C.c_void_p(planes.data_ptr()), self.words,
+                                               C.c_void_p(nbits.data_ptr()), len(bx["jobs"]), self.B,
+                                               self.width // 8, C.c_void_p(bx["buf"].data_ptr()), self.box_cap,
+                                               self.hdr, None, C.c_void_p(bx["ends"].data_ptr()),
+                                               C.c_void_p(bx["lens"].dev_addr(0)),
+                                               C.c_void_p(self.side.cuda_stream)))
             bx["ev"] = torch.cuda.Event()
-            bx["ev"].record()                                    # the box's last pack (caller's stream)
+            bx["ev"].record(self.side)
+        bx["closed"] = True
+        self.queue.append((i, self.k + self.lag))
         self.cur = (i + 1) % self.depth
+
+    def _prepare(self, i):
+        """Box i is about to be refilled: exchange it (and every box queued before it, in
+        order) and finish it; the encode's stream waits for its packs."""
+        import torch
+        bx = self.boxes[i]
+        while any(q[0] == i for q in self.queue):
+            self._post(self.queue.popleft()[0])
+        self._finish(i)
+        if bx["ev"] is not None:
+            torch.cuda.current_stream(self.device).wait_event(bx["ev"])   # its slots were packed
+            bx["ev"] = None
+        bx["closed"] = False
+
+    def _next_output(self):
+        """Point the coder at the next job's slot (its box prepared first if closed)."""
+        i = self.cur
+        if self.boxes[i]["closed"]:
+            self._prepare(i)
+        self.coder.set_output(*self._slot(i, len(self.boxes[i]["jobs"])))
+
+    def _slot(self, i, n):
+        planes, nbits = self.slots[i]
+        return planes[n], nbits[n]
 
     def _recv_buffer(self, i, r, n):
         import torch
@@ -333,18 +413,22 @@ class BitstreamGatherer:
         import torch
         import torch.distributed as dist
         bx = self.boxes[i]
+        self._t("post", i)
         if bx["ev"] is not None:
-            bx["ev"].synchronize()                               # its last pack only (not the next encode)
+            self._t("ev_ready" if bx["ev"].query() else "ev_wait", i)
+            bx["ev"].synchronize()                               # its packs (side stream) only
+        self._t("packed", i)
         n = len(bx["jobs"])
         lens = [bx["lens"][j] for j in range(n)]
         if any(v >= 1 << 63 for v in lens):
-            raise RuntimeError("a packed job did not fit its outbox slot")
+            raise RuntimeError("a packed job did not fit its outbox")
         mine = torch.zeros(self.META + self.batch, dtype=torch.int64)
         mine[:self.META] = torch.tensor([n, self.B, self.width, self.hdr])
         mine[self.META:self.META + n] = torch.tensor(lens, dtype=torch.int64)
         meta = torch.empty((self.world, self.META + self.batch), dtype=torch.int64)
         _all_gather(meta.view(-1), mine, self.meta_group, self.world)
         rows = meta.tolist()
+        self._t("meta", i)
         if any(row[0] != n for row in rows):
             raise RuntimeError(f"ranks disagree on the batch's job count: {[row[0] for row in rows]}")
         tot = [sum(row[self.META:self.META + n]) for row in rows]
@@ -358,12 +442,13 @@ class BitstreamGatherer:
             if self.gloo and src.is_cuda:
                 src = src.cpu()
             ops.append(dist.P2POp(dist.isend, src, self.root, group=self.group))
-        ctx = torch.cuda.stream(self.side) if self.side is not None else _nullctx()
+        ctx = torch.cuda.stream(self.side) if (self.side is not None and not self.gloo) else _nullctx()
         with ctx:
             bx["works"] = dist.batch_isend_irecv(ops) if ops else []
+        self._t("posted", i)
         if self.rank == self.root and not self.self_p2p:         # the root's own share: a local copy
             buf = self._recv_buffer(i, self.root, tot[self.root])
-            buf[:tot[self.root]].copy_(bx["buf"][:tot[self.root]], non_blocking=True)
+            buf[:tot[self.root]].copy_(bx["buf"][:tot[self.root]])
         bx["meta"] = rows
         self.seq += 1
         bx["seq"] = self.seq
@@ -373,11 +458,13 @@ class BitstreamGatherer:
         self.jobs += n
 
     def _finish(self, i):
+        """Box i's exchange is complete for the caller's stream (the root's bytes are read
+        there; and the side stream packs over the outbox only after an event recorded
+        later on that stream, _close_box).  Under nccl this queues a wait on an event
+        the batch's send/recv passed long ago -- once per batch."""
         bx = self.boxes[i]
         if bx["works"] is None:
             return
-        # the caller's stream waits for this batch's sends / receives only (its outbox is
-        # about to be refilled; the root's received bytes are then visible)
         for w in bx["works"]:
             w.wait()
         if self.rank == self.root:
@@ -385,27 +472,37 @@ class BitstreamGatherer:
             self.recent.append(self.last)
             self.finished_jobs = [j for b in self.recent for j in b["jobs"]]
             self.last_job = bx["jobs"][-1]
-        bx.update(jobs=[], works=None, ev=None, meta=None)
+        bx.update(jobs=[], works=None, meta=None)
 
     def drain(self):
         """Exchange every job submitted so far and complete every batch in flight (the
-        caller's stream waits for them)."""
-        if self.pending is not None:
-            i, self.pending = self.pending, None
-            self._post(i)
+        caller's stream waits for them); the coder then shows its last job's output."""
+        import torch
         i = self.cur
-        if self.boxes[i]["jobs"] and self.boxes[i]["works"] is None:   # a part-filled batch
+        if self.boxes[i]["jobs"] and not self.boxes[i]["closed"]:   # a part-filled batch
             self._close_box(i)
-            self._post(i)
+        while self.queue:
+            self._post(self.queue.popleft()[0])
         for _, j in sorted((bx["seq"], j) for j, bx in enumerate(self.boxes) if bx["works"] is not None):
             self._finish(j)
+        for bx in self.boxes:
+            bx["closed"] = False
+        if self.native:
+            cs = torch.cuda.current_stream(self.device)
+            for bx in self.boxes:
+                if bx["ev"] is not None:
+                    cs.wait_event(bx["ev"])
+                    bx["ev"] = None
+            if self.last_slot is not None:                       # the last job's slot, shown again
+                self.resume = self.last_slot
+                self.coder.set_output(*self._slot(*self.resume))
         return self.last
 
     def last_unpacked(self, job=None):
         """Root: one job of the finished batches still held (``finished_jobs``; default
         the newest), rank by rank, as (bits [streams, width], nbits [streams]) with width
-        the widest rank's slot.  A batch's bytes stay until its outbox is exchanged
-        again, so read them after the ``submit`` / ``drain`` that finished it."""
+        the widest rank's slot.  A batch's bytes stay until its box is exchanged again,
+        so read them after the ``submit`` / ``drain`` that finished it."""
         import torch
         job = self.last_job if job is None else job
         last = next((b for b in self.recent if job in b["jobs"]), None)
@@ -422,6 +519,17 @@ class BitstreamGatherer:
         return torch.cat(bits), torch.cat([p[1] for p in parts])
 
     def close(self):
+        """Free the mapped words; the coder writes to its own buffers again."""
+        if self.trace:
+            import json
+            with open(self.trace_path, "a") as f:
+                t0 = self.trace[0][0]
+                for t, k, what, *extra in self.trace:
+                    f.write(json.dumps({"t_us": round((t - t0) * 1e6, 1), "job": k, "what": what, "extra": extra})
+                            + "\n")
+            self.trace = []
+        if self.native:
+            self.coder.set_output(None, None)
         for bx in self.boxes:
             if isinstance(bx["lens"], HostWords):
                 bx["lens"].close()

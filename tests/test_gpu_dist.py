@@ -58,16 +58,26 @@ def test_rccl_gatherer_world1_real_coder(nccl_world1, batch, depth, jobs):
         when.append(g.last_job)
     g.drain()
     record()
-    assert [s[0] for s in seen] == list(range(1, jobs + 1))
-    for k, last in enumerate(when, start=1):
-        assert last == max(0, (k - 1) // batch - depth + 1) * batch, (k, last)
+    # the coder shows its last job's output again after drain (its slot)
+    assert torch.equal(coder.nbits_tensor(), made[-1][1]) and torch.equal(coder.bits_tensor(), made[-1][0])
+    # and jobs after a drain continue the rotation
+    for j in range(jobs, jobs + batch + 1):
+        bits, nbits, _, _ = _job(coder, j, T, B, V)
+        made.append((bits, nbits))
+        g.submit()
+        record()
+    g.drain()
+    record()
+    assert [s[0] for s in seen] == list(range(1, jobs + batch + 2))
+    for k, last in enumerate(when, start=1):     # the box of job k + 1 is prepared after job k
+        assert last == max(0, k // batch - depth + 1) * batch, (k, last)
     for j, b, n in seen:
         want_b, want_n = made[j - 1]
         assert torch.equal(n, want_n)
         nb = ((want_n + 7) // 8).tolist()
         for r in range(B):
             assert torch.equal(b[r, :nb[r]], want_b[r, :nb[r]]) and not b[r, nb[r]:].any()
-    assert g.jobs == jobs and g.payload_bytes > 0
+    assert g.jobs == jobs + batch + 1 and g.payload_bytes > 0
     g.close()
     coder.close()
 
@@ -100,6 +110,45 @@ def test_pack_bits_at_chains_jobs(nccl_world1):
     torch.cuda.synchronize()
     assert words[3] == (1 << 64) - 1 and int(ends[3]) == 0 and not small.any()
     words.close()
+    coder.close()
+
+
+@pytest.mark.parametrize("streams", [77, 2500])
+def test_pack_jobs_one_launch_equals_chained(nccl_world1, streams):
+    """lac_pack_jobs packs several jobs' planes (strided rows, as the gatherer's slots) in
+    one launch: bytes and ends equal packing them one by one; a base offset shifts
+    everything; lengths land in the mapped host words."""
+    import ctypes as C
+    from lac_amd.batch import BatchCoder
+    from lac_amd.dist import HostWords, pack_bitstreams
+    from lac_amd._lib import check
+    V, B, T, J = 1000, streams, 5, 3
+    coder = BatchCoder(V, B, prec=48, capacity_bits=T * 50 + 256, device=nccl_world1)
+    words = coder.output_words()
+    planes = torch.zeros((J, words), dtype=torch.int64, device=nccl_world1)
+    nbits = torch.zeros((J, B), dtype=torch.int64, device=nccl_world1)
+    want = []
+    for j in range(J):
+        coder.set_output(planes[j], nbits[j])
+        bits, nb, _, _ = _job(coder, 60 + j, T, B, V)
+        p, L = pack_bitstreams(bits, nb, 2)
+        want.append(p[:int(L)].clone())
+    coder.set_output(None, None)
+    host = HostWords(coder.lib, J)
+    ends = torch.zeros(J, dtype=torch.int64, device=nccl_world1)
+    base = torch.tensor([13], dtype=torch.int64, device=nccl_world1)
+    cap = 13 + J * B * (2 + coder.bits_stride())
+    out = torch.zeros(cap, dtype=torch.uint8, device=nccl_world1)
+    check(coder.lib.lac_pack_jobs(0, C.c_void_p(planes.data_ptr()), words, C.c_void_p(nbits.data_ptr()), J, B,
+                                  coder.bits_stride() // 8, C.c_void_p(out.data_ptr()), cap, 2,
+                                  C.c_void_p(base.data_ptr()), C.c_void_p(ends.data_ptr()),
+                                  C.c_void_p(host.dev_addr(0)), None))
+    torch.cuda.synchronize()
+    lens = [w.numel() for w in want]
+    assert [host[j] for j in range(J)] == lens
+    assert ends.tolist() == [13 + sum(lens[:j + 1]) for j in range(J)]
+    assert not out[:13].any() and torch.equal(out[13:13 + sum(lens)], torch.cat(want))
+    host.close()
     coder.close()
 
 
