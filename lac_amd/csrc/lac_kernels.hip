@@ -2448,6 +2448,11 @@ __constant__ uint32_t c_q1_tab[LAC_Q1_TAB_SIZE] = LAC_Q1_TAB_INIT;
 #ifndef LAC_Q1_SCHED
 #define LAC_Q1_SCHED 0           // scheduling fence between vectors in k_q1_stats
 #endif
+#ifndef LAC_Q1_DEFER_DEC
+#define LAC_Q1_DEFER_DEC 0       // k_q1_stats decode form: a row's chunk stores after the next row's max
+                                 // (measured: 3 VGPRs spilled, decode stats 42.1 -> 42.7 us per bf16 c3
+                                 // step, profiles/r05/q1dec_pf/; off)
+#endif
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef short s16x2 __attribute__((ext_vector_type(2)));
@@ -2633,6 +2638,20 @@ __device__ inline void multi_halve(uint32_t (&v)[R]) {
     }
 }
 
+// The two cross-row steps of a wave sum on gfx950's half-wave swaps (v_permlane16_swap /
+// v_permlane32_swap: VALU, no LDS round trip) instead of two 64-bit ds_bpermute
+// shuffles.  With x = y = v, swap(x, y) returns x with its odd rows (halves) taken from
+// y's even ones and y with its even rows from x's odd ones, so x + y = v[l] + v[l ^ 16]
+// (^ 32) in every lane.  r: a 16-lane row total (< 2^31); two rows can reach 2^32 (a
+// flat q1 row at k = 24), so the sum widens to 64 bits first.
+__device__ inline uint64_t cross_row_sum64(uint32_t r) {
+    const auto a = __builtin_amdgcn_permlane16_swap(r, r, false, false);
+    const uint64_t r2 = (uint64_t)a[0] + a[1];
+    const auto lo = __builtin_amdgcn_permlane32_swap((uint32_t)r2, (uint32_t)r2, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((uint32_t)(r2 >> 32), (uint32_t)(r2 >> 32), false, false);
+    return (((uint64_t)hi[0] << 32) | lo[0]) + (((uint64_t)hi[1] << 32) | lo[1]);
+}
+
 // Sums of R per-lane u32 values (each < 2^27) across the wave, all R at once:
 // halving steps over lane bits 0..log2(R)-1 and the rest of the 16-lane row in
 // 32 bits on DPP (a row sums 16 values < 2^31), then the two cross-row steps in
@@ -2646,10 +2665,7 @@ __device__ inline uint64_t wave_multi_sum32(uint32_t (&v)[R]) {
     if constexpr (R < 4) r += xor_dpp<1>(r);
     if constexpr (R < 8) r += xor_dpp<2>(r);
     if constexpr (R < 16) r += xor_dpp<3>(r);
-    uint64_t r64 = r;
-    r64 += shfl_xor_u64(r64, 16);
-    r64 += shfl_xor_u64(r64, 32);
-    return r64;
+    return cross_row_sum64(r);
 }
 // One halving step of multi_halve<R, BIT> for one pair (v[i], v[i + live/2]),
 // so callers can run it as soon as both values exist.
@@ -2662,10 +2678,7 @@ __device__ inline uint32_t halve_pair(uint32_t lo, uint32_t hi) {
 // itself (halve_pair<0/1/2>, see k_q1_stats_rl): r = its stage-2 value.
 __device__ inline uint64_t wave_multi_sum32_tail8(uint32_t r) {
     r += xor_dpp<3>(r);
-    uint64_t r64 = r;
-    r64 += shfl_xor_u64(r64, 16);
-    r64 += shfl_xor_u64(r64, 32);
-    return r64;
+    return cross_row_sum64(r);
 }
 constexpr int kHalveOrder[8] = {0, 4, 2, 6, 1, 5, 3, 7};   // butterfly pairs complete early
 
@@ -2779,6 +2792,22 @@ __global__ __launch_bounds__(64 * NWB, LAC_Q1_MINW) void k_q1_stats(const LT *__
     const uint32_t loff = (uint32_t)(lane & (kQ1Rep - 1)) << 2;
     // one 16-B vector of a tile, for the rolling prefetches
     auto ld_vec = [&](const Src &src, int tile, int j) { return src(tile * NT * R + gt + NT * j); };
+    // decode form, deferred stores (LAC_Q1_DEFER_DEC): the group's writer wave keeps row
+    // r's 64 chunk totals and maximum in registers and stores them once the next row's
+    // maximum is taken.  A store counts in vmcnt like a load, so one issued at the row's
+    // end sat in front of the waits for the next row's prefetched vectors: the writer
+    // wave -- and at the next barrier its block -- waited for the store's completion.
+    constexpr bool DEFER = DEC && LAC_Q1_DEFER_DEC;
+    uint64_t pend_tot = 0;
+    float pend_m = 0.f;
+    int64_t pend_r = -1;
+    auto flush_pending = [&]() {
+        if (DEFER && pend_r >= 0) {
+            chunks[pend_r * 64 + lane] = pend_tot;
+            if (lane == 0) mrow[pend_r] = pend_m;
+            pend_r = -1;
+        }
+    };
     for (int64_t rb = (int64_t)blockIdx.x * NR; rb < rows; rb += stride) {
         // gt opaque per row: the R per-vector lane offsets / indices derived from it are
         // recomputed (one add each) instead of hoisted out of the row loop, where
@@ -2861,6 +2890,7 @@ __global__ __launch_bounds__(64 * NWB, LAC_Q1_MINW) void k_q1_stats(const LT *__
         }
         const bool fast = q1_fast_row(m);
         const float c = q1_c(m);
+        flush_pending();                                       // the previous row's totals (DEFER)
         int sfull = -1, sr = 0;
         if (!DEC && valid) {
             const int64_t s = sym[(t0 + r / B) * B + r % B];
@@ -2930,12 +2960,16 @@ __global__ __launch_bounds__(64 * NWB, LAC_Q1_MINW) void k_q1_stats(const LT *__
                     }
                 }
             };
+            // (each halving step runs one vector late: its DPP reads a sum written a whole
+            // vector earlier, not the instruction before -- DPP after a VALU write of its
+            // source needs wait states, and roll()'s scheduling fence kept the compiler
+            // from filling them)
             if (fast) {                                        // row-uniform branch, outside the vector loop
 #pragma unroll
                 for (int q = 0; q < R; q++) {
                     const int j = STREAM ? kHalveOrder[q] : q;
                     take(j, q1_vec_sum<LT>(x[j], c, true, tabr, loff));
-                    pair_halve(j);
+                    if (q > 0) pair_halve(STREAM ? kHalveOrder[q - 1] : q - 1);
                     roll(j);
                 }
             } else {
@@ -2943,10 +2977,11 @@ __global__ __launch_bounds__(64 * NWB, LAC_Q1_MINW) void k_q1_stats(const LT *__
                 for (int q = 0; q < R; q++) {
                     const int j = STREAM ? kHalveOrder[q] : q;
                     take(j, q1_vec_sum<LT>(x[j], c, false, tabr, loff));
-                    pair_halve(j);
+                    if (q > 0) pair_halve(STREAM ? kHalveOrder[q - 1] : q - 1);
                     roll(j);
                 }
             }
+            pair_halve(STREAM ? kHalveOrder[R - 1] : R - 1);
             if (DEC) {
                 uint64_t gsum;                                 // group total of index q_index(lane)
                 if constexpr (STREAM) gsum = wave_multi_sum32_tail8(sv[0]);
@@ -2964,9 +2999,15 @@ __global__ __launch_bounds__(64 * NWB, LAC_Q1_MINW) void k_q1_stats(const LT *__
         __syncthreads();
         if (DEC) {
             if (wg == 0) {
-                if (valid) chunks[r * 64 + lane] = bins[g][lane];
+                if constexpr (DEFER) {
+                    pend_tot = bins[g][lane];
+                    pend_m = m;
+                    pend_r = valid ? r : -1;
+                } else {
+                    if (valid) chunks[r * 64 + lane] = bins[g][lane];
+                    if (valid && lane == 0) mrow[r] = m;
+                }
                 bins[g][lane] = 0;
-                if (valid && lane == 0) mrow[r] = m;
             }
         } else if (gt == 0 && valid) {
             uint64_t T = 0, L = 0;
@@ -2982,6 +3023,7 @@ __global__ __launch_bounds__(64 * NWB, LAC_Q1_MINW) void k_q1_stats(const LT *__
             out[r] = st;
         }
     }
+    flush_pending();
 }
 
 // k_q1_stats_rl: the q1 row statistics for rows of 8193..16384 16-B vectors (bf16
