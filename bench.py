@@ -89,7 +89,9 @@ def main():
                     help="pmf = max(1 or 2, floor(softmax * 2^k)); 0 = 31 for u32, 60 (llama-scale) for u64")
     ap.add_argument("--cpu-baseline", default="on", choices=("on", "off"))
     ap.add_argument("--cpu-threads", type=int, default=0, help="cpu_baseline threads (0 = nproc: host_cores())")
-    ap.add_argument("--decode-reps", type=int, default=3, help="timed decode passes, back to back, after a warm one")
+    ap.add_argument("--decode-reps", type=int, default=10,
+                    help="timed decode passes, back to back, after two warm ones (the first passes after "
+                         "the encode jobs run slower: profiles/r05/q1dec_pf/)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="minimum CPU-baseline sample time")
     ap.add_argument("--cpu-streams", type=int, default=0, help="oracle sample streams (0 = all)")
     ap.add_argument("--path", default="auto", choices=("auto", "split", "fused"), help="encode kernel path")

@@ -49,6 +49,12 @@ struct EncState {          // per stream, persistent across lac_encode calls
     int8_t flush[8];       // flush digits
 };
 
+struct TailState {                 // the decoder's tail in the reference frame; mirrors lac_tail_state (include/lac.h)
+    int64_t l, h, lb, hb;
+    int32_t err, done;
+    int64_t still, nsym;
+};
+
 struct DecState {
     int64_t l, h, x;       // registers and the prec-bit value window (bits past the end read as 0)
     uint64_t pos;          // next bit to read

@@ -1,5 +1,5 @@
 // lac_tail.h -- the decoder's tail in the reference's own register frame
-// (included by lac_kernels.hip inside its kernel namespace).
+// (included by lac_decode.hip inside its kernel namespace; TailState is in lac_core.h).
 //
 // A_from_bin (/root/reference/arith_code.py:248-334) keeps l, h and the received
 // window [lb, hb] (the bits so far padded with 0s / 1s).  The value-form decoders
@@ -30,12 +30,6 @@
 // inverse on [0, w) for the ceil mapping; for the floor mapping of Predictor(n)
 // the window still covers them), so their ratio is exactly 1.0 -- only
 // k(ls) and k(hs) need computing (lac_core.h cr_ratio, CPython's rounding).
-
-struct TailState {                 // mirrors lac_tail_state (include/lac.h)
-    int64_t l, h, lb, hb;
-    int32_t err, done;
-    int64_t still, nsym;
-};
 
 enum { kTailDecide = 0, kTailFlush = 1 };
 enum { kTailEmitted = 0, kTailIdle = 1 };   // code_out >= 0: a symbol / nothing (undetermined or flushed)
