@@ -221,6 +221,28 @@ int lac_pack_bits(lac_ctx *ctx, uint8_t *dst_dev, int hdr_bytes, uint64_t *len_d
 int lac_pack_bits_at(lac_ctx *ctx, uint8_t *dst_dev, uint64_t dst_bytes, int hdr_bytes, const uint64_t *base_dev,
                      uint64_t *end_dev, uint64_t *len_out, void *stream);
 
+/* The packing kernel of lac_pack_bits_at over `jobs` finished jobs at once, no
+ * context: job j's plane A at planeA_dev + j * plane_stride uint64 words (streams
+ * slots of cap_words each: a context's plane A after its job, e.g. buffers
+ * lac_set_output gave it) and its bit counts at nbits_dev + j * streams.  The jobs are
+ * packed back to back from byte *base_dev (0 when NULL) of dst_dev; ends_dev[j]
+ * (device) receives the end of job j and lens_out[j] (when not NULL; host memory from
+ * lac_host_alloc allowed) its packed length.  One launch on `device`, asynchronous on
+ * `stream`; same header rule and fit test as lac_pack_bits_at, per job. */
+int lac_pack_jobs(int device, const uint64_t *planeA_dev, uint64_t plane_stride, const uint64_t *nbits_dev,
+                  int64_t jobs, int64_t streams, uint64_t cap_words, uint8_t *dst_dev, uint64_t dst_bytes,
+                  int hdr_bytes, const uint64_t *base_dev, uint64_t *ends_dev, uint64_t *lens_out, void *stream);
+
+/* Redirect where the context's encodes write their output: plane A (streams *
+ * cap_words + 1 uint64, the packed bytes after the job) and the bit counts (streams
+ * uint64), caller-owned device buffers that must outlive their use; NULL, NULL
+ * restores the context's own.  Every later call that reads or writes the output
+ * (encode, finish, lac_copy_bits*, lac_encoded_*, lac_pack_bits*, lac_decode_open
+ * with no bits) uses them, so consecutive jobs can leave their output in separate
+ * buffers with no copy (lac_amd.dist.BitstreamGatherer packs a batch of them at once,
+ * off the encode's stream).  The context is not finished afterwards. */
+int lac_set_output(lac_ctx *ctx, uint64_t *planeA_dev, uint64_t *nbits_dev);
+
 /* Pinned host memory mapped into the device's address space, coherent (kernels'
  * stores are visible to the host when the launch completes), zero-filled:
  * *host_out is the host address, *dev_out the address kernels use.  For the few
