@@ -5,7 +5,7 @@
 // within +-2^62.  Every product and doubling is formed in 128 bits and narrowed
 // only after the range check, so no input -- prec up to 61, registers up to
 // +-2^62, any int64 range -- overflows (checked under UBSan by tests/native).
-// Shared by liblac.so (lac_kernels.hip wraps each in its C-ABI entry point) and
+// Shared by liblac.so (lac_api.hip wraps each in its C-ABI entry point) and
 // the host sanitizer build.  No device code.
 #pragma once
 

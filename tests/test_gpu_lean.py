@@ -1,4 +1,4 @@
-"""The lean few-stream decode step (k_decode_lean, lac_kernels.hip) and its hand-over to
+"""The lean few-stream decode step (k_decode_lean, lac_decode.hip) and its hand-over to
 k_decode_seq: streams that leave the lean case part-way -- a row whose total reaches
 2^32, a fudged row (T > w*minp, arith_code.py:84) -- continue on k_decode_seq from the
 step they stopped at, in the same launch chunk, and every path decodes the same symbols
