@@ -280,22 +280,11 @@ __device__ inline int decode_advance(DecState &st, uint64_t a, uint64_t bb, cons
 // builds a separate library with -DLAC_DEC_PHASES=1; the product build passes no clock
 // and the marks compile to nothing).  Phases: 0 row totals + scan, 1 targets, 2 chunk
 // search, 3 re-read + scan of the chunk, 4 ranges, 5 narrowing + renormalisation.
-struct NoClock {
-    __device__ void mark(int) {}
-};
+// (NoClock / PhaseClock: lac_dev.h)
 #ifndef LAC_DEC_PHASES
 #define LAC_DEC_PHASES 0
 #endif
 #if LAC_DEC_PHASES
-struct PhaseClock {
-    uint64_t prev = 0, acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    __device__ void start() { prev = __builtin_amdgcn_s_memtime(); }
-    __device__ void mark(int k) {
-        const uint64_t now = __builtin_amdgcn_s_memtime();
-        acc[k] += now - prev;
-        prev = now;
-    }
-};
 __device__ unsigned long long g_dec_phase[8];
 #endif
 

@@ -537,12 +537,35 @@ __device__ inline void frac_pair(uint64_t f0, uint64_t f1, uint64_t c0, uint64_t
 // v_mad_u64_u32 plus readlanes per lane-split pair) and the fudge test as one
 // compare against the row's precomputed threshold fthr = ceil(T / minp) (T > w minp
 // iff w < ceil(T / minp)).
-template <typename E, bool UNI = false>
+// Per-phase cycle accounting of the sequential coder steps for probe builds
+// (-DLAC_ENC_PHASES=1 / -DLAC_DEC_PHASES=1, tools/enc_phase_probe.py and
+// tools/dec_phase_probe.py): s_memtime deltas between marks.  The product build passes
+// NoClock, whose marks compile to nothing.
+struct NoClock {
+    __device__ void start() {}
+    __device__ void mark(int) {}
+};
+struct PhaseClock {
+    uint64_t prev = 0, acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    __device__ void start() { prev = __builtin_amdgcn_s_memtime(); }
+    __device__ void mark(int k) {
+        const uint64_t now = __builtin_amdgcn_s_memtime();
+        acc[k] += now - prev;
+        prev = now;
+    }
+};
+#ifndef LAC_ENC_PHASES
+#define LAC_ENC_PHASES 0
+#endif
+
+// Phases marked on `clk` (probe builds): 1 the range (fudge test, two mul-divs), 2 the
+// narrowing and renormalisation, 3 the plane append.
+template <typename E, bool UNI = false, typename Clock = NoClock>
 __device__ inline bool coder_step(EncState &st, int64_t &l, int64_t &h, uint64_t lo, uint64_t hi, uint64_t T,
                                   uint64_t minp, int64_t s, const E *row, int64_t V, int prec, uint64_t *pa,
                                   uint64_t *pc, uint64_t cap_words, uint64_t *trace_slot, int lane, int mapping,
                                   double inv_T = 0.0, bool allow_fudge = true, uint64_t flo = kNoFrac,
-                                  uint64_t fhi = kNoFrac, uint64_t fthr = 0) {
+                                  uint64_t fhi = kNoFrac, uint64_t fthr = 0, Clock *clk = nullptr) {
     if (s < 0 || s >= V) { st.err = LAC_E_SYMBOL_RANGE; return false; }   // arith_code.py:100-101
     if (T == 0) { st.err = LAC_E_TABLE; return false; }
     const uint64_t w = (uint64_t)(h - l + 1);
@@ -566,18 +589,21 @@ __device__ inline bool coder_step(EncState &st, int64_t &l, int64_t &h, uint64_t
         a = rfl_u64(a);             //  uniform again here, or l and h -- and the chain -- would
         bb = rfl_u64(bb);           //  move to the vector unit)
     }
+    if (clk) clk->mark(1);
     if (a >= bb) { st.err = LAC_E_ZERO_WIDTH; return false; }   // the reference hangs here
     h = l + (int64_t)bb - 1;
     l = l + (int64_t)a;
     int k;
     uint64_t Ev;
     renorm(l, h, prec, &k, &Ev);
+    if (clk) clk->mark(2);
     if (trace_slot && lane == 0) { trace_slot[0] = Ev; trace_slot[1] = (uint64_t)k; }
     auto store = [&](uint64_t idx, uint64_t wa, uint64_t wc) {
         if (lane == 0) { pa[idx] = wa; pc[idx] = wc; }
     };
     if (!plane_append(st.L, st.wa, st.wc, k, Ev, cap_words, store)) { st.err = LAC_E_CAPACITY; return false; }
     st.nsym++;
+    if (clk) clk->mark(3);
     return true;
 }
 

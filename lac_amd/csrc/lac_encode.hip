@@ -17,6 +17,10 @@
 
 namespace {
 
+#if LAC_ENC_PHASES
+__device__ unsigned long long g_enc_phase[8];
+#endif
+
 // ------------------------------------------------------------------ split path
 // k_row_stats: one wave per (step, stream) row -> RowStats.  Fully parallel over
 // steps x streams: the path for small stream counts.
@@ -72,6 +76,14 @@ __global__ __launch_bounds__(256) void k_encode(const RowStats *__restrict__ sta
     st.wa = rfl_u64(st.wa);
     st.wc = rfl_u64(st.wc);
     st.nsym = (int64_t)rfl_u64((uint64_t)st.nsym);
+    // probe builds (-DLAC_ENC_PHASES=1, tools/enc_phase_probe.py): 0 the step's stats out of
+    // the prefetch lanes, 1..3 coder_step's phases, 4 the per-64-step prefetch block
+#if LAC_ENC_PHASES
+    PhaseClock clock, *clk = &clock;
+    clock.start();
+#else
+    NoClock *clk = nullptr;
+#endif
     bool ok = true;
     for (int64_t g0 = 0; g0 < nsteps && ok; g0 += 64) {
         const int n = (int)((nsteps - g0) < 64 ? (nsteps - g0) : 64);
@@ -86,6 +98,7 @@ __global__ __launch_bounds__(256) void k_encode(const RowStats *__restrict__ sta
         const uint64_t flo = lane < n ? row_frac(my.lo, my.tot) : kNoFrac;
         const uint64_t fhi = lane < n ? row_frac(my.hi, my.tot) : kNoFrac;
         const uint64_t fthr = lane < n && my.minp ? div_floor((u128)my.tot + (my.minp - 1), my.minp) : 0;
+        if (clk) clk->mark(4);
         for (int i = 0; i < n; i++) {
             const uint64_t lo = readlane_u64(my.lo, i), hi = readlane_u64(my.hi, i);
             const uint64_t T = readlane_u64(my.tot, i), minp = readlane_u64(my.minp, i);
@@ -94,15 +107,22 @@ __global__ __launch_bounds__(256) void k_encode(const RowStats *__restrict__ sta
             const int64_t s = __builtin_amdgcn_readlane(mys, i);
             const int64_t t = t0 + g0 + i;
             const E *row = pmf + t * step_stride + b * stream_stride;
+            if (clk) clk->mark(0);
             if (!coder_step<E, true>(st, l, h, lo, hi, T, minp, s, row, V, prec, pa, pc, cap_words,
                                      trace ? trace + 2 * (t * B + b) : nullptr, lane, mapping,
-                                     __builtin_bit_cast(double, invb), allow_fudge, fl, fh, ft)) {
+                                     __builtin_bit_cast(double, invb), allow_fudge, fl, fh, ft, clk)) {
                 ok = false;
                 break;
             }
         }
     }
     if (lane == 0) store_state(st, l, h, pa, pc, cap_words, &states[b]);
+#if LAC_ENC_PHASES
+    if (lane == 0) {
+        for (int k = 0; k < 5; k++) atomicAdd(&g_enc_phase[k], (unsigned long long)clock.acc[k]);
+        atomicAdd(&g_enc_phase[6], (unsigned long long)st.nsym);
+    }
+#endif
 }
 
 // ------------------------------------------------------------------ fused path
@@ -373,6 +393,20 @@ int enc_finish_launch(lac_ctx *c, int term, hipStream_t st) {
 }
 
 extern "C" {
+
+#if LAC_ENC_PHASES
+// probe builds only (tools/enc_phase_probe.py): k_encode's phase cycle sums (s_memtime)
+// and the symbols they cover; reset != 0 clears them
+int lac_debug_enc_phases(uint64_t *out8, int reset) {
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_enc_phase), sizeof(uint64_t) * 8));
+    if (reset) {
+        const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_enc_phase), z, sizeof z));
+    }
+    return LAC_OK;
+}
+#endif
 
 int lac_encode_reset(lac_ctx *c, void *stream) {
     if (!c) return fail(LAC_E_ARG, "ctx is NULL");
