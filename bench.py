@@ -224,16 +224,14 @@ def main():
     gather_ok = None
     gather_info = None
     if gatherer:                                           # the root's last job == every rank's own bits
-        from lac_amd.dist import gather_bitstreams
+        from lac_amd.dist import bitstreams_equal, gather_bitstreams
         mine_b = coder.bits_tensor()
         mine_n = coder.nbits_tensor()
         ref_b, ref_n = gather_bitstreams(mine_b, mine_n)   # a separate, exact-width all-gather
         okg = True
         if rank == 0:
             gb, gn = gatherer.last_unpacked()
-            w = min(gb.shape[1], ref_b.shape[1])
-            okg = bool(torch.equal(gn.to(ref_n.device), ref_n)) and bool(
-                torch.equal(gb[:, :w].to(ref_b.device), ref_b[:, :w]))
+            okg = bitstreams_equal(gb, gn, ref_b, ref_n)
         flag = torch.tensor([1 if okg else 0], device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         gather_ok = bool(flag.item())

@@ -156,6 +156,25 @@ def unpack_bitstreams(payload, streams, width, hdr_bytes):
     return out, nb
 
 
+def bitstreams_equal(got_bits, got_nbits, bits, nbits):
+    """Whether an unpacked (zero padded) job ``got_*`` holds the streams ``bits`` /
+    ``nbits`` (rows of a coder's output, any stride): equal bit counts, equal bytes over
+    each stream's ceil(nbits/8) bytes -- past them a coder's output words hold whatever
+    the buffer held before, never read and never sent -- and zeros after them in ``got``."""
+    import torch
+    got_bits, got_nbits = got_bits.to(bits.device), got_nbits.to(nbits.device)
+    if got_bits.shape[0] != bits.shape[0] or not torch.equal(got_nbits, nbits.to(got_nbits.dtype)):
+        return False
+    nbytes = (nbits.to(torch.int64) + 7) // 8
+    if bool((nbytes > min(got_bits.shape[1], bits.shape[1])).any()):
+        return False
+    w = min(got_bits.shape[1], bits.shape[1])
+    live = torch.arange(got_bits.shape[1], device=bits.device)[None, :] < nbytes[:, None]
+    ref = torch.zeros_like(got_bits)
+    ref[:, :w] = bits[:, :w]
+    return bool(torch.equal(torch.where(live, ref, torch.zeros_like(ref)), got_bits))
+
+
 class HostWords:
     """``n`` int64 words of pinned host memory mapped into the device (liblac's
     lac_host_alloc, coherent): kernels write them at ``dev_addr(i)``, the host reads
@@ -177,15 +196,11 @@ class HostWords:
         return int(self.words[i])
 
     def close(self):
+        """Free the words (call while the HIP runtime is up: there is no finaliser, since one
+        running at interpreter exit could call into a runtime already torn down)."""
         if self._h:
             self.lib.lac_host_free(self._h)
             self._h = self._d = None
-
-    def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass
 
 
 class BitstreamGatherer:

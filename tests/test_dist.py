@@ -7,7 +7,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from lac_amd.dist import BitstreamGatherer, gather_bitstreams, scatter_bitstreams, shard_range
+from lac_amd.dist import BitstreamGatherer, bitstreams_equal, gather_bitstreams, scatter_bitstreams, shard_range
 
 
 def _free_port():
@@ -33,6 +33,26 @@ def _worker(rank, world, port, q):
     q.put((rank, bits.tolist(), nbits.tolist(), allb.tolist(), alln.tolist()))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def test_bitstreams_equal_ignores_bytes_past_each_stream():
+    """Rows agree over ceil(nbits/8) bytes; past them the coder's row may hold anything,
+    the unpacked row must hold zeros; bit counts must agree."""
+    nbits = torch.tensor([0, 5, 16, 17])
+    coder = torch.randint(1, 256, (4, 8), dtype=torch.uint8)
+    got = torch.zeros((4, 16), dtype=torch.uint8)
+    for r, n in enumerate(nbits.tolist()):
+        got[r, :(n + 7) // 8] = coder[r, :(n + 7) // 8]
+    assert bitstreams_equal(got, nbits, coder, nbits)
+    bad = got.clone()
+    bad[2, 1] ^= 1                                      # a stream byte differs
+    assert not bitstreams_equal(bad, nbits, coder, nbits)
+    bad = got.clone()
+    bad[1, 3] = 7                                       # padding not zero
+    assert not bitstreams_equal(bad, nbits, coder, nbits)
+    assert not bitstreams_equal(got, nbits + 1, coder, nbits + 1)   # bytes short of the new counts
+    assert not bitstreams_equal(got, torch.tensor([0, 5, 16, 18]), coder, nbits)
+    assert not bitstreams_equal(got[:3], nbits[:3], coder, nbits)
 
 
 def test_shard_range_partitions():
@@ -116,7 +136,16 @@ def _gatherer_worker(rank, world, port, q, shards, stride, jobs, batch, depth):
     g.drain()
     if rank == 0:
         _record(g, seen)
-    q.put((rank, seen, g.bytes_sent, g.payload_bytes, g.jobs, g.hdr, when))
+    # bench.py's check: the root's newest job against a separate all-gather of every
+    # rank's current output (garbage past each stream's bytes, as a coder's slots hold)
+    # (gather_bitstreams needs equal shards; uneven ones are rebuilt on the root)
+    if len(set(shards)) == 1:
+        ref_b, ref_n = gather_bitstreams(coder.bits, coder.nbits)
+    else:
+        want = [_FakeCoder.job_data(shards[r], stride, r, jobs) for r in range(world)]
+        ref_b, ref_n = torch.cat([b for b, _ in want]), torch.cat([n for _, n in want])
+    same = bitstreams_equal(*g.last_unpacked(), ref_b, ref_n) if rank == 0 else None
+    q.put((rank, seen, g.bytes_sent, g.payload_bytes, g.jobs, g.hdr, when, same))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -144,6 +173,7 @@ def _check_root(res, shards, stride, jobs, batch=2, depth=2):
     streams, bytes and bit counts, exactly."""
     seen, when = res[0][0], res[0][5]
     assert [s[0] for s in seen] == list(range(1, jobs + 1))
+    assert res[0][6] is True
     for k, last in enumerate(when, start=1):             # after submitting job k: job k's batch
         done = max(0, (k - 1) // batch - depth + 1)      # reuses an outbox, finishing the batch
         assert last == done * batch, (k, last)           # that held it depth batches earlier

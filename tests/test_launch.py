@@ -64,3 +64,19 @@ def test_bench_refuses_more_gpus_than_visible():
                        capture_output=True, text=True, timeout=300)
     assert p.returncode == 2, p.stderr
     assert "needs 2 GPUs" in p.stderr
+
+
+def test_workload_labels_follow_baseline_configs():
+    """bench.py names the BASELINE.json config a run measures: c2..c5 by
+    vocab, streams per GPU and GPU count -- `--gpus 8 --vocab 128256` is c5."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(REPO, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    assert bench.workload_name(32000, 1, 1) == "c2"
+    assert bench.workload_name(32000, 4096, 1) == "c3"
+    assert bench.workload_name(32000, 4096, 8).startswith("c3 weak-scaled over 8")
+    assert bench.workload_name(128256, 4096, 1) == "c4"
+    assert bench.workload_name(128256, 4096, 8) == "c5"
+    assert bench.workload_name(128256, 4096, 2).startswith("c5 shape on 2 GPUs")
+    assert bench.workload_name(1000, 7, 1) == "custom"
