@@ -31,6 +31,9 @@ __constant__ uint32_t c_q1_tab[LAC_Q1_TAB_SIZE] = LAC_Q1_TAB_INIT;
 #else
 #define LAC_Q1_DMA_POLICY ""
 #endif
+#ifndef LAC_Q1_DEC_DIRECT
+#define LAC_Q1_DEC_DIRECT 1      // k_q1_stats decode form, one row per block of 64 groups: per-wave chunk stores
+#endif
 #ifndef LAC_Q1_SCHED
 #define LAC_Q1_SCHED 0           // scheduling fence between vectors in k_q1_stats
 #endif
@@ -351,8 +354,14 @@ __global__ __launch_bounds__(64 * NWB, LAC_Q1_MINW) void k_q1_stats(const LT *__
     typedef RowSrc<BUF, sizeof(LT)> Src;
     static_assert(R * N <= 128, "lane sums must fit 32 bits");
     __shared__ uint32_t tabr[LAC_Q1_TAB_SIZE * kQ1Rep];
-    __shared__ float smax[NWB];
-    __shared__ int smaxi[NWB];
+    // decode form, rows of <= 64 groups of 64 vectors owned by a whole block (shapes 4 / 6,
+    // bf16 c3): each wave stores its 8 group totals -- the row's chunk totals, since G = 1
+    // there -- straight to HBM, with no LDS bins, no second barrier and no writer wave;
+    // the maxima's LDS words alternate between rows, so a wave may start the next row
+    // while the others still read this one's
+    constexpr bool DIRECT = DEC && !MULTI && RW * R == 64 && !LAC_Q1_DEFER_DEC && LAC_Q1_DEC_DIRECT;
+    __shared__ float smax[2][NWB];
+    __shared__ int smaxi[2][NWB];
     __shared__ uint64_t ssum[NWB][2];
     __shared__ uint32_t sps[NR];
     __shared__ unsigned long long bins[DEC ? NR : 1][64];
@@ -394,7 +403,8 @@ __global__ __launch_bounds__(64 * NWB, LAC_Q1_MINW) void k_q1_stats(const LT *__
             pend_r = -1;
         }
     };
-    for (int64_t rb = (int64_t)blockIdx.x * NR; rb < rows; rb += stride) {
+    int par = 0;
+    for (int64_t rb = (int64_t)blockIdx.x * NR; rb < rows; rb += stride, par ^= 1) {
         // gt opaque per row: the R per-vector lane offsets / indices derived from it are
         // recomputed (one add each) instead of hoisted out of the row loop, where
         // 2R loop-invariant VGPRs spilled the 16-vector shapes
@@ -445,12 +455,12 @@ __global__ __launch_bounds__(64 * NWB, LAC_Q1_MINW) void k_q1_stats(const LT *__
             const int wi = (int)wave_reduce((uint32_t)li, [](uint32_t a, uint32_t b) {
                 return (uint32_t)((int)a > (int)b ? (int)a : (int)b);
             });
-            if (lane == 0) smaxi[w] = wi;
+            if (lane == 0) smaxi[par][w] = wi;
             if (!DEC && gt == 0) sps[g] = 0;
             __syncthreads();
-            int bi = smaxi[0];
+            int bi = smaxi[par][0];
 #pragma unroll
-            for (int i = 1; i < NWB; i++) bi = smaxi[i] > bi ? smaxi[i] : bi;
+            for (int i = 1; i < NWB; i++) bi = smaxi[par][i] > bi ? smaxi[par][i] : bi;
             if (bi >= 0 && bi <= 0x7F80) {                    // block-uniform
                 m = __uint_as_float((uint32_t)bi << 16);
             } else {
@@ -459,20 +469,20 @@ __global__ __launch_bounds__(64 * NWB, LAC_Q1_MINW) void k_q1_stats(const LT *__
 #pragma unroll
                     for (int e = 0; e < N; e++) mx = fmaxf(mx, logit_at<LT>(x[j], e));
                 mx = wave_max_f32(mx);
-                if (lane == 0) smax[w] = mx;
+                if (lane == 0) smax[par][w] = mx;
                 __syncthreads();
-                m = smax[0];
+                m = smax[par][0];
 #pragma unroll
-                for (int i = 1; i < NWB; i++) m = fmaxf(m, smax[i]);
+                for (int i = 1; i < NWB; i++) m = fmaxf(m, smax[par][i]);
             }
         } else {
             mx = wave_max_f32(mx);
-            if (lane == 0) smax[w] = mx;
+            if (lane == 0) smax[par][w] = mx;
             if (!DEC && gt == 0) sps[g] = 0;
             __syncthreads();
-            m = smax[g * RW];
+            m = smax[par][g * RW];
 #pragma unroll
-            for (int i = 1; i < RW; i++) m = fmaxf(m, smax[g * RW + i]);
+            for (int i = 1; i < RW; i++) m = fmaxf(m, smax[par][g * RW + i]);
         }
         const bool fast = q1_fast_row(m);
         const float c = q1_c(m);
@@ -572,7 +582,10 @@ __global__ __launch_bounds__(64 * NWB, LAC_Q1_MINW) void k_q1_stats(const LT *__
                 uint64_t gsum;                                 // group total of index q_index(lane)
                 if constexpr (STREAM) gsum = wave_multi_sum32_tail8(sv[0]);
                 else gsum = wave_multi_sum32<R>(sv);
-                if (lane < R) {
+                if constexpr (DIRECT) {                        // every chunk once: grp covers 0..63
+                    const int grp = wg + RW * q_index<R>(lane);
+                    if (lane < R && valid) chunks[r * 64 + grp] = grp * 64 < nvec ? gsum : 0;
+                } else if (lane < R) {
                     const int grp = tile * RW * R + wg + RW * q_index<R>(lane);
                     if (grp * 64 < nvec) atomicAdd(&bins[g][grp / (int)G], (unsigned long long)gsum);
                 }
@@ -582,9 +595,13 @@ __global__ __launch_bounds__(64 * NWB, LAC_Q1_MINW) void k_q1_stats(const LT *__
             const uint64_t t64 = wave_sum_u64(tot), l64 = wave_sum_u64(lo);
             if (lane == 0) { ssum[w][0] = t64; ssum[w][1] = l64; }
         }
-        __syncthreads();
+        if constexpr (DIRECT) {
+            if (valid && w == 0 && lane == 0) mrow[r] = m;
+        } else {
+            __syncthreads();
+        }
         if (DEC) {
-            if (wg == 0) {
+            if (!DIRECT && wg == 0) {
                 if constexpr (DEFER) {
                     pend_tot = bins[g][lane];
                     pend_m = m;
