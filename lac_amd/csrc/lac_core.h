@@ -24,6 +24,10 @@
 #include <stdint.h>
 #include <string.h>
 
+#ifndef LAC_PLANE_FAST
+#define LAC_PLANE_FAST 1     // plane_append: the within-one-word case without the loop
+#endif
+
 namespace lac {
 
 typedef unsigned __int128 u128;
@@ -346,6 +350,17 @@ template <typename Store>
 __host__ __device__ inline bool plane_append(uint64_t &L, uint64_t &wa, uint64_t &wc, int k, uint64_t E,
                                              uint64_t cap_words, Store store) {
     if (k <= 0) return true;
+#if LAC_PLANE_FAST
+    // the common case: the digits land inside the word bit L-1 is in (no word completes,
+    // so no store and no loop), the carry on that word's bit L-1
+    const int off0 = (int)(L & 63);
+    if (off0 != 0 && k <= 64 - off0) {                    // k <= 63
+        if (E >> k) wc |= 1ull << (64 - off0);
+        wa |= (E & ((1ull << k) - 1)) << (64 - off0 - k);
+        L += (uint64_t)k;
+        return ((L - 1) >> 6) < cap_words;
+    }
+#endif
     const uint64_t ehi = E >> k;
     uint64_t elo = E & ((k == 64) ? ~0ull : ((1ull << k) - 1));
     if (ehi) wc |= 1ull << (63 - ((L - 1) & 63));         // carry onto bit L-1 (L >= 1 here)
