@@ -352,13 +352,15 @@ __host__ __device__ inline bool plane_append(uint64_t &L, uint64_t &wa, uint64_t
     if (k <= 0) return true;
 #if LAC_PLANE_FAST
     // the common case: the digits land inside the word bit L-1 is in (no word completes,
-    // so no store and no loop), the carry on that word's bit L-1
+    // so no store and no loop), the carry on that word's bit L-1.  Bit L-1 stays in the
+    // same word, which is within capacity: an earlier append put it there, or a restored
+    // state did (lac_encode_set_state refuses L > cap_words * 64)
     const int off0 = (int)(L & 63);
     if (off0 != 0 && k <= 64 - off0) {                    // k <= 63
         if (E >> k) wc |= 1ull << (64 - off0);
         wa |= (E & ((1ull << k) - 1)) << (64 - off0 - k);
         L += (uint64_t)k;
-        return ((L - 1) >> 6) < cap_words;
+        return true;
     }
 #endif
     const uint64_t ehi = E >> k;
