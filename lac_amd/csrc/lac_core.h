@@ -234,9 +234,38 @@ __host__ __device__ inline uint64_t row_frac(uint64_t c, uint64_t T) {
 // <= 61) and T < 2^63.  f*w/2^63 lies within w/2^63 <= 1/4 below c*w/T, so
 // q = floor(f*w/2^63) is the floor or one less; the remainder c*w - q*T is then
 // in [0, 2T), below 2^64, so wrapping 64-bit arithmetic computes it exactly.
+// d >= 0 for a wave-uniform d, tested on the high word alone.  On gfx950 the compiler
+// lowers every 64-bit ordered compare -- even of SGPR operands, even against 0 -- to a
+// VALU v_cmp whose result crosses back to the scalar unit; an empty asm holding the high
+// word in an SGPR keeps the 32-bit test (s_cmp) from being folded back into one.
+// Uniform values only.
+__host__ __device__ inline bool nonneg_uni(int64_t d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    int hi = (int)((uint64_t)d >> 32);
+    asm("" : "+s"(hi));
+    return hi >= 0;
+#else
+    return d >= 0;
+#endif
+}
+
+//
+// UNIF (the wave-uniform chain of k_encode; needs T < 2^62): the same quotient with no
+// compare at all.  With r = c*w - q*T (+ T - 1 for ceil) in [0, 3T - 1), the result is
+// q + [r >= T] (+ [r >= 2T] for ceil), each bracket 1 + the sign mask of a difference
+// (an arithmetic shift): plain scalar adds and shifts on the GPU, where an ordered
+// 64-bit compare is a VALU v_cmp and a compare's boolean is a lane mask whose use moves
+// the sum to the vector unit.
+template <bool UNIF = false>
 __host__ __device__ inline uint64_t frac_mul_div(uint64_t f, uint64_t c, uint64_t w, uint64_t T, bool ceil) {
     const u128 p = (u128)f * w;
     uint64_t q = (uint64_t)(p >> 63);
+    if constexpr (UNIF) {
+        const uint64_t r = c * w - q * T + (ceil ? T - 1 : 0);
+        q += 1 + (uint64_t)((int64_t)(r - T) >> 63);
+        if (ceil) q += 1 + (uint64_t)((int64_t)(r - 2 * T) >> 63);
+        return q;
+    }
     uint64_t r = c * w - q * T;
     if (r >= T) { q += 1; r -= T; }
     return q + (uint64_t)(ceil && r != 0);

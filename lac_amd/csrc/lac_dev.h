@@ -566,31 +566,49 @@ __device__ inline bool coder_step(EncState &st, int64_t &l, int64_t &h, uint64_t
                                   uint64_t *pc, uint64_t cap_words, uint64_t *trace_slot, int lane, int mapping,
                                   double inv_T = 0.0, bool allow_fudge = true, uint64_t flo = kNoFrac,
                                   uint64_t fhi = kNoFrac, uint64_t fthr = 0, Clock *clk = nullptr) {
-    if (s < 0 || s >= V) { st.err = LAC_E_SYMBOL_RANGE; return false; }   // arith_code.py:100-101
+    // UNI (k_encode, symbols from int32, vocab <= 2^31, w <= 2^61, fthr clamped to 2^62 by
+    // the caller): 32-bit symbol test, and the fudge and zero-width tests as the signs of
+    // differences -- scalar tests of a high word where a 64-bit ordered compare is a VALU
+    // v_cmp plus an SGPR round trip on the chain
+    if (UNI ? (uint32_t)s >= (uint32_t)V : (s < 0 || s >= V)) {   // arith_code.py:100-101
+        st.err = LAC_E_SYMBOL_RANGE;
+        return false;
+    }
     if (T == 0) { st.err = LAC_E_TABLE; return false; }
     const uint64_t w = (uint64_t)(h - l + 1);
     uint64_t a, bb;
-    if (mapping == LAC_MAP_FLOOR || !(UNI ? w < fthr : is_fudged(T, w, minp))) {  // floor: Predictor/ACSampler; else ceil
+    if (mapping == LAC_MAP_FLOOR ||
+        !(UNI ? !nonneg_uni((int64_t)(w - fthr)) : is_fudged(T, w, minp))) {   // floor: Predictor/ACSampler; else ceil
         if (UNI && flo != kNoFrac) {
-            a = frac_mul_div(flo, lo, w, T, mapping != LAC_MAP_FLOOR);
-            bb = frac_mul_div(fhi, hi, w, T, mapping != LAC_MAP_FLOOR);
-        } else if (flo != kNoFrac)
-            frac_pair(flo, fhi, lo, hi, w, T, mapping != LAC_MAP_FLOOR, &a, &bb);
-        else
-            div_pair(lo, hi, w, mapping == LAC_MAP_FLOOR ? 0 : T - 1, T, inv_T != 0.0 ? inv_T : recip(T), &a, &bb);
+            a = frac_mul_div<UNI>(flo, lo, w, T, mapping != LAC_MAP_FLOOR);
+            bb = frac_mul_div<UNI>(fhi, hi, w, T, mapping != LAC_MAP_FLOOR);
+        } else {
+            if (flo != kNoFrac)
+                frac_pair(flo, fhi, lo, hi, w, T, mapping != LAC_MAP_FLOOR, &a, &bb);
+            else
+                div_pair(lo, hi, w, mapping == LAC_MAP_FLOOR ? 0 : T - 1, T, inv_T != 0.0 ? inv_T : recip(T), &a,
+                         &bb);
+            if (UNI) {
+                a = rfl_u64(a);
+                bb = rfl_u64(bb);
+            }
+        }
     } else {                                                  // CDFPredictor.fudged_dist
         if (!allow_fudge) { st.err = LAC_E_TABLE; return false; }
         const i128 xprev = s > 0 ? wave_xmax_prefix<E>(row, s, w, T) : kI128Min;
         const i128 xs = fudge_x(hi, s, w, T);
         a = s > 0 ? fudge_f(s - 1, xprev, T, w, V) : 0;
         bb = fudge_f(s, xs > xprev ? xs : xprev, T, w, V);
-    }
-    if (UNI) {                      // (the fudged branch's wave reductions leave them in VGPRs:
-        a = rfl_u64(a);             //  uniform again here, or l and h -- and the chain -- would
-        bb = rfl_u64(bb);           //  move to the vector unit)
+        // (UNI: the wave reductions leave them in VGPRs -- uniform again here, in the
+        // branches that make them, so the scalar branch's results never visit the vector
+        // unit at the join, and l and h -- the chain -- stay scalar)
+        if (UNI) {
+            a = rfl_u64(a);
+            bb = rfl_u64(bb);
+        }
     }
     if (clk) clk->mark(1);
-    if (a >= bb) { st.err = LAC_E_ZERO_WIDTH; return false; }   // the reference hangs here
+    if (UNI ? nonneg_uni((int64_t)(a - bb)) : a >= bb) { st.err = LAC_E_ZERO_WIDTH; return false; }   // the reference hangs here
     h = l + (int64_t)bb - 1;
     l = l + (int64_t)a;
     int k;

@@ -52,8 +52,10 @@ __global__ __launch_bounds__(256) void k_row_stats(const E *__restrict__ pmf, in
 }
 
 // k_encode: one wave per stream over a chunk of steps; lane i prefetches the
-// RowStats of step g0 + i, 64 steps at a time.
-template <typename E>
+// RowStats of step g0 + i, 64 steps at a time.  MAP: the mapping (LAC_MAP_*) as a
+// compile-time constant (the launch passes it as `mapping` too), so the uniform chain's
+// ceil / floor choice folds away instead of becoming a lane-mask select.
+template <typename E, int MAP>
 __global__ __launch_bounds__(256) void k_encode(const RowStats *__restrict__ stats, const int32_t *__restrict__ sym,
                                                 int64_t B, int64_t t0, int64_t nsteps, const E *pmf,
                                                 int64_t step_stride, int64_t stream_stride, int64_t V, int prec,
@@ -61,7 +63,9 @@ __global__ __launch_bounds__(256) void k_encode(const RowStats *__restrict__ sta
                                                 uint64_t cap_words, uint64_t *trace, int mapping,
                                                 bool allow_fudge) {
     const int lane = (int)lane_id();
-    const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    // (the stream index provably wave-uniform: the row and trace addresses -- and the
+    // per-step trace test -- stay on the scalar unit)
+    const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + wave_in_block();
     if (b >= B) return;
     EncState st = states[b];
     if (st.err || st.nflush >= 0) {
@@ -95,9 +99,12 @@ __global__ __launch_bounds__(256) void k_encode(const RowStats *__restrict__ sta
         }
         // the 64 steps' row fractions and fudge thresholds at once, one lane each: off
         // the serial chain
-        const uint64_t flo = lane < n ? row_frac(my.lo, my.tot) : kNoFrac;
-        const uint64_t fhi = lane < n ? row_frac(my.hi, my.tot) : kNoFrac;
-        const uint64_t fthr = lane < n && my.minp ? div_floor((u128)my.tot + (my.minp - 1), my.minp) : 0;
+        // (totals of 2^62 and more divide instead: frac_mul_div's uniform form needs T < 2^62)
+        const bool frac_ok = lane < n && !(my.tot >> 62);
+        const uint64_t flo = frac_ok ? row_frac(my.lo, my.tot) : kNoFrac;
+        const uint64_t fhi = frac_ok ? row_frac(my.hi, my.tot) : kNoFrac;
+        uint64_t fthr = lane < n && my.minp ? div_floor((u128)my.tot + (my.minp - 1), my.minp) : 0;
+        fthr = fthr < (1ull << 62) ? fthr : (1ull << 62);   // w <= 2^61: w < fthr unchanged (coder_step's sign test)
         if (clk) clk->mark(4);
         for (int i = 0; i < n; i++) {
             const uint64_t lo = readlane_u64(my.lo, i), hi = readlane_u64(my.hi, i);
@@ -109,7 +116,7 @@ __global__ __launch_bounds__(256) void k_encode(const RowStats *__restrict__ sta
             const E *row = pmf + t * step_stride + b * stream_stride;
             if (clk) clk->mark(0);
             if (!coder_step<E, true>(st, l, h, lo, hi, T, minp, s, row, V, prec, pa, pc, cap_words,
-                                     trace ? trace + 2 * (t * B + b) : nullptr, lane, mapping,
+                                     trace ? trace + 2 * (t * B + b) : nullptr, lane, MAP,
                                      __builtin_bit_cast(double, invb), allow_fudge, fl, fh, ft, clk)) {
                 ok = false;
                 break;
@@ -325,9 +332,14 @@ static int encode_impl(lac_ctx *c, const E *pmf, int64_t step_stride, int64_t st
         CHECK_LAUNCH();
         {
             ProfScope ps(c, KID_ENCODE, st);
-            k_encode<E><<<blocks, 64 * kWavesPerBlock, 0, st>>>(c->stats, sym, c->B, t0, n, pmf, step_stride,
-                                                                stream_stride, c->V, c->prec, c->enc, c->planeA,
-                                                                c->planeC, c->cap_words, trace, c->mapping, true);
+            if (c->mapping == LAC_MAP_FLOOR)
+                k_encode<E, LAC_MAP_FLOOR><<<blocks, 64 * kWavesPerBlock, 0, st>>>(
+                    c->stats, sym, c->B, t0, n, pmf, step_stride, stream_stride, c->V, c->prec, c->enc, c->planeA,
+                    c->planeC, c->cap_words, trace, c->mapping, true);
+            else
+                k_encode<E, LAC_MAP_CEIL><<<blocks, 64 * kWavesPerBlock, 0, st>>>(
+                    c->stats, sym, c->B, t0, n, pmf, step_stride, stream_stride, c->V, c->prec, c->enc, c->planeA,
+                    c->planeC, c->cap_words, trace, c->mapping, true);
         }
         CHECK_LAUNCH();
     }
@@ -376,7 +388,7 @@ int enc_stats_launch(lac_ctx *c, const int32_t *sym, int64_t t0, int64_t n, uint
     const unsigned blocks = (unsigned)((c->B + kWavesPerBlock - 1) / kWavesPerBlock);
     {
         ProfScope ps(c, KID_ENCODE, st);
-        k_encode<uint32_t><<<blocks, 64 * kWavesPerBlock, 0, st>>>(
+        k_encode<uint32_t, LAC_MAP_CEIL><<<blocks, 64 * kWavesPerBlock, 0, st>>>(
             c->stats, sym, c->B, t0, n, (const uint32_t *)nullptr, 0, 0, c->V, c->prec, c->enc, c->planeA,
             c->planeC, c->cap_words, trace, LAC_MAP_CEIL, false);
     }

@@ -65,6 +65,11 @@ uint64_t cc_frac_mul_div(uint64_t c, uint64_t w, uint64_t T, int ceil) {
     const uint64_t f = row_frac(c, T);
     return f == kNoFrac ? ~0ull : frac_mul_div(f, c, w, T, ceil != 0);
 }
+// the compare-free form of k_encode's uniform chain (T < 2^62)
+uint64_t cc_frac_mul_div_uni(uint64_t c, uint64_t w, uint64_t T, int ceil) {
+    const uint64_t f = row_frac(c, T);
+    return f == kNoFrac || (T >> 62) ? ~0ull : frac_mul_div<true>(f, c, w, T, ceil != 0);
+}
 
 // pmf rows [steps][V] (eb = 4 or 8 bytes), one stream.  Returns status, writes
 // MSB-first bytes and the bit count.

@@ -80,6 +80,26 @@ def test_frac_mul_div_exact(core):
     assert core.cc_frac_mul_div(5, 1 << 47, 1 << 63, 1) == (1 << 64) - 1     # T >= 2^63: no fraction
 
 
+def test_frac_mul_div_uniform_form_exact(core):
+    """frac_mul_div<true> (k_encode's compare-free form: sign masks of r - T and r - 2T)
+    against exact big-int floor/ceil for T < 2^62, edges included (T just below 2^62,
+    c == T, c == 0, w at both ends of its range)."""
+    f = core.cc_frac_mul_div_uni
+    f.restype = C.c_uint64
+    f.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_int]
+    rng = random.Random(12)
+    for i in range(60000):
+        T = rng.choice([1, 2, 3, rng.randrange(1, 1 << 20), rng.randrange(1, 1 << 40), rng.randrange(1, 1 << 62),
+                        (1 << 62) - rng.randrange(1, 1000), (1 << 61) + rng.randrange(0, 1000)])
+        c = rng.choice([0, T, rng.randrange(0, T + 1), T - 1 if T > 1 else 0, 1 if T >= 1 else 0])
+        prec = rng.randint(2, 61)
+        w = rng.choice([(1 << (prec - 1)) + 1, 1 << prec, rng.randrange((1 << (prec - 1)) + 1, (1 << prec) + 1)])
+        ceil = i & 1
+        want = -(-(c * w) // T) if ceil else (c * w) // T
+        assert f(c, w, T, ceil) == want, (c, w, T, ceil)
+    assert f(5, 1 << 47, 1 << 62, 1) == (1 << 64) - 1                         # T >= 2^62: not this form
+
+
 def test_div_small_exact(core):
     """div_small (the decode step's quotient at prec <= 50 / totals < 2^50): exact
     floor((n*m + add)/d) for quotients below 2^50, with the reciprocal up to 2^-49
