@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--streams", type=int, default=1)
     ap.add_argument("--kernel", default="lean", choices=("lean", "seq"),
                     help="which sequential kernel the probe library runs (seq: a -DLAC_LEAN=0 build)")
+    ap.add_argument("--one-generator", action="store_true",
+                    help="tables from one torch generator (for runs under rocprofv3 --pmc)")
     a = ap.parse_args()
     import torch
     from lac_amd import synth
@@ -39,15 +41,22 @@ def main():
     dev = torch.device("cuda", 0)
     V, B, T, P = a.vocab, a.streams, a.tokens, 48
     coder = BatchCoder(V, B, prec=P, pmf_bits=32, capacity_bits=T * (P + 2) + 256, device=dev)
-    pmf, sym = synth.softmax_tables(T, B, V, seed=1234, device=dev, scale_bits=31, storage_bits=32)
+    if a.one_generator:                     # (for runs under rocprofv3 --pmc: tools/probe_tables.py)
+        from tools.probe_tables import one_generator_tables
+        pmf, sym = one_generator_tables(T, B, V, dev)
+    else:
+        pmf, sym = synth.softmax_tables(T, B, V, seed=1234, device=dev, scale_bits=31, storage_bits=32)
     coder.encode_job(pmf, sym)
     lib = coder.lib
-    lib.lac_debug_dec_phases.argtypes = [C.c_void_p, C.c_int]
+    probe = hasattr(lib, "lac_debug_dec_phases")     # (a plain library: kernel times only)
+    if probe:
+        lib.lac_debug_dec_phases.argtypes = [C.c_void_p, C.c_int]
     out = (C.c_uint64 * 8)()
     res = {}
     for rep in range(3):
         coder.decode_open()
-        lib.lac_debug_dec_phases(C.cast(out, C.c_void_p), 1)
+        if probe:
+            lib.lac_debug_dec_phases(C.cast(out, C.c_void_p), 1)
         ms = (C.c_double * 8)()
         cnt = (C.c_int64 * 8)()
         lib.lac_profile_read(coder.ctx, None, None, 1)
@@ -56,7 +65,8 @@ def main():
         torch.cuda.synchronize()
         lib.lac_profile_enable(coder.ctx, 0)
         lib.lac_profile_read(coder.ctx, C.cast(ms, C.c_void_p), C.cast(cnt, C.c_void_p), 1)
-        lib.lac_debug_dec_phases(C.cast(out, C.c_void_p), 1)
+        if probe:
+            lib.lac_debug_dec_phases(C.cast(out, C.c_void_p), 1)
         steps = max(int(out[6]), 1)
         names = (["top+window", "target+ballot+load_issue", "shadow(thi,next_row)", "wait+scan+select", "ranges",
                   "advance+output"] if a.kernel == "lean" else

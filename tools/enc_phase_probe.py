@@ -40,19 +40,9 @@ def main():
     dev = torch.device("cuda", 0)
     V, B, T, P = a.vocab, a.streams, a.tokens, 48
     coder = BatchCoder(V, B, prec=P, pmf_bits=32, capacity_bits=T * (P + 2) + 256, device=dev)
-    if a.one_generator:
-        # one torch generator for the whole batch: synth.softmax_tables seeds one per step, and
-        # 4096 of them crashed torch.randn in the host under rocprofv3 --pmc (SIGSEGV)
-        g = torch.Generator(device=dev)
-        g.manual_seed(1234)
-        p = torch.softmax(3.0 * torch.randn((T, B, V), generator=g, device=dev, dtype=torch.float32).double(), -1)
-        q = torch.clamp(torch.floor(p * float(1 << 31)), min=1).to(torch.int64)
-        cdf = torch.cumsum(q, -1)
-        u = torch.rand((T, B), generator=g, device=dev, dtype=torch.float64)
-        tgt = torch.minimum((u * cdf[..., -1].double()).floor().long(), cdf[..., -1] - 1)
-        sym = torch.searchsorted(cdf, tgt.unsqueeze(-1), right=True).squeeze(-1).to(torch.int32)
-        pmf = q.to(torch.int32)
-        del p, q, cdf
+    if a.one_generator:                     # (for runs under rocprofv3 --pmc: tools/probe_tables.py)
+        from tools.probe_tables import one_generator_tables
+        pmf, sym = one_generator_tables(T, B, V, dev)
     else:
         pmf, sym = synth.softmax_tables(T, B, V, seed=1234, device=dev, scale_bits=31, storage_bits=32)
     lib = coder.lib
