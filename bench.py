@@ -78,8 +78,8 @@ def workload_name(V, B, world):
 def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=10)   # ~12 ms of encodes before the timed 40 (clocks settled)
     ap.add_argument("--vocab", type=int, default=32000)
     ap.add_argument("--streams", type=int, default=4096, help="streams per GPU")
     ap.add_argument("--tokens", type=int, default=16, help="symbols per stream per job")
