@@ -875,6 +875,10 @@ constexpr int kLeanHelpers = LAC_LEAN_HELPERS;  // helper waves per stream
 #endif
 constexpr int64_t kLeanMaxStreams = LAC_LEAN_MAX_STREAMS;   // k_decode_lean up to this many streams
 constexpr int kLeanHelpMaxStreams = 16;         // above: no helpers (L2: ~2.6 MB ahead per stream)
+#ifndef LAC_LEAN_PUB
+#define LAC_LEAN_PUB 8
+#endif
+constexpr int kLeanPub = LAC_LEAN_PUB;          // the decoder publishes its progress every kLeanPub steps
 
 __device__ inline int32_t lean_progress(const int32_t *p) {
     return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -1021,7 +1025,7 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ pmf, i
                 ps[g] = pr[vc];
             }
             const BitWin win = bit_window(mybits, mynbits, pos);
-            if (progress && (i & 7) == 0 && lane == 0)             // the helpers' pace (after the loads)
+            if (progress && (i & (kLeanPub - 1)) == 0 && lane == 0)   // the helpers' pace (after the loads)
                 __hip_atomic_store(progress + b, i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             // a step outside the lean case leaves at the end (a branch here would let the
             // compiler sink the loads below it); until then its divisions run on safe values
