@@ -527,6 +527,32 @@ def test_edge_u64_totals_near_2_63(path):
     assert (_decode_both(c, dpmf) == sym).all()
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("prec", [48, 61])
+def test_edge_u64_totals_near_2_62(prec):
+    """The split path's compare-free row-fraction quotients (frac_mul_div<true>: sign
+    masks of r - T and r - 2T, valid for totals below 2^62) and, from 2^62 on, the
+    divisions k_encode falls back to: u64 rows whose totals straddle 2^62, few streams
+    (k_encode's uniform chain), fudged rows mixed in; bit-exact vs the oracle."""
+    from oracle import oracle as coracle
+    rng = np.random.default_rng(62)
+    V, B, steps = 6, 12, 40
+    pmf = np.zeros((steps, B, V), dtype=np.uint64)
+    for b in range(B):
+        hi = (1 << 62) // V * (36 + b) // 40                    # totals from ~0.8 to ~1.2 x 2^62
+        pmf[:, b, :] = rng.integers(hi // 8 * 7, hi, size=(steps, V), dtype=np.uint64)
+    pmf[::3, ::3, 5] = 1                                        # minp 1: fudged_dist at these totals
+    sym = rng.integers(0, V, size=(steps, B)).astype(np.int32)
+    tot = pmf.astype(object).sum(axis=2)
+    assert (tot >= (1 << 62)).any() and (tot < (1 << 62)).any()
+    c, dpmf, data, n, tr = _gpu_encode(pmf, sym, prec, path="split")
+    out, nb, status, rc = coracle.encode_batch(pmf, sym, prec, nthreads=4)
+    assert rc == 0
+    for b in range(B):
+        assert int(n[b]) == int(nb[b]) and data[b] == out[b, :(int(nb[b]) + 7) // 8].tobytes(), b
+    assert (_decode_both(c, dpmf) == sym).all()
+
+
 def test_stats_decode_spans_step_chunks():
     """600 streams x 150 steps: the stats-path decode (AUTO below 2048 streams)
     runs in 64-step chunks; symbols and determined counts match the other paths."""
