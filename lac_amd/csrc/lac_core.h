@@ -27,6 +27,9 @@
 #ifndef LAC_PLANE_FAST
 #define LAC_PLANE_FAST 1     // plane_append: the within-one-word case without the loop
 #endif
+#ifndef LAC_ENC_STRAIGHT
+#define LAC_ENC_STRAIGHT 1   // k_encode: 64-step blocks without per-step tests where no step can need one
+#endif
 
 namespace lac {
 
@@ -269,6 +272,19 @@ __host__ __device__ inline uint64_t frac_mul_div(uint64_t f, uint64_t c, uint64_
     uint64_t r = c * w - q * T;
     if (r >= T) { q += 1; r -= T; }
     return q + (uint64_t)(ceil && r != 0);
+}
+
+// frac_mul_div<true> for 32-bit counts and totals (c <= T < 2^32): the remainder's two
+// products then take three 32-bit multiplies each instead of four (k_encode's straight
+// block, u32 tables).
+template <bool CEIL>
+__host__ __device__ inline uint64_t frac_mul_div32(uint64_t f, uint32_t c, uint64_t w, uint32_t T) {
+    uint64_t q = (uint64_t)(((u128)f * w) >> 63);
+    const uint64_t T64 = T;
+    const uint64_t r = (uint64_t)c * w - q * T64 + (CEIL ? T64 - 1 : 0);
+    q += 1 + (uint64_t)((int64_t)(r - T64) >> 63);
+    if (CEIL) q += 1 + (uint64_t)((int64_t)(r - 2 * T64) >> 63);
+    return q;
 }
 
 // Floor mapping of Predictor.symbol_to_range (arith_code.py:69-70) and of

@@ -103,6 +103,63 @@ __global__ __launch_bounds__(256) void k_encode(const RowStats *__restrict__ sta
         const bool frac_ok = lane < n && !(my.tot >> 62);
         const uint64_t flo = frac_ok ? row_frac(my.lo, my.tot) : kNoFrac;
         const uint64_t fhi = frac_ok ? row_frac(my.hi, my.tot) : kNoFrac;
+#if LAC_ENC_STRAIGHT
+        // The block's straight form: when every step's row has 0 < T <= 2^(prec-1) < 2^32, a
+        // positive width at the symbol and an in-range symbol, and the state's width is in
+        // (2^(prec-1), 2^prec] (every renormalised state's is), no step can fudge
+        // (T <= w minp), hit a zero width (w > T, so the two mul-divs differ by >= 1) or
+        // leave that width range, so the 64 steps need none of coder_step's tests: per
+        // step two mul-divs in 32 x 64-bit products, a branch-free renormalisation and the
+        // plane append's one-word case, one rarely taken branch (the append crossing a
+        // word).  Results, registers and error steps are coder_step's.
+        {
+            const uint64_t half = 1ull << (prec - 1);
+            const bool lfast = lane >= n || (frac_ok && my.tot != 0 && my.tot <= half && !(my.tot >> 32) &&
+                                             my.hi > my.lo && (uint32_t)mys < (uint32_t)V);
+            const uint64_t d0 = (uint64_t)(h - l);
+            if (!trace && prec <= 61 && __ballot(!lfast) == 0 && nonneg_uni((int64_t)(d0 - half)) &&
+                !(d0 >> prec)) {
+                constexpr bool CEIL = MAP != LAC_MAP_FLOOR;
+                const int64_t nsym0 = st.nsym;
+                auto store = [&](uint64_t idx, uint64_t wa, uint64_t wc) {
+                    if (lane == 0) { pa[idx] = wa; pc[idx] = wc; }
+                };
+                int i = 0;
+                for (; i < n; i++) {
+                    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)my.lo, i);
+                    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)my.hi, i);
+                    const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)my.tot, i);
+                    const uint64_t fl = readlane_u64(flo, i), fh = readlane_u64(fhi, i);
+                    const uint64_t w = (uint64_t)(h - l + 1);
+                    const uint64_t a = frac_mul_div32<CEIL>(fl, lo, w, T), bb = frac_mul_div32<CEIL>(fh, hi, w, T);
+                    h = l + (int64_t)bb - 1;
+                    l = l + (int64_t)a;
+                    // renorm() without its kk <= 0 branch: kk = 0 keeps l and h (e = 0)
+                    const uint64_t d = (uint64_t)(h - l);
+                    const int sh = bitlen64(d), kk = prec - sh;
+                    const uint64_t e = kk > 0 ? (uint64_t)l >> sh : 0;
+                    l = (int64_t)(((uint64_t)l - (e << sh)) << kk);
+                    h = l + (int64_t)((d + 1) << kk) - 1;
+                    // plane_append: digits inside the word of bit L-1 (or none) inline
+                    const int off0 = (int)(st.L & 63);
+                    const int avail = off0 ? 64 - off0 : 0;
+                    if (__builtin_expect(kk > avail, 0)) {
+                        if (!plane_append(st.L, st.wa, st.wc, kk, e, cap_words, store)) {
+                            st.err = LAC_E_CAPACITY;
+                            ok = false;
+                            break;
+                        }
+                    } else {
+                        st.wc |= (e >> kk) << ((64 - off0) & 63);
+                        st.wa |= (e & ((1ull << kk) - 1)) << ((64 - off0 - kk) & 63);
+                        st.L += (uint64_t)kk;
+                    }
+                }
+                st.nsym = nsym0 + i;
+                continue;
+            }
+        }
+#endif
         uint64_t fthr = lane < n && my.minp ? div_floor((u128)my.tot + (my.minp - 1), my.minp) : 0;
         fthr = fthr < (1ull << 62) ? fthr : (1ull << 62);   // w <= 2^61: w < fthr unchanged (coder_step's sign test)
         if (clk) clk->mark(4);

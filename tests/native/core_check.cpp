@@ -70,6 +70,13 @@ uint64_t cc_frac_mul_div_uni(uint64_t c, uint64_t w, uint64_t T, int ceil) {
     const uint64_t f = row_frac(c, T);
     return f == kNoFrac || (T >> 62) ? ~0ull : frac_mul_div<true>(f, c, w, T, ceil != 0);
 }
+// its 32-bit-count form (k_encode's straight block; c <= T < 2^32)
+uint64_t cc_frac_mul_div32(uint64_t c, uint64_t w, uint64_t T, int ceil) {
+    const uint64_t f = row_frac(c, T);
+    if (f == kNoFrac || (T >> 32) || c > T) return ~0ull;
+    return ceil ? frac_mul_div32<true>(f, (uint32_t)c, w, (uint32_t)T)
+                : frac_mul_div32<false>(f, (uint32_t)c, w, (uint32_t)T);
+}
 
 // pmf rows [steps][V] (eb = 4 or 8 bytes), one stream.  Returns status, writes
 // MSB-first bytes and the bit count.

@@ -100,6 +100,27 @@ def test_frac_mul_div_uniform_form_exact(core):
     assert f(5, 1 << 47, 1 << 62, 1) == (1 << 64) - 1                         # T >= 2^62: not this form
 
 
+def test_frac_mul_div32_exact(core):
+    """frac_mul_div32 (k_encode's straight block: 32-bit counts and totals, the
+    remainder's products in 32 x 64 bits) against exact big-int floor/ceil, edges
+    included (T = 1 and just below 2^32, c == T, c == 0, w at both ends of its range)."""
+    f = core.cc_frac_mul_div32
+    f.restype = C.c_uint64
+    f.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_int]
+    rng = random.Random(13)
+    for i in range(60000):
+        T = rng.choice([1, 2, 3, rng.randrange(1, 1 << 20), rng.randrange(1, 1 << 32), (1 << 32) - rng.randrange(1, 1000),
+                        (1 << 31) + rng.randrange(0, 1 << 20)])
+        c = rng.choice([0, T, rng.randrange(0, T + 1), T - 1 if T > 1 else 0, 1])
+        c = min(c, T)
+        prec = rng.randint(2, 61)
+        w = rng.choice([(1 << (prec - 1)) + 1, 1 << prec, rng.randrange((1 << (prec - 1)) + 1, (1 << prec) + 1)])
+        ceil = i & 1
+        want = -(-(c * w) // T) if ceil else (c * w) // T
+        assert f(c, w, T, ceil) == want, (c, w, T, ceil)
+    assert f(5, 1 << 47, 1 << 32, 1) == (1 << 64) - 1                         # T >= 2^32: not this form
+
+
 def test_div_small_exact(core):
     """div_small (the decode step's quotient at prec <= 50 / totals < 2^50): exact
     floor((n*m + add)/d) for quotients below 2^50, with the reciprocal up to 2^-49
