@@ -30,6 +30,12 @@
 #ifndef LAC_ENC_STRAIGHT
 #define LAC_ENC_STRAIGHT 1   // k_encode: 64-step blocks without per-step tests where no step can need one
 #endif
+#ifndef LAC_ENC_PIPE
+#define LAC_ENC_PIPE 1       // k_encode straight blocks: the next step's row values read one step ahead
+#endif
+#ifndef LAC_ENC_UNROLL
+#define LAC_ENC_UNROLL 2     // k_encode straight blocks: steps per loop iteration
+#endif
 
 namespace lac {
 
@@ -198,6 +204,18 @@ __host__ __device__ inline uint64_t div_small_fix(uint64_t q, uint64_t n, uint64
 }
 __host__ __device__ inline uint64_t div_small(uint64_t n, uint64_t m, uint64_t add, uint64_t d, double inv) {
     return div_small_fix(div_small_est(n, m, add, inv), n, m, add, d);
+}
+// div_small_fix without a branch, for the sequential decoders' wave-uniform chains:
+// with the remainder r in [-3d, 3d) (above: the rounded estimate is at most 3 above the
+// floor and 2 below it), the quotient is q - [r < -2d] - [r < -d] - [r < 0] + [r >= d] +
+// [r >= 2d], each bracket the sign mask of a difference (an arithmetic shift; 0 or -1) --
+// scalar adds and shifts on the GPU, where the loops' ordered 64-bit tests were VALU
+// compares feeding a branch each.
+__host__ __device__ inline uint64_t sign_mask64(uint64_t x) { return (uint64_t)((int64_t)x >> 63); }
+__host__ __device__ inline uint64_t div_small_fix_mask(uint64_t q, uint64_t n, uint64_t m, uint64_t add, uint64_t d) {
+    const uint64_t r = n * m + add - q * d;
+    return q + 2 + sign_mask64(r + 2 * d) + sign_mask64(r + d) + sign_mask64(r) + sign_mask64(r - d) +
+           sign_mask64(r - 2 * d);
 }
 
 // CDFPredictor.fudged_dist test (arith_code.py:84): fudged iff T > w*minp.

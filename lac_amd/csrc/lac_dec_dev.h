@@ -295,7 +295,16 @@ __device__ unsigned long long g_dec_phase[8];
 __device__ inline bool neg_u(uint64_t r) { return (int64_t)r < 0; }
 
 // div_small_fix for wave-uniform values (|r| < 3d < 2^53).
+#ifndef LAC_DIVFIX_MASK
+#define LAC_DIVFIX_MASK 1        // div_small_fix_u as sign masks (lac_core.h div_small_fix_mask), no loops
+#endif
+// MASK: the branch-free correction -- for the lone-wave chains (k_decode_lean, k_decode_seq:
+// c2 decode 1.253 -> 1.229 us per step); k_q1_decode, whose 16 stream-waves per CU hide the
+// loops' branches, keeps the loops (the masks' extra instructions: 4.3 -> 4.6 us per bf16 c3
+// step; profiles/r05/straight/)
+template <bool MASK = LAC_DIVFIX_MASK>
 __device__ inline uint64_t div_small_fix_u(uint64_t q, uint64_t n, uint64_t m, uint64_t add, uint64_t d) {
+    if constexpr (MASK) return div_small_fix_mask(q, n, m, add, d);
     uint64_t r = n * m + add - q * d;
     // (corrections as a fixed count of selects instead of these loops, which are never
     // entered past their first test: c2 1.29 -> 1.48 us/step, profiles/r04/lean/)
@@ -311,16 +320,18 @@ __device__ inline uint64_t div_small_fix_u(uint64_t q, uint64_t n, uint64_t m, u
 
 // div_small with wave-uniform arguments: the double estimate on the vector unit (the
 // SALU has no FP64), read back, the 64-bit remainder and its corrections on the SALU.
+template <bool MASK = LAC_DIVFIX_MASK>
 __device__ inline uint64_t div_small_u(uint64_t n, uint64_t m, uint64_t add, uint64_t d, double inv) {
-    return div_small_fix_u(rfl_u64(div_small_est(n, m, add, inv)), n, m, add, d);
+    return div_small_fix_u<MASK>(rfl_u64(div_small_est(n, m, add, inv)), n, m, add, d);
 }
 // Two of them with one divisor (the ranges ceil(lo*w/T), ceil(hi*w/T)): both estimates
 // first, so the two FP64 chains overlap, then both corrections.
+template <bool MASK = LAC_DIVFIX_MASK>
 __device__ inline void div_small_u2(uint64_t n0, uint64_t n1, uint64_t m, uint64_t add, uint64_t d, double inv,
                                     uint64_t *q0, uint64_t *q1) {
     const uint64_t e0 = rfl_u64(div_small_est(n0, m, add, inv)), e1 = rfl_u64(div_small_est(n1, m, add, inv));
-    *q0 = div_small_fix_u(e0, n0, m, add, d);
-    *q1 = div_small_fix_u(e1, n1, m, add, d);
+    *q0 = div_small_fix_u<MASK>(e0, n0, m, add, d);
+    *q1 = div_small_fix_u<MASK>(e1, n1, m, add, d);
 }
 
 // Everything after the row's totals are known: val_to_symbol + symbol_to_range

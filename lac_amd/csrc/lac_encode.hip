@@ -20,6 +20,7 @@ namespace {
 #if LAC_ENC_PHASES
 __device__ unsigned long long g_enc_phase[8];
 #endif
+constexpr int kEncUnroll = LAC_ENC_UNROLL;
 
 // ------------------------------------------------------------------ split path
 // k_row_stats: one wave per (step, stream) row -> RowStats.  Fully parallel over
@@ -124,36 +125,60 @@ __global__ __launch_bounds__(256) void k_encode(const RowStats *__restrict__ sta
                 auto store = [&](uint64_t idx, uint64_t wa, uint64_t wc) {
                     if (lane == 0) { pa[idx] = wa; pc[idx] = wc; }
                 };
+                // step i's row values out of lane i (LAC_ENC_PIPE: read one step ahead, so
+                // the readlanes' latency is not on the chain)
+                auto rd = [&](int j, uint32_t &lo, uint32_t &hi, uint32_t &T, uint64_t &fl, uint64_t &fh) {
+                    lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)my.lo, j);
+                    hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)my.hi, j);
+                    T = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)my.tot, j);
+                    fl = readlane_u64(flo, j);
+                    fh = readlane_u64(fhi, j);
+                };
+                uint32_t nlo, nhi, nT;
+                uint64_t nfl, nfh;
+                if constexpr (LAC_ENC_PIPE) rd(0, nlo, nhi, nT, nfl, nfh);
                 int i = 0;
-                for (; i < n; i++) {
-                    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)my.lo, i);
-                    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)my.hi, i);
-                    const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)my.tot, i);
-                    const uint64_t fl = readlane_u64(flo, i), fh = readlane_u64(fhi, i);
-                    const uint64_t w = (uint64_t)(h - l + 1);
-                    const uint64_t a = frac_mul_div32<CEIL>(fl, lo, w, T), bb = frac_mul_div32<CEIL>(fh, hi, w, T);
-                    h = l + (int64_t)bb - 1;
-                    l = l + (int64_t)a;
-                    // renorm() without its kk <= 0 branch: kk = 0 keeps l and h (e = 0)
-                    const uint64_t d = (uint64_t)(h - l);
-                    const int sh = bitlen64(d), kk = prec - sh;
-                    const uint64_t e = kk > 0 ? (uint64_t)l >> sh : 0;
-                    l = (int64_t)(((uint64_t)l - (e << sh)) << kk);
-                    h = l + (int64_t)((d + 1) << kk) - 1;
-                    // plane_append: digits inside the word of bit L-1 (or none) inline
-                    const int off0 = (int)(st.L & 63);
-                    const int avail = off0 ? 64 - off0 : 0;
-                    if (__builtin_expect(kk > avail, 0)) {
-                        if (!plane_append(st.L, st.wa, st.wc, kk, e, cap_words, store)) {
-                            st.err = LAC_E_CAPACITY;
-                            ok = false;
-                            break;
+                int kk = 0;
+                uint64_t e = 0;
+                // the inner loop leaves only at the block's end or at a step whose digits
+                // cross a plane word (~1 step in 7), whose append runs below it; one exit
+                // test per step, no other branch
+                while (i < n) {
+                    for (; i < n; i++) {
+                        uint32_t lo, hi, T;
+                        uint64_t fl, fh;
+                        if constexpr (LAC_ENC_PIPE) {
+                            lo = nlo, hi = nhi, T = nT, fl = nfl, fh = nfh;
+                            rd(i + 1 < n ? i + 1 : i, nlo, nhi, nT, nfl, nfh);
+                        } else {
+                            rd(i, lo, hi, T, fl, fh);
                         }
-                    } else {
+                        const uint64_t w = (uint64_t)(h - l + 1);
+                        const uint64_t a = frac_mul_div32<CEIL>(fl, lo, w, T), bb = frac_mul_div32<CEIL>(fh, hi, w, T);
+                        h = l + (int64_t)bb - 1;
+                        l = l + (int64_t)a;
+                        // renorm() without its kk <= 0 branch: kk = 0 keeps l and h (e = 0)
+                        const uint64_t d = (uint64_t)(h - l);
+                        const int sh = bitlen64(d);
+                        kk = prec - sh;
+                        e = kk > 0 ? (uint64_t)l >> sh : 0;
+                        l = (int64_t)(((uint64_t)l - (e << sh)) << kk);
+                        h = l + (int64_t)((d + 1) << kk) - 1;
+                        // plane_append's case of digits inside the word of bit L-1 (or none)
+                        const int off0 = (int)(st.L & 63);
+                        const int avail = off0 ? 64 - off0 : 0;
+                        if (__builtin_expect(kk > avail, 0)) break;
                         st.wc |= (e >> kk) << ((64 - off0) & 63);
                         st.wa |= (e & ((1ull << kk) - 1)) << ((64 - off0 - kk) & 63);
                         st.L += (uint64_t)kk;
                     }
+                    if (i >= n) break;
+                    if (!plane_append(st.L, st.wa, st.wc, kk, e, cap_words, store)) {   // step i's crossing
+                        st.err = LAC_E_CAPACITY;
+                        ok = false;
+                        break;
+                    }
+                    i++;
                 }
                 st.nsym = nsym0 + i;
                 continue;

@@ -1629,8 +1629,8 @@ __global__ LAC_DEC_BOUNDS void k_q1_decode(const LT *__restrict__ lg, int64_t st
             uint64_t tgt, thi;
             if (small) {
                 const double iw = recip(w);
-                tgt = div_small_u(v, T, 0, w, iw);
-                thi = vh == v ? tgt : (vh < w ? div_small_u(vh, T, 0, w, iw) : 0);
+                tgt = div_small_u<false>(v, T, 0, w, iw);
+                thi = vh == v ? tgt : (vh < w ? div_small_u<false>(vh, T, 0, w, iw) : 0);
             } else {
                 div_pair(v, vh < w ? vh : 0, T, 0, w, recip(w), &tgt, &thi);
             }
@@ -1704,7 +1704,7 @@ __global__ LAC_DEC_BOUNDS void k_q1_decode(const LT *__restrict__ lg, int64_t st
                     s = cv0 * N + (int64_t)cnt;
                     uint64_t a, bb;
                     if (small) {
-                        div_small_u2(lo_c, hi_c, w, T - 1, T, recip(T), &a, &bb);
+                        div_small_u2<false>(lo_c, hi_c, w, T - 1, T, recip(T), &a, &bb);
                     } else {
                         div_pair(lo_c, hi_c, w, T - 1, T, recip(T), &a, &bb);
                     }

@@ -60,6 +60,10 @@ uint64_t cc_cr_ratio(uint64_t a, uint64_t b) {
 uint64_t cc_div_small(uint64_t n, uint64_t m, uint64_t add, uint64_t d, double rel) {
     return div_small(n, m, add, d, (1.0 / (double)d) * (1.0 + rel));
 }
+// the same quotient with the decoders' branch-free correction (div_small_fix_mask)
+uint64_t cc_div_small_mask(uint64_t n, uint64_t m, uint64_t add, uint64_t d, double rel) {
+    return div_small_fix_mask(div_small_est(n, m, add, (1.0 / (double)d) * (1.0 + rel)), n, m, add, d);
+}
 
 uint64_t cc_frac_mul_div(uint64_t c, uint64_t w, uint64_t T, int ceil) {
     const uint64_t f = row_frac(c, T);

@@ -128,6 +128,8 @@ def test_div_small_exact(core):
     import random
     core.cc_div_small.restype = C.c_uint64
     core.cc_div_small.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_double]
+    core.cc_div_small_mask.restype = C.c_uint64          # the sign-mask correction (div_small_fix_mask)
+    core.cc_div_small_mask.argtypes = core.cc_div_small.argtypes
     rng = random.Random(11)
     n_cases = 0
     while n_cases < 40000:
@@ -140,6 +142,7 @@ def test_div_small_exact(core):
             continue
         rel = rng.choice([0.0, 2.0 ** -49, -2.0 ** -49, rng.uniform(-1, 1) * 2.0 ** -50])
         assert core.cc_div_small(n, m, add, d, rel) == q, (n, m, add, d, rel)
+        assert core.cc_div_small_mask(n, m, add, d, rel) == q, (n, m, add, d, rel)
         n_cases += 1
     # the decoder's own shapes: targets floor(v*T/w), v < w, and ranges ceil(c*w/T), c <= T
     for _ in range(20000):
@@ -150,6 +153,8 @@ def test_div_small_exact(core):
         c = rng.randint(0, T)
         assert core.cc_div_small(v, T, 0, w, 2.0 ** -50) == v * T // w
         assert core.cc_div_small(c, w, T - 1, T, -2.0 ** -50) == -(-(c * w) // T)
+        assert core.cc_div_small_mask(v, T, 0, w, 2.0 ** -50) == v * T // w
+        assert core.cc_div_small_mask(c, w, T - 1, T, -2.0 ** -50) == -(-(c * w) // T)
 
 
 def test_core_matches_golden(core):
