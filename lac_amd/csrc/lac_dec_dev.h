@@ -56,6 +56,19 @@ __device__ inline uint64_t window_bits(const BitWin &win, uint64_t nbits, uint64
     return v;
 }
 
+// window_bits for 0 <= k <= 62 with no branch (the lone-wave decoder's step): the second
+// word always shifted in (its bits lie past the stream's end whenever the test above
+// skips it, and the end mask clears them), shifts by 64 split into two, the end mask's
+// drop clamped to 63 (past the end everything is dropped: v < 2^k).
+__device__ inline uint64_t window_bits_nb(const BitWin &win, uint64_t nbits, uint64_t pos, int k) {
+    const int off = (int)(pos & 63);
+    uint64_t v = (bswap64(win.w0) << off) | ((bswap64(win.w1) >> 1) >> (63 - off));
+    v = (v >> 1) >> (63 - k);                                 // the top k bits; 0 for k = 0
+    const int64_t over = (int64_t)(pos + (uint64_t)k - nbits);
+    const int drop = over <= 0 ? 0 : (over > 63 ? 63 : (int)over);
+    return (v >> drop) << drop;
+}
+
 // A decoder state loaded by one wave for its own stream, moved to SGPRs: the compiler
 // cannot tell a value loaded from a wave-uniform address is uniform.
 __device__ inline void dec_state_uniform(DecState &st) {

@@ -990,12 +990,13 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ pmf, i
             const uint64_t cwi = cw;
             cw = cw1;
             lm = lm1;
-            if (i + 2 < n32) {                                  // row i+2
-                cw1 = *lcv;
-                lm1 = lmeta[li];
+            {                                                   // row i+2 (the last row again past the end)
+                const bool more = i + 2 < n32;
+                cw1 = *(more ? lcv : lcv - (int64_t)B32 * 64);
+                lm1 = lmeta[more ? li : li - B32];
             }
-            lcv += (int64_t)B32 * 64;
-            li += B32;
+            lcv += i + 2 < n32 ? (int64_t)B32 * 64 : 0;
+            li += i + 2 < n32 ? B32 : 0;
             const E *row = rowp;
             const uint32_t *pr = prp;
             rowp += step_stride;
@@ -1025,29 +1026,30 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ pmf, i
                 ps[g] = pr[vc];
             }
             const BitWin win = bit_window(mybits, mynbits, pos);
-            if (progress && (i & (kLeanPub - 1)) == 0 && lane == 0)   // the helpers' pace (after the loads)
-                __hip_atomic_store(progress + b, i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__builtin_expect(progress && (i & (kLeanPub - 1)) == 0, 0) && lane == 0)   // the helpers' pace
+                __hip_atomic_store(progress + b, i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // (after the loads)
             // a step outside the lean case leaves at the end (a branch here would let the
             // compiler sink the loads below it); until then its divisions run on safe values
-            const bool bad = (T == 0) | neg_u((uint64_t)(x - l)) | neg_u((uint64_t)(h - x)) |
-                             (ceil_map & neg_u(w - fthr)) | (cm == 0);
+            // (the step's tests as sign bits of differences and ORs on the scalar unit, one
+            // exit test per step: each ordered 64-bit compare had been a VALU compare feeding
+            // a branch)
+            const uint64_t bad = (uint64_t)(T == 0) | ((uint64_t)(x - l) >> 63) | ((uint64_t)(h - x) >> 63) |
+                                 ((uint64_t)ceil_map & ((w - fthr) >> 63)) | (uint64_t)(cm == 0);
             const uint64_t Ts = bad ? 1 : T, ws = bad ? 1 : w, vs = bad ? 0 : v;
             const double iw = recip(ws);
             const uint64_t tgt = div_small_u(vs, Ts, 0, ws, iw);   // < T < 2^32
             const uint32_t t32 = (uint32_t)tgt;
             clk.mark(1);
-            // in the loads' shadow: the 1-padded end's target
             const uint64_t past = pos > mynbits ? pos - mynbits : 0;
             const int u = past < (uint64_t)prec ? (int)past : prec;
-            const uint64_t vhi = vs + ((1ull << u) - 1);
-            const bool vhi_in = neg_u(vhi - ws);                 // vhi < w
-            const uint64_t thi = u == 0 ? tgt : (vhi_in ? div_small_u(vhi, Ts, 0, ws, iw) : 0);
             clk.mark(2);
             // the iteration holding the target: the last whose first vector starts at or below it
             int gs = 0;
 #pragma unroll
-            for (int g = 1; g < CIM; g++)
-                if (cv0 + g * 64 < nv32 && (uint32_t)__builtin_amdgcn_readfirstlane((int)ps[g]) <= t32) gs = g;
+            for (int g = 1; g < CIM; g++) {
+                const bool take = (cv0 + g * 64 < nv32) & ((uint32_t)__builtin_amdgcn_readfirstlane((int)ps[g]) <= t32);
+                gs = take ? g : gs;
+            }
             Vt xg = xs[0];
             uint32_t pg = ps[0];
 #pragma unroll
@@ -1078,23 +1080,31 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ pmf, i
             uint64_t a, bb;
             div_small_u2(lo_c, hi_c, ws, ceil_map ? Ts - 1 : 0, Ts, bad ? 1.0 : iT, &a, &bb);
             // (l + a <= x <= l + bb - 1: v in [a, bb))
-            if (bad || !m2 || neg_u(vs - a) || !neg_u(vs - bb)) break;
+            if (bad | (uint64_t)(m2 == 0) | ((vs - a) >> 63) | (((vs - bb) >> 63) ^ 1)) break;
             clk.mark(4);
-            if (firstnd < 0 && !(vhi_in && neg_u(thi - hi_c))) firstnd = i;
-            // narrow + renormalise (decode_advance<true>)
-            int64_t nl = l + (int64_t)a, nh = l + (int64_t)bb - 1;
-            int kk;
-            uint64_t Ev;
-            renorm(nl, nh, prec, &kk, &Ev);
-            if (kk > 0) {
-                const BitWin wu{rfl_u64(win.w0), rfl_u64(win.w1)};
-                x = (int64_t)((((uint64_t)x - (Ev << (prec - kk))) << kk) | window_bits(wu, mynbits, pos, kk));
-                pos += (uint64_t)kk;
+            // the 1-padded end's target only past the stream's end (u > 0): before it the
+            // step is determined (thi = tgt < hi_c)
+            if (__builtin_expect(u != 0, 0)) {
+                const uint64_t vhi = vs + ((1ull << u) - 1);
+                const bool vhi_in = (vhi - ws) >> 63;             // vhi < w
+                const uint64_t thi = vhi_in ? div_small_u(vhi, Ts, 0, ws, iw) : 0;
+                if (firstnd < 0 && !(vhi_in && ((thi - hi_c) >> 63))) firstnd = i;
             }
+            // narrow + renormalise (decode_advance<true>) without branches: kk = 0 keeps the
+            // registers, and window_bits_nb(.., 0) is 0
+            int64_t nl = l + (int64_t)a, nh = l + (int64_t)bb - 1;
+            const uint64_t d = (uint64_t)(nh - nl);
+            const int sh = bitlen64(d), kk = prec - sh;
+            const uint64_t Ev = kk > 0 ? (uint64_t)nl >> sh : 0;
+            nl = (int64_t)(((uint64_t)nl - (Ev << sh)) << kk);
+            nh = nl + (int64_t)((d + 1) << kk) - 1;
+            const BitWin wu{rfl_u64(win.w0), rfl_u64(win.w1)};
+            x = (int64_t)((((uint64_t)x - (Ev << sh)) << kk) | window_bits_nb(wu, mynbits, pos, kk));
+            pos += (uint64_t)kk;
             l = nl;
             h = nh;
             if (lane == (i & 63)) sbuf = sym;
-            if ((i & 63) == 63) {
+            if (__builtin_expect((i & 63) == 63, 0)) {
                 *outv = sbuf;
                 outv += (int64_t)B32 * 64;
             }
