@@ -15,6 +15,8 @@
 //   k_pack        the multi-GPU gather's payload (lac_pack_jobs, lac_amd/dist.py).
 #include "lac_host.h"
 
+#include <type_traits>
+
 namespace {
 
 #if LAC_ENC_PHASES
@@ -50,6 +52,103 @@ __global__ __launch_bounds__(256) void k_row_stats(const E *__restrict__ pmf, in
         st.pad = 0;
         out[r] = st;
     }
+}
+
+// k_encode's straight steps over one 64-step block (see k_encode): step i's row values
+// out of lane i (LAC_ENC_PIPE: read one step ahead, off the chain), the two mul-divs
+// through the row fractions (T32: 32 x 64-bit remainder products), renorm() without its
+// kk <= 0 branch (kk = 0 keeps l and h, e = 0), plane_append's one-word case inline.  The
+// inner loop leaves only at the block's end, at a step whose digits cross a plane word
+// (~1 step in 7; its append runs after the loop, which then resumes) and, FT (a row of the
+// block can fudge: T > 2^(prec-1)), at a fudged step, before it changes anything; so one
+// exit test per step (two with FT).  Returns the first step not done (n at the block's
+// end); results, registers and error steps are coder_step's.
+struct SP {
+    uint64_t lo, hi, tot, flo, fhi, fthr;              // this lane's row values (lane i: step i)
+    int n, prec;
+    uint64_t cap_words, *pa, *pc;
+    int lane;
+};
+template <bool CEIL, bool T32, bool FT>
+__device__ inline int straight_steps(const SP &sp, EncState &st, int64_t &l, int64_t &h, bool &ok) {
+    auto store = [&](uint64_t idx, uint64_t wa, uint64_t wc) {
+        if (sp.lane == 0) { sp.pa[idx] = wa; sp.pc[idx] = wc; }
+    };
+    typedef typename std::conditional<T32, uint32_t, uint64_t>::type CT;   // counts and totals
+    struct Row {
+        CT lo, hi, T;
+        uint64_t fl, fh, ft;
+    };
+    auto rd = [&](int j) {
+        Row r;
+        if constexpr (T32) {
+            r.lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)sp.lo, j);
+            r.hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)sp.hi, j);
+            r.T = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)sp.tot, j);
+        } else {
+            r.lo = readlane_u64(sp.lo, j);
+            r.hi = readlane_u64(sp.hi, j);
+            r.T = readlane_u64(sp.tot, j);
+        }
+        r.fl = readlane_u64(sp.flo, j);
+        r.fh = readlane_u64(sp.fhi, j);
+        r.ft = FT ? readlane_u64(sp.fthr, j) : 0;
+        return r;
+    };
+    const int n = sp.n, prec = sp.prec;
+    const int64_t nsym0 = st.nsym;
+    Row nx = rd(0);
+    int i = 0;
+    int kk = 0;
+    uint64_t e = 0;
+    bool fudged = false;
+    while (i < n) {
+        for (; i < n; i++) {
+            const Row r = LAC_ENC_PIPE ? nx : rd(i);
+            if constexpr (LAC_ENC_PIPE) nx = rd(i + 1 < n ? i + 1 : i);
+            const uint64_t w = (uint64_t)(h - l + 1);
+            if constexpr (FT) {
+                if (!nonneg_uni((int64_t)(w - r.ft))) {         // fudged (arith_code.py:84): the general step
+                    fudged = true;
+                    break;
+                }
+            }
+            uint64_t a, bb;
+            if constexpr (T32) {
+                a = frac_mul_div32<CEIL>(r.fl, r.lo, w, r.T);
+                bb = frac_mul_div32<CEIL>(r.fh, r.hi, w, r.T);
+            } else {
+                a = frac_mul_div<true>(r.fl, r.lo, w, r.T, CEIL);
+                bb = frac_mul_div<true>(r.fh, r.hi, w, r.T, CEIL);
+            }
+            h = l + (int64_t)bb - 1;
+            l = l + (int64_t)a;
+            const uint64_t d = (uint64_t)(h - l);
+            const int sh = bitlen64(d);
+            kk = prec - sh;
+            e = kk > 0 ? (uint64_t)l >> sh : 0;
+            l = (int64_t)(((uint64_t)l - (e << sh)) << kk);
+            h = l + (int64_t)((d + 1) << kk) - 1;
+            const int off0 = (int)(st.L & 63);
+            const int avail = off0 ? 64 - off0 : 0;
+            if (__builtin_expect(kk > avail, 0)) break;
+            st.wc |= (e >> kk) << ((64 - off0) & 63);
+            st.wa |= (e & ((1ull << kk) - 1)) << ((64 - off0 - kk) & 63);
+            st.L += (uint64_t)kk;
+        }
+        if (i >= n) break;
+        if constexpr (FT) {
+            if (fudged) break;                              // step i for the general loop
+        }
+        if (!plane_append(st.L, st.wa, st.wc, kk, e, sp.cap_words, store)) {   // step i's crossing
+            st.err = LAC_E_CAPACITY;
+            ok = false;
+            break;
+        }
+        i++;
+    }
+    st.nsym = nsym0 + i;
+    return i;
 }
 
 // k_encode: one wave per stream over a chunk of steps; lane i prefetches the
@@ -104,7 +203,41 @@ __global__ __launch_bounds__(256) void k_encode(const RowStats *__restrict__ sta
         const bool frac_ok = lane < n && !(my.tot >> 62);
         const uint64_t flo = frac_ok ? row_frac(my.lo, my.tot) : kNoFrac;
         const uint64_t fhi = frac_ok ? row_frac(my.hi, my.tot) : kNoFrac;
+        int i0 = 0;                                       // the first step the general loop takes
 #if LAC_ENC_STRAIGHT
+        if constexpr (sizeof(E) == 8) {
+            // u64 tables: the straight form of straight_steps -- every step's row with
+            // 0 < T < 2^62, a positive width at the symbol (for the floor mapping also
+            // T <= 2^(prec-1) (hi - lo), so its two quotients differ by >= 1) and an in-range
+            // symbol, and the state's width in (2^(prec-1), 2^prec]: no step can then meet a
+            // zero width unfudged or leave that width range, and only rows with
+            // T > 2^(prec-1) can fudge -- a fudged step leaves for the general loop below,
+            // which takes the rest of the block.  (The u32 kernel keeps only the form below:
+            // written beside these, its loop compiled ~3 % slower, profiles/r05/straight/.)
+            const uint64_t half = 1ull << (prec - 1);
+            const bool lfast = lane >= n || (frac_ok && my.tot != 0 && my.hi > my.lo && (uint32_t)mys < (uint32_t)V &&
+                                             (MAP != LAC_MAP_FLOOR || ((my.tot - 1) >> (prec - 1)) < my.hi - my.lo));
+            const uint64_t d0 = (uint64_t)(h - l);
+            if (!trace && prec <= 61 && __ballot(!lfast) == 0 && nonneg_uni((int64_t)(d0 - half)) &&
+                !(d0 >> prec)) {
+                constexpr bool CEIL = MAP != LAC_MAP_FLOOR;
+                const bool t32 = __ballot(lane < n && (my.tot >> 32)) == 0;
+                const bool ft = CEIL && __ballot(lane < n && my.tot > half) != 0;   // a row that can fudge
+                uint64_t ftl = 0;
+                if (ft) {
+                    ftl = lane < n && my.minp ? div_floor((u128)my.tot + (my.minp - 1), my.minp) : 0;
+                    ftl = ftl < (1ull << 62) ? ftl : (1ull << 62);
+                }
+                SP sp{my.lo, my.hi, my.tot, flo, fhi, ftl, n, prec, cap_words, pa, pc, lane};
+                if (t32)
+                    i0 = ft ? straight_steps<CEIL, true, true>(sp, st, l, h, ok)
+                            : straight_steps<CEIL, true, false>(sp, st, l, h, ok);
+                else
+                    i0 = ft ? straight_steps<CEIL, false, true>(sp, st, l, h, ok)
+                            : straight_steps<CEIL, false, false>(sp, st, l, h, ok);
+                if (!ok || i0 >= n) continue;
+            }
+        }
         // The block's straight form: when every step's row has 0 < T <= 2^(prec-1) < 2^32, a
         // positive width at the symbol and an in-range symbol, and the state's width is in
         // (2^(prec-1), 2^prec] (every renormalised state's is), no step can fudge
@@ -113,7 +246,7 @@ __global__ __launch_bounds__(256) void k_encode(const RowStats *__restrict__ sta
         // step two mul-divs in 32 x 64-bit products, a branch-free renormalisation and the
         // plane append's one-word case, one rarely taken branch (the append crossing a
         // word).  Results, registers and error steps are coder_step's.
-        {
+        if (i0 == 0) {
             const uint64_t half = 1ull << (prec - 1);
             const bool lfast = lane >= n || (frac_ok && my.tot != 0 && my.tot <= half && !(my.tot >> 32) &&
                                              my.hi > my.lo && (uint32_t)mys < (uint32_t)V);
@@ -188,7 +321,7 @@ __global__ __launch_bounds__(256) void k_encode(const RowStats *__restrict__ sta
         uint64_t fthr = lane < n && my.minp ? div_floor((u128)my.tot + (my.minp - 1), my.minp) : 0;
         fthr = fthr < (1ull << 62) ? fthr : (1ull << 62);   // w <= 2^61: w < fthr unchanged (coder_step's sign test)
         if (clk) clk->mark(4);
-        for (int i = 0; i < n; i++) {
+        for (int i = i0; i < n; i++) {
             const uint64_t lo = readlane_u64(my.lo, i), hi = readlane_u64(my.hi, i);
             const uint64_t T = readlane_u64(my.tot, i), minp = readlane_u64(my.minp, i);
             const uint64_t invb = readlane_u64(__builtin_bit_cast(uint64_t, my.inv_tot), i);
