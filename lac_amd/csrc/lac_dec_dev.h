@@ -289,6 +289,30 @@ __device__ inline int decode_advance(DecState &st, uint64_t a, uint64_t bb, cons
     return 0;
 }
 
+#ifndef LAC_Q1D_NB
+#define LAC_Q1D_NB 1             // k_q1_decode and k_decode_seq: decode_advance_nb (no renormalisation branches)
+#endif
+// decode_advance<true> with no branch past its range test (k_q1_decode, LAC_Q1D_NB):
+// renorm()'s kk <= 0 case as kk = 0 (e = 0 keeps the registers), window_bits_nb.
+__device__ inline int decode_advance_nb(DecState &st, uint64_t a, uint64_t bb, const BitWin &win, uint64_t nbits,
+                                        int prec) {
+    const int64_t l = st.l, x = st.x;
+    if (!((l + (int64_t)a) <= x && x <= l + (int64_t)bb - 1)) return LAC_E_DECODE_RANGE;  // :277-278
+    int64_t nl = l + (int64_t)a, nh = l + (int64_t)bb - 1;
+    const uint64_t d = (uint64_t)(nh - nl);
+    const int sh = bitlen64(d), k0 = prec - sh, k = k0 > 0 ? k0 : 0;
+    const uint64_t Ev = k > 0 ? (uint64_t)nl >> sh : 0;
+    nl = (int64_t)(((uint64_t)nl - (Ev << (sh & 63))) << k);
+    nh = nl + (int64_t)((d + 1) << k) - 1;
+    const BitWin wu{rfl_u64(win.w0), rfl_u64(win.w1)};
+    st.x = (int64_t)((((uint64_t)x - (Ev << (sh & 63))) << k) | window_bits_nb(wu, nbits, st.pos, k));
+    st.pos += (uint64_t)k;
+    st.l = nl;
+    st.h = nh;
+    st.nsym++;
+    return 0;
+}
+
 // Per-phase cycle accounting of the sequential decode step (tools/dec_phase_probe.sh
 // builds a separate library with -DLAC_DEC_PHASES=1; the product build passes no clock
 // and the marks compile to nothing).  Phases: 0 row totals + scan, 1 targets, 2 chunk
@@ -414,7 +438,9 @@ __device__ inline int decode_symbol(DecState &st, const E *row, int64_t V, uint6
     if (st.det && det) st.ndet++;
     else st.det = 0;
     *s_out = s;
-    const int rc = decode_advance<UNI>(st, a, bb, win, nbits, prec);
+    // (UNI, the lone-wave k_decode_seq: the renormalisation without branches, as k_q1_decode)
+    const int rc = (UNI && LAC_Q1D_NB) ? decode_advance_nb(st, a, bb, win, nbits, prec)
+                                        : decode_advance<UNI>(st, a, bb, win, nbits, prec);
     mark(5);
     return rc;
 }

@@ -1094,12 +1094,12 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ pmf, i
             // registers, and window_bits_nb(.., 0) is 0
             int64_t nl = l + (int64_t)a, nh = l + (int64_t)bb - 1;
             const uint64_t d = (uint64_t)(nh - nl);
-            const int sh = bitlen64(d), kk = prec - sh;
+            const int sh = bitlen64(d), kk0 = prec - sh, kk = kk0 > 0 ? kk0 : 0;   // (renorm: kk <= 0 is 0)
             const uint64_t Ev = kk > 0 ? (uint64_t)nl >> sh : 0;
-            nl = (int64_t)(((uint64_t)nl - (Ev << sh)) << kk);
+            nl = (int64_t)(((uint64_t)nl - (Ev << (sh & 63))) << kk);
             nh = nl + (int64_t)((d + 1) << kk) - 1;
             const BitWin wu{rfl_u64(win.w0), rfl_u64(win.w1)};
-            x = (int64_t)((((uint64_t)x - (Ev << sh)) << kk) | window_bits_nb(wu, mynbits, pos, kk));
+            x = (int64_t)((((uint64_t)x - (Ev << (sh & 63))) << kk) | window_bits_nb(wu, mynbits, pos, kk));
             pos += (uint64_t)kk;
             l = nl;
             h = nh;

@@ -1711,7 +1711,8 @@ __global__ LAC_DEC_BOUNDS void k_q1_decode(const LT *__restrict__ lg, int64_t st
                     const bool det = vh < w && thi < hi_c;
                     if (st.det && det) st.ndet++;
                     else st.det = 0;
-                    err = decode_advance<true>(st, a, bb, win, mynbits, prec);
+                    err = LAC_Q1D_NB ? decode_advance_nb(st, a, bb, win, mynbits, prec)
+                                     : decode_advance<true>(st, a, bb, win, mynbits, prec);
                 }
             }
         }
