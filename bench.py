@@ -182,17 +182,25 @@ def main():
     # N > 1: each job's bitstreams go to rank 0 over RCCL, packed and sized to the
     # payload, --gather-batch jobs per exchange, overlapping the next jobs' encodes
     gatherer = BitstreamGatherer(coder, batch=args.gather_batch) if (world > 1 or args.gather) else None
+    # with a gather, consecutive jobs code different symbols (the streams' symbols rolled by
+    # 0..3 across streams, prepared before timing), so a job unpacked at another job's
+    # offset cannot pass gather_ok; the last timed job codes `sym` itself (the oracle check)
+    nvar = 4 if gatherer else 1
+    symv = [sym] + [torch.roll(sym, k, dims=1).contiguous() for k in range(1, nvar)]
+    job_variant = []
 
-    def job():
+    def job(v=0):
+        s_ = symv[v]
         if logits_in:
-            coder.encode_logits_job(pmf, sym)
+            coder.encode_logits_job(pmf, s_)
         else:
-            coder.encode_job(pmf, sym)
+            coder.encode_job(pmf, s_)
         if gatherer:
             gatherer.submit()
+            job_variant.append(v)
 
-    for _ in range(args.warmup):
-        job()
+    for i in range(args.warmup):
+        job(i % nvar)
     if gatherer:
         gatherer.drain()                                   # the timed region holds its own jobs' gathers
     torch.cuda.synchronize()
@@ -202,8 +210,8 @@ def main():
     coder.lib.lac_profile_read(coder.ctx, None, None, 1)
     coder.lib.lac_profile_enable(coder.ctx, 1)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        job()
+    for i in range(args.steps):
+        job((args.steps - 1 - i) % nvar)
     if gatherer:
         gatherer.drain()                                   # every gather is inside the timed region
     torch.cuda.synchronize()
@@ -223,20 +231,34 @@ def main():
     # ---------------- checks, outside the timed region
     gather_ok = None
     gather_info = None
-    if gatherer:                                           # the root's last job == every rank's own bits
+    if gatherer:
+        # every job the root still holds (the last `depth` batches) == every rank's own
+        # bits for that job's symbols, coded again by a separate coder and collected by a
+        # separate exact-width all-gather
         from lac_amd.dist import bitstreams_equal, gather_bitstreams
-        mine_b = coder.bits_tensor()
-        mine_n = coder.nbits_tensor()
-        ref_b, ref_n = gather_bitstreams(mine_b, mine_n)   # a separate, exact-width all-gather
+        refc = BatchCoder(V, B, prec=P, pmf_bits=args.pmf_bits, capacity_bits=T * (P + 2) + 256, device=dev)
+        refs = []
+        for v in range(nvar):
+            if logits_in:
+                refc.encode_logits_job(pmf, symv[v])
+            else:
+                refc.encode_job(pmf, symv[v])
+            refs.append(gather_bitstreams(refc.bits_tensor(), refc.nbits_tensor()))
+        refc.close()
         okg = True
+        checked = 0
         if rank == 0:
-            gb, gn = gatherer.last_unpacked()
-            okg = bitstreams_equal(gb, gn, ref_b, ref_n)
+            for j in gatherer.finished_jobs:
+                gb, gn = gatherer.last_unpacked(j)
+                okg = okg and bitstreams_equal(gb, gn, *refs[job_variant[j - 1]])
+                checked += 1
+            okg = okg and checked > 0
         flag = torch.tensor([1 if okg else 0], device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         gather_ok = bool(flag.item())
         jobs = max(gatherer.jobs, 1)
-        gather_info = {"to_rank": 0, "link_bytes_per_job": gatherer.bytes_sent / jobs,
+        gather_info = {"to_rank": 0, "jobs_checked": checked, "symbol_variants": nvar,
+                       "link_bytes_per_job": gatherer.bytes_sent / jobs,
                        "payload_bytes_per_job": gatherer.payload_bytes / jobs,
                        "header_bytes_per_stream": gatherer.hdr, "jobs_per_exchange": gatherer.batch,
                        "host_meta_bytes_per_job": gatherer.meta_bytes / jobs}
@@ -331,12 +353,16 @@ def main():
         exact = bool(ok.item())
     parity.update({"oracle_streams_checked": S * world, "oracle_ranks_checked": world,
                    "bit_exact_vs_oracle": bool(exact)})
+    if dist:
+        dist.barrier()                                     # every rank's parity run is over
     if rank == 0:
         if args.cpu_baseline == "on":
-            # cpu_baseline: repeat the same bounded sample until >= --cpu-seconds of CPU
-            # work (the first repetition above was the parity check); other ranks wait
-            reps = 1
-            while c1 - c0 < args.cpu_seconds:
+            # cpu_baseline: repetitions of the same bounded sample of their own, timed from
+            # here until >= --cpu-seconds of CPU work (the parity run above is not counted: at
+            # N > 1 it overlapped the other ranks' own parity runs); other ranks wait
+            reps = 0
+            c0 = c1 = time.perf_counter()
+            while reps == 0 or c1 - c0 < args.cpu_seconds:
                 tabs = coracle.q1_quantize(host, P) if logits_in else host
                 coracle.encode_batch(tabs, hsym, P, nthreads=nthreads)
                 reps += 1

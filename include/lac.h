@@ -240,7 +240,16 @@ int lac_pack_jobs(int device, const uint64_t *planeA_dev, uint64_t plane_stride,
  * (encode, finish, lac_copy_bits*, lac_encoded_*, lac_pack_bits*, lac_decode_open
  * with no bits) uses them, so consecutive jobs can leave their output in separate
  * buffers with no copy (lac_amd.dist.BitstreamGatherer packs a batch of them at once,
- * off the encode's stream).  The context is not finished afterwards. */
+ * off the encode's stream).
+ * Only between jobs: LAC_E_STATE (nothing changed) while a decode is open, or while the
+ * streams hold coded symbols that are not finished -- an lac_encode / lac_encode_logits
+ * call (or an lac_encode_set_state with symbols) since the last lac_encode_reset, not yet
+ * followed by lac_encode_finish: those streams have written part of their planes to the
+ * current buffers, and the finish would carry-add over the new ones.  Redirect before a
+ * job's first call (lac_encode_job does its own reset) or after it finished.
+ * Afterwards the context counts as finished (lac_pack_bits*) exactly when the new
+ * buffers are the ones its last finished job was written to (showing that job again);
+ * any other buffers need the next finished job first. */
 int lac_set_output(lac_ctx *ctx, uint64_t *planeA_dev, uint64_t *nbits_dev);
 
 /* Pinned host memory mapped into the device's address space, coherent (kernels'

@@ -322,7 +322,11 @@ class BatchCoder:
         """Direct later encodes' output (plane A and the bit counts, include/lac.h
         lac_set_output) into caller-owned device tensors: ``planes`` of >= streams *
         cap_words + 1 int64 (``output_words()``), ``nbits`` of streams int64; None, None
-        restores the coder's own.  The tensors are kept referenced while in use."""
+        restores the coder's own.  The tensors are kept referenced while in use.
+        Only between jobs: raises LacError(LAC_E_STATE) while a decode is open or an
+        encode has coded symbols it has not finished (``encode`` since ``reset``, no
+        ``finish`` yet).  Afterwards the coder counts as finished (``pack_bits``) only
+        when the buffers are those its last finished job went to."""
         if (planes is None) != (nbits is None):
             raise ValueError("planes and nbits: both or neither")
         if planes is not None:

@@ -640,6 +640,7 @@ int lac_encode_reset(lac_ctx *c, void *stream) {
     HIPCHK(hipSetDevice(c->device));
     c->mode = 0;
     c->finished = 0;
+    c->open = 0;
     k_enc_reset<<<(unsigned)((c->B + 255) / 256), 256, 0, S(stream)>>>(c->enc, c->B, c->prec);
     CHECK_LAUNCH();
     return LAC_OK;
@@ -658,7 +659,7 @@ int lac_encode(lac_ctx *c, const void *pmf_dev, int64_t step_stride, int64_t str
                int64_t steps, uint64_t *trace_dev, void *stream) {
     if (c && c->mode != 0) return fail(LAC_E_STATE, "context is decoding; call lac_encode_reset first");
     const int rc = encode_dispatch(c, pmf_dev, step_stride, stream_stride, sym_dev, steps, trace_dev, stream, 0);
-    if (rc == LAC_OK && steps > 0) c->finished = 0;
+    if (rc == LAC_OK && steps > 0) enc_mark_open(c);
     return rc;
 }
 
@@ -666,7 +667,7 @@ int lac_encode_job(lac_ctx *c, const void *pmf_dev, int64_t step_stride, int64_t
                    const int32_t *sym_dev, int64_t steps, uint64_t *trace_dev, void *stream) {
     const int rc = encode_dispatch(c, pmf_dev, step_stride, stream_stride, sym_dev, steps, trace_dev, stream,
                                    kReset | kFinish);
-    if (rc == LAC_OK) c->finished = 1;
+    if (rc == LAC_OK) enc_mark_finished(c);
     return rc;
 }
 
@@ -675,7 +676,7 @@ int lac_encode_finish(lac_ctx *c, void *stream) {
     if (c->mode != 0) return fail(LAC_E_STATE, "context is decoding");
     HIPCHK(hipSetDevice(c->device));
     ProfScope ps(c, KID_FINISH, S(stream));
-    c->finished = 1;
+    enc_mark_finished(c);
     k_finish<<<(unsigned)((c->B + 255) / 256), 256, 0, S(stream)>>>(c->enc, c->planeA, c->planeC, c->cap_words, c->B,
                                                                    c->prec, c->nbits, c->term);
     CHECK_LAUNCH();
@@ -714,9 +715,16 @@ int lac_set_output(lac_ctx *c, uint64_t *planeA_dev, uint64_t *nbits_dev) {
     if (!c) return fail(LAC_E_ARG, "ctx is NULL");
     if (!planeA_dev != !nbits_dev) return fail(LAC_E_ARG, "planeA_dev and nbits_dev: both or neither");
     if ((uintptr_t)planeA_dev % 8 || (uintptr_t)nbits_dev % 8) return fail(LAC_E_ARG, "buffers must be 8-byte aligned");
+    // Only between jobs: an open encode has written part of its planes to the current
+    // buffers, and k_finish would carry-add over the new ones (silently wrong bytes).
+    if (c->mode != 0) return fail(LAC_E_STATE, "context is decoding; redirect the output between encode jobs");
+    if (c->open)
+        return fail(LAC_E_STATE, "streams hold coded symbols that are not finished: redirect the output before "
+                                 "the job's first encode call or after lac_encode_finish / lac_encode_reset");
     c->planeA = planeA_dev ? planeA_dev : c->own_planeA;
     c->nbits = nbits_dev ? nbits_dev : c->own_nbits;
-    c->finished = 0;
+    // finished again exactly when the new buffers are the ones the last finished job went to
+    c->finished = c->fin_planeA && c->planeA == c->fin_planeA && c->nbits == c->fin_nbits;
     return LAC_OK;
 }
 
@@ -770,6 +778,8 @@ int lac_encode_set_state(lac_ctx *c, const lac_enc_state *host_in, const uint64_
             q.nflush < -1 || q.nflush > 8)
             return fail(LAC_E_ARG, "stream %lld: encoder registers out of range", (long long)b);
     }
+    bool coded = false;
+    for (int64_t b = 0; b < c->B; b++) coded = coded || host_in[b].nsym > 0 || host_in[b].L > 0;
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipMemcpyAsync(c->enc, host_in, sizeof(EncState) * c->B, hipMemcpyHostToDevice, S(stream)));
     if (planes_host) {
@@ -778,6 +788,7 @@ int lac_encode_set_state(lac_ctx *c, const lac_enc_state *host_in, const uint64_
         HIPCHK(hipMemcpyAsync(c->planeC, planes_host + c->cap_words * c->B, n, hipMemcpyHostToDevice, S(stream)));
     }
     c->finished = 0;
+    c->open = coded ? 1 : 0;
     HIPCHK(hipStreamSynchronize(S(stream)));
     return LAC_OK;
 }

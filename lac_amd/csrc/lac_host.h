@@ -25,6 +25,9 @@ struct lac_ctx {
     const uint64_t *dnbits = nullptr;
     int mode = 0;                       // 0 encode, 1 decode
     int finished = 0;                   // nbits / planeA hold finished streams (a job, lac_encode_finish)
+    int open = 0;                       // streams hold coded symbols since the last reset and are not
+                                        // finished: their output is split between calls (lac_set_output refuses)
+    const uint64_t *fin_planeA = nullptr, *fin_nbits = nullptr;   // where the last finished job was written
     int path = LAC_PATH_AUTO;           // encode kernel path (lac_set_option)
     int64_t fused_min_streams = 2048;   // AUTO: fused kernel from this many streams
     int64_t chunk_steps = 64;           // split path: steps per row-stats launch
@@ -108,6 +111,19 @@ int fail(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
 #define CHECK_LAUNCH() HIPCHK(hipGetLastError())
 
 static inline hipStream_t S(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Encode bookkeeping for lac_set_output / lac_pack_bits: a call that coded symbols leaves the
+// streams open; a job or finish closes them and records which buffers hold the result.
+static inline void enc_mark_open(lac_ctx *c) {
+    c->open = 1;
+    c->finished = 0;
+}
+static inline void enc_mark_finished(lac_ctx *c) {
+    c->open = 0;
+    c->finished = 1;
+    c->fin_planeA = c->planeA;
+    c->fin_nbits = c->nbits;
+}
 
 // encode family (lac_encode.hip), for the logits path's encode (q1_encode)
 int enc_reset_launch(lac_ctx *c, hipStream_t st);

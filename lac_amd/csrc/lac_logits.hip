@@ -2209,7 +2209,7 @@ int lac_encode_logits_job(lac_ctx *c, const void *logits_dev, int logit_type, in
                           void *stream) {
     const int rc = logits_encode(c, logits_dev, logit_type, step_stride, stream_stride, sym_dev, steps, trace_dev,
                                  stream, kReset | kFinish);
-    if (rc == LAC_OK) c->finished = 1;
+    if (rc == LAC_OK) enc_mark_finished(c);
     return rc;
 }
 
@@ -2218,7 +2218,7 @@ int lac_encode_logits(lac_ctx *c, const void *logits_dev, int logit_type, int64_
                       void *stream) {
     const int rc = logits_encode(c, logits_dev, logit_type, step_stride, stream_stride, sym_dev, steps, trace_dev,
                                  stream, 0);
-    if (rc == LAC_OK && steps > 0) c->finished = 0;
+    if (rc == LAC_OK && steps > 0) enc_mark_open(c);
     return rc;
 }
 

@@ -3,13 +3,18 @@
 Streams are independent (no coder state crosses streams), so each rank owns a
 contiguous block of streams, ``[r*B, (r+1)*B)``, and encodes it with no
 collective at all.  The only exchange is collecting the variable-length
-bitstreams afterwards: RCCL has no gather-v, so ranks
-first agree on the widest stream (an all-reduce MAX of one int64) and then
-all-gather fixed-width slots of that width plus the per-stream bit counts.
-Decoding reverses it: ``scatter_bitstreams`` hands each rank its shard of a
-job's bitstreams from the rank that holds them.
-With the ``nccl`` backend (RCCL on ROCm) the tensors stay in HBM and move
-over xGMI; with ``gloo`` (tests) they are CPU tensors.
+bitstreams on one rank.
+
+The path bench.py times is ``BitstreamGatherer``: jobs are encoded straight into
+job slots, a whole batch of them is packed by one kernel on a side stream, the
+packed lengths travel between hosts (gloo), and one grouped exact-size send/recv
+per batch moves every rank's packed bytes point to point to the root (RCCL over
+xGMI under ``nccl``; host copies under ``gloo``).  No all-gather and no padding.
+
+``gather_bitstreams`` is the one-off helper (an all-reduce MAX of the widest
+stream, then an all-gather of fixed-width slots and the bit counts), and decoding
+reverses the exchange with ``scatter_bitstreams``, which hands each rank its
+shard of a job's bitstreams from the rank that holds them.
 """
 from __future__ import annotations
 
@@ -203,6 +208,23 @@ class HostWords:
             self._h = self._d = None
 
 
+_HOST_GROUPS = {}
+
+
+def host_group(group=None):
+    """A gloo group over the ranks of ``group`` (default: the whole world) for the
+    gatherer's host-side size exchange, made once per rank set.  ``dist.new_group`` is
+    collective over the default group: every rank of the default world calls this in
+    the same order."""
+    import torch.distributed as dist
+    ranks = tuple(dist.get_process_group_ranks(group)) if group is not None else tuple(range(dist.get_world_size()))
+    world = dist.group.WORLD
+    hit = _HOST_GROUPS.get(ranks)
+    if hit is None or hit[0] is not world:                   # (a re-initialised world: make it again)
+        hit = _HOST_GROUPS[ranks] = (world, dist.new_group(ranks=list(ranks), backend="gloo"))
+    return hit[1]
+
+
 class BitstreamGatherer:
     """Bitstreams of back-to-back compression jobs gathered to one rank, sized to
     the payload, in batches of jobs (the path's one exchange).
@@ -248,7 +270,7 @@ class BitstreamGatherer:
     META = 4                                                 # int64 per rank ahead of the lengths
 
     def __init__(self, coder, group=None, batch: int = 8, depth: int = 3, root: int = 0, self_p2p=None,
-                 lag=None):
+                 lag=None, meta_group=None):
         import torch
         import torch.distributed as dist
         self.coder, self.group, self.root = coder, group, int(root)
@@ -265,12 +287,16 @@ class BitstreamGatherer:
         self.gloo = dist.get_backend(group) == "gloo"
         self.self_p2p = (not self.gloo) if self_p2p is None else bool(self_p2p)
         # sizes travel between hosts, never through the GPU: the group itself under
-        # gloo, else a gloo group over the same ranks (created collectively, once)
+        # gloo, else ``meta_group`` (a gloo group over the same ranks) or one made here.
+        # dist.new_group is collective over the whole default group, so without a
+        # meta_group every rank of the default world constructs the gatherer (ranks
+        # outside ``group`` too); the group is made once per rank set and reused.
         if self.gloo:
             self.meta_group = group
+        elif meta_group is not None:
+            self.meta_group = meta_group
         else:
-            ranks = dist.get_process_group_ranks(group) if group is not None else list(range(self.world))
-            self.meta_group = dist.new_group(ranks=ranks, backend="gloo")
+            self.meta_group = host_group(group)
         self.width = coder.bits_stride()                      # cap_words * 8 bytes per stream
         self.hdr = 2 if self.width * 8 < (1 << 16) else 4
         B, dev = coder.streams, coder.device
@@ -435,15 +461,21 @@ class BitstreamGatherer:
         self._t("packed", i)
         n = len(bx["jobs"])
         lens = [bx["lens"][j] for j in range(n)]
-        if any(v >= 1 << 63 for v in lens):
-            raise RuntimeError("a packed job did not fit its outbox")
+        # a failure travels in the metadata (job count -1) and every rank raises after the
+        # exchange, before any send/recv is posted: raising alone would leave the other
+        # ranks waiting in the all-gather or the P2P batch
+        overflow = any(v >= 1 << 63 for v in lens)
         mine = torch.zeros(self.META + self.batch, dtype=torch.int64)
-        mine[:self.META] = torch.tensor([n, self.B, self.width, self.hdr])
-        mine[self.META:self.META + n] = torch.tensor(lens, dtype=torch.int64)
+        mine[:self.META] = torch.tensor([-1 if overflow else n, self.B, self.width, self.hdr])
+        if not overflow:
+            mine[self.META:self.META + n] = torch.tensor(lens, dtype=torch.int64)
         meta = torch.empty((self.world, self.META + self.batch), dtype=torch.int64)
         _all_gather(meta.view(-1), mine, self.meta_group, self.world)
         rows = meta.tolist()
         self._t("meta", i)
+        bad = [r for r, row in enumerate(rows) if row[0] < 0]
+        if bad:
+            raise RuntimeError(f"a packed job did not fit its outbox on rank(s) {bad}")
         if any(row[0] != n for row in rows):
             raise RuntimeError(f"ranks disagree on the batch's job count: {[row[0] for row in rows]}")
         tot = [sum(row[self.META:self.META + n]) for row in rows]

@@ -133,8 +133,11 @@ def softmax_tables(steps: int, streams: int, V: int, seed: int = 1234, device="c
         out = torch.empty((steps, streams, V), dtype=dt, device=device)
     sym = torch.empty((steps, streams), dtype=torch.int32, device=device)
     floor_v = 2 if scale_bits >= 60 else 1
+    # one generator, reseeded per step: the same streams as a fresh generator per step
+    # (tests/test_gpu_api.py), without thousands of device generators (4096 of them
+    # crashed torch.randn on the host under rocprofv3 --pmc, round 5)
+    g = torch.Generator(device=device)
     for t in range(steps):
-        g = torch.Generator(device=device)
         g.manual_seed(seed + t)
         logits = torch.randn((streams, V), generator=g, device=device, dtype=torch.float32) * sigma
         p = torch.softmax(logits.double(), dim=-1)
@@ -160,8 +163,8 @@ def logits_batch(steps: int, streams: int, V: int, seed: int = 1234, device="cud
     dtype = dtype or torch.bfloat16
     out = torch.empty((steps, streams, V), dtype=dtype, device=device)
     sym = torch.empty((steps, streams), dtype=torch.int32, device=device)
+    g = torch.Generator(device=device)                         # (reseeded per step, as above)
     for t in range(steps):
-        g = torch.Generator(device=device)
         g.manual_seed(seed + t)
         out[t] = (torch.randn((streams, V), generator=g, device=device, dtype=torch.float32) * sigma).to(dtype)
         q = quantise(out[t:t + 1])[0].to(torch.int64) & 0xFFFFFFFF

@@ -570,3 +570,32 @@ def test_acsampler_per_token_pdfs_bits_and_entropy():
         s.flush_compress()
         assert "".join(map(str, bits)) == case["bits"]
         assert ent == case["entropy"]
+
+
+def test_synth_tables_one_generator_equal_per_step_generators():
+    """synth.softmax_tables / logits_batch reseed one torch.Generator per step: the tables
+    and symbols equal the per-step-generator form they replaced (thousands of
+    device generators crashed torch.randn under rocprofv3 --pmc)."""
+    import torch
+    from lac_amd import synth
+    dev = "cuda"
+    T, B, V, seed = 5, 7, 1000, 99
+    for scale, bits in ((31, 32), (60, 64)):
+        got, gs = synth.softmax_tables(T, B, V, seed=seed, device=dev, scale_bits=scale, storage_bits=bits)
+        for t in range(T):
+            g = torch.Generator(device=dev)
+            g.manual_seed(seed + t)
+            logits = torch.randn((B, V), generator=g, device=dev, dtype=torch.float32) * 3.0
+            q = torch.clamp(torch.floor(torch.softmax(logits.double(), dim=-1) * float(1 << scale)),
+                            min=2 if scale >= 60 else 1).to(torch.int64)
+            cdf = torch.cumsum(q, dim=-1)
+            u = torch.rand((B,), generator=g, device=dev, dtype=torch.float64)
+            tgt = torch.minimum((u * cdf[:, -1].double()).floor().long(), cdf[:, -1] - 1)
+            s = torch.searchsorted(cdf, tgt.unsqueeze(1), right=True).squeeze(1).to(torch.int32)
+            assert torch.equal(got[t], q.to(got.dtype)) and torch.equal(gs[t], s), (scale, t)
+    lg, _ = synth.logits_batch(T, B, V + 8, seed=seed, device=dev, quantise=lambda x: x.float().to(torch.int64))
+    for t in range(T):
+        g = torch.Generator(device=dev)
+        g.manual_seed(seed + t)
+        want = (torch.randn((B, V + 8), generator=g, device=dev, dtype=torch.float32) * 3.0).to(torch.bfloat16)
+        assert torch.equal(lg[t], want), t

@@ -197,3 +197,56 @@ def test_pack_bits_kernel_equals_torch_packing(nccl_world1, hdr):
     coder.pack_bits(out, hdr, ln)
     assert int(ln) == B * hdr
     coder.close()
+
+
+def test_set_output_only_between_jobs():
+    """lac_set_output refuses a redirect while streams hold unfinished coded symbols (their
+    plane words are split between buffers: the finish would carry-add over the new ones)
+    and while decoding; between jobs it redirects, and a redirect back to the buffers of
+    the last finished job shows that job again (lac_pack_bits packs it)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from lac_amd.batch import BatchCoder
+    from lac_amd._lib import LacError, LAC_E_STATE
+    from lac_amd.dist import pack_bitstreams
+    from lac_amd import synth
+    dev = torch.device("cuda", 0)
+    V, B, T = 1000, 40, 8
+    coder = BatchCoder(V, B, prec=48, capacity_bits=T * 50 + 256, device=dev)
+    words = coder.output_words()
+    planes = torch.zeros((2, words), dtype=torch.int64, device=dev)
+    nbits = torch.zeros((2, B), dtype=torch.int64, device=dev)
+    pmf, sym = synth.make_batch(77, T, B, V, "loguniform")
+    dpmf, dsym = torch.from_numpy(pmf.view(np.int32)).to(dev), torch.from_numpy(sym).to(dev)
+    coder.set_output(planes[0], nbits[0])                   # fresh context: allowed
+    coder.reset()
+    coder.encode(dpmf[:T // 2], dsym[:T // 2])              # an open encode ...
+    with pytest.raises(LacError) as e:
+        coder.set_output(planes[1], nbits[1])
+    assert e.value.code == LAC_E_STATE
+    coder.encode(dpmf[T // 2:], dsym[T // 2:])
+    coder.finish()                                          # ... finished: the bytes are whole
+    want_b, want_n = coder.bits_tensor().clone(), coder.nbits_tensor().clone()
+    ref = BatchCoder(V, B, prec=48, capacity_bits=T * 50 + 256, device=dev)
+    ref.encode_job(dpmf, dsym)
+    assert torch.equal(want_n, ref.nbits_tensor()) and torch.equal(want_b, ref.bits_tensor())
+    coder.set_output(planes[1], nbits[1])                   # between jobs
+    coder.encode_job(dpmf, dsym)
+    assert torch.equal(coder.nbits_tensor(), want_n)
+    coder.set_output(planes[0], nbits[0])                   # the previous job's buffers: not finished
+    out = torch.zeros(B * (2 + coder.bits_stride()) + 1, dtype=torch.uint8, device=dev)
+    ln = torch.zeros(1, dtype=torch.int64, device=dev)
+    with pytest.raises(LacError):
+        coder.pack_bits(out, 2, ln)
+    coder.set_output(planes[1], nbits[1])                   # the last finished job's: packs again
+    coder.pack_bits(out, 2, ln)
+    p, L = pack_bitstreams(want_b, want_n, 2)
+    assert int(ln) == int(L) and torch.equal(out[:int(L)], p[:int(L)])
+    coder.decode_open()                                     # decoding: refused
+    with pytest.raises(LacError) as e:
+        coder.set_output(None, None)
+    assert e.value.code == LAC_E_STATE
+    coder.reset()
+    coder.set_output(None, None)
+    ref.close()
+    coder.close()

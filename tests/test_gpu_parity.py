@@ -110,6 +110,55 @@ def test_golden_small_cases(path):
             cd.close()
 
 
+STRAIGHT_FIX = load_golden("straight_cases.json")
+
+
+def _storages(rows):
+    """The fixture's rows in u32 (where they fit) and u64 storage: the reference's output
+    does not depend on it, and each storage reaches other straight encode forms."""
+    out = [rows.astype(np.uint64)]
+    if rows.dtype == np.uint32:
+        out.insert(0, rows)
+    return out
+
+
+@pytest.mark.parametrize("case", load_golden("gen_cases.json") + STRAIGHT_FIX, ids=lambda c: c["name"])
+def test_golden_untraced_straight(case):
+    """Untraced split-path encodes -- the only ones that take k_encode's straight 64-step
+    blocks (lac_encode.hip; a trace buffer sends every block to the general loop) -- of
+    the reference-run fixtures, in u32 and u64 storage, and the untraced fused job: bytes
+    and bit counts equal the reference's.  tests/straight_forms.py predicts which form
+    each block takes; test_oracle_golden.py checks that these fixtures reach all of them
+    (u32; u64 t32 / t32+ft / wide / wide+ft and both fudge exits)."""
+    from straight_forms import forms_reached
+    rows = np.stack([synth.pmf_row(case["seed"], t, 0, case["V"], case["kind"], case["exp_range"])
+                     for t in range(case["steps"])])
+    sym = np.asarray(case["syms"], dtype=np.int32)[:, None]
+    for r in _storages(rows):
+        for path, job in (("split", False), ("split", True), ("fused", True)):
+            c, dpmf, data, n, _ = _gpu_encode(r[:, None, :], sym, case["prec"], path=path, job=job)
+            assert int(n[0]) == case["L"] and data[0].hex() == case["bytes"], (r.dtype, path, job,
+                                                                                forms_reached(r, case["syms"], case["prec"], r.dtype.itemsize * 8))
+            c.close()
+
+
+def test_golden_small_cases_untraced_straight():
+    """The 500 small reference cases, untraced on the split path, u32 and u64 storage
+    (the u32 form and the u64 t32 / t32+ft forms with the fudge exit, tests/straight_forms.py)."""
+    for kind in ("static", "perstep"):
+        for c in load_golden("small_cases.json")[kind]:
+            if not c["syms"]:
+                continue
+            T = len(c["syms"])
+            rows = np.array(c["rows"], dtype=np.uint32)
+            rows = rows if rows.shape[0] == T else np.repeat(rows[:1], T, axis=0)
+            for r in _storages(rows):
+                cd, dpmf, data, n, _ = _gpu_encode(r[:, None, :], np.array(c["syms"])[:, None], c["prec"],
+                                                   path="split")
+                assert int(n[0]) == c["L"] and data[0].hex() == c["bytes"], (r.dtype, c)
+                cd.close()
+
+
 def test_kat1_identity_static_model():
     """KAT-1 on the GPU: uniform-256 static table (stride 0), prec 48, 1 MiB -> identity."""
     kat = load_golden("kat.json")["kat1"]

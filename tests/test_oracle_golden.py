@@ -14,6 +14,7 @@ from oracle import oracle as coracle
 from oracle import restate
 
 SMALL = load_golden("small_cases.json")
+STRAIGHT = load_golden("straight_cases.json")     # round 6: cases for the straight encode forms
 GEN = load_golden("gen_cases.json")
 MISC = load_golden("misc.json")
 
@@ -52,7 +53,7 @@ def test_c_oracle_small(kind):
         assert coracle.decode(c["rows"], data, L, len(c["syms"]), c["prec"]) == c["syms"]
 
 
-@pytest.mark.parametrize("case", GEN, ids=[c["name"] for c in GEN])
+@pytest.mark.parametrize("case", GEN + STRAIGHT, ids=[c["name"] for c in GEN + STRAIGHT])
 def test_c_oracle_gen(case):
     rows = _gen_rows(case)
     syms = [synth.sample_symbol(r, case["seed"], t, 0) for t, r in enumerate(rows)]
@@ -63,7 +64,7 @@ def test_c_oracle_gen(case):
     assert coracle.decode(np.stack(rows), data, L, len(syms), case["prec"]) == syms
 
 
-@pytest.mark.parametrize("case", [c for c in GEN if c["V"] <= 1000], ids=lambda c: c["name"])
+@pytest.mark.parametrize("case", [c for c in GEN + STRAIGHT if c["V"] <= 1000], ids=lambda c: c["name"])
 def test_python_restatement_gen(case):
     rows = [[int(x) for x in r] for r in _gen_rows(case)]
     data, L = restate.encode_bytes(rows, case["syms"], case["prec"])
@@ -203,3 +204,23 @@ def test_c_bitserial_decoder_counts_match_reference():
         rows = np.stack(_gen_rows(c))
         got = coracle.decode_bitserial(rows, bytes.fromhex(c["bytes"]), c["L"], c["prec"])
         assert len(got) == c["decoded_count"] and got[:len(c["syms"])] == c["syms"], c["name"]
+
+
+def test_fixtures_reach_every_straight_encode_form():
+    """The reference-run fixtures, coded untraced on the split path in u32 and u64 storage
+    (tests/test_gpu_parity.py test_golden_untraced_straight), reach every straight 64-step
+    form of k_encode, and the fudge exit of both u64 forms that have one."""
+    from straight_forms import forms_reached
+    seen = {}
+    for c in GEN + STRAIGHT:
+        rows = _gen_rows(c)
+        for bits in ((32, 64) if rows[0].dtype == np.uint32 else (64,)):
+            for f in forms_reached(rows, c["syms"], c["prec"], bits):
+                seen.setdefault(f, c["name"])
+    for kind in ("static", "perstep"):
+        for c in SMALL[kind]:
+            for bits in (32, 64):
+                for f in forms_reached(c["rows"], c["syms"], c["prec"], bits):
+                    seen.setdefault(f, f"small {kind}")
+    want = {"u32", "t32", "t32+ft", "t32+ft+exit", "wide", "wide+ft", "wide+ft+exit"}
+    assert want <= set(seen), (sorted(seen.items()), want - set(seen))

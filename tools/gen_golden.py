@@ -131,6 +131,20 @@ GEN_CASES = [
 ]
 
 
+# Round 6: cases that reach each straight 64-step form of the split-path encoder
+# (lac_encode.hip k_encode) when coded untraced -- u32 tables with every total below both
+# 2^32 and 2^(prec-1) (the u32 form), and 32-bit totals above 2^(prec-1) (the u64 kernel's
+# T32 + FT form once stored as u64: every row can fudge at prec 21, some at prec 31) --
+# with full 64-step blocks and a part-filled last one.
+STRAIGHT_CASES = [
+    ("u32s_lu1000_p48", 31, "loguniform", 16, 1000, 150, 48, True, True),
+    ("u32s_lu32000_p40", 32, "loguniform", 11, 32000, 70, 40, True, False),
+    ("t32ft_lu1000_p21", 33, "loguniform", 16, 1000, 140, 21, True, True),
+    ("t32ft_lu1000_p31", 34, "loguniform", 18, 1000, 140, 31, True, True),
+    ("t32ft_flat300_p10", 35, "flat", 24, 300, 130, 10, True, True),
+]
+
+
 def gen_case(name, seed, kind, er, V, steps, prec, trace, decode):
     rows = [synth.pmf_row(seed, t, 0, V, kind, er or 24) for t in range(steps)]
     syms = [synth.sample_symbol(r, seed, t, 0) for t, r in enumerate(rows)]
@@ -293,9 +307,13 @@ def errors():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--kat", action="store_true", help="also run the 1 MiB KATs (~2 min)")
-    ap.add_argument("--only", choices=["acsampler_cb"], help="write just this fixture file")
+    ap.add_argument("--only", choices=["acsampler_cb", "straight"], help="write just this fixture file")
     a = ap.parse_args()
     os.makedirs(GOLDEN, exist_ok=True)
+    if a.only == "straight":
+        with open(os.path.join(GOLDEN, "straight_cases.json"), "w") as f:
+            json.dump([gen_case(*c) for c in STRAIGHT_CASES], f, separators=(",", ":"))
+        return
     if a.only == "acsampler_cb":
         with open(os.path.join(GOLDEN, "acsampler_cb.json"), "w") as f:
             json.dump(acsampler_callbacks(), f, separators=(",", ":"))
