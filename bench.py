@@ -426,6 +426,7 @@ def main():
         }
         print(json.dumps(line), flush=True)
     if gatherer:
+        coder.reset()                                      # (decoding: back to an encoder between jobs)
         gatherer.close()
     coder.close()
     if dist:

@@ -65,7 +65,10 @@ enum {
     LAC_E_HIP = -8,
     LAC_E_STATE = -9,
     LAC_E_FLUSH_ZERO_WIDTH = -10,
-    LAC_E_FLUSH_LOOP = -11
+    LAC_E_FLUSH_LOOP = -11,
+    LAC_E_UNDETERMINED = -12      /* not a failure: with LAC_OPT_DECODE_STOP a stream stopped before
+                                     the first symbol its bits do not determine, registers and
+                                     counters as they were before that symbol (lac_decode_get_state) */
 };
 
 enum {                       /* lac_set_option */
@@ -103,8 +106,14 @@ enum {                       /* lac_set_option */
     LAC_OPT_DECODE_FINE = 7,       /* one-wave decode (FUSED path): 1 = one total per 64 vectors of
                                       the row, so only 1 KB is re-read after the search (default,
                                       rows <= 131072 u32 / 65536 u64 entries); 0 = <= 64 chunk totals */
-    LAC_OPT_BLOCK_WAVES = 8        /* BLOCK decode path: waves per stream (4, 8, 16; 0 = by stream
+    LAC_OPT_BLOCK_WAVES = 8,       /* BLOCK decode path: waves per stream (4, 8, 16; 0 = by stream
                                       count, the default) */
+    LAC_OPT_DECODE_STOP = 9        /* 1: a decoding stream stops before the first symbol its bits do
+                                      not determine (decide_symbol's ls != hs, arith_code.py:268-273)
+                                      with LAC_E_UNDETERMINED, registers unchanged, instead of decoding
+                                      on over zero padding; decodes then take the STATS path.  0 =
+                                      off (default).  For decoders that stop where the reference's
+                                      run(bits, stop=0) stops (lac_amd.coder.A_from_bin) */
 };
 enum {
     LAC_MAP_CEIL = 0,              /* CDFPredictor.symbol_to_range + fudged_dist (arith_code.py:83-110) */

@@ -25,6 +25,7 @@ LAC_E_HIP = -8
 LAC_E_STATE = -9
 LAC_E_FLUSH_ZERO_WIDTH = -10
 LAC_E_FLUSH_LOOP = -11
+LAC_E_UNDETERMINED = -12
 
 STATUS_NAMES = {
     LAC_OK: "LAC_OK", LAC_E_ARG: "LAC_E_ARG", LAC_E_PREC: "LAC_E_PREC",
@@ -32,6 +33,7 @@ STATUS_NAMES = {
     LAC_E_TABLE: "LAC_E_TABLE", LAC_E_DECODE_RANGE: "LAC_E_DECODE_RANGE",
     LAC_E_CAPACITY: "LAC_E_CAPACITY", LAC_E_HIP: "LAC_E_HIP", LAC_E_STATE: "LAC_E_STATE",
     LAC_E_FLUSH_ZERO_WIDTH: "LAC_E_FLUSH_ZERO_WIDTH", LAC_E_FLUSH_LOOP: "LAC_E_FLUSH_LOOP",
+    LAC_E_UNDETERMINED: "LAC_E_UNDETERMINED",
 }
 
 # (name, restype, argtypes) for every symbol include/lac.h declares
@@ -98,6 +100,7 @@ LAC_OPT_DECODE_PATH = 5
 LAC_OPT_Q1_SHAPE = 6
 LAC_OPT_DECODE_FINE = 7
 LAC_OPT_BLOCK_WAVES = 8
+LAC_OPT_DECODE_STOP = 9
 LAC_MAP_CEIL, LAC_MAP_FLOOR = 0, 1
 LAC_TERM_FLUSH, LAC_TERM_ACSAMPLER = 0, 1
 LAC_TAIL_DECIDE, LAC_TAIL_FLUSH = 0, 1

@@ -181,6 +181,13 @@ class BatchCoder:
         check(self.lib.lac_set_option(self.ctx, _lib.LAC_OPT_DECODE_PATH, v))
         check(self.lib.lac_set_option(self.ctx, _lib.LAC_OPT_DECODE_FINE, 0 if path == "fused_chunk" else 1))
 
+    def set_decode_stop(self, on: bool):
+        """Stop each stream before the first symbol its bits do not determine (include/lac.h
+        LAC_OPT_DECODE_STOP): its status becomes LAC_E_UNDETERMINED with the registers
+        as they were before that symbol, where A_from_bin.run(bits, stop=0) stops
+        (arith_code.py:268-299); decodes then take the stats path."""
+        check(self.lib.lac_set_option(self.ctx, _lib.LAC_OPT_DECODE_STOP, 1 if on else 0))
+
     def set_block_waves(self, n: int):
         """Waves per stream of the 'block' decode path: 4, 8, 16 (0 = by stream count)."""
         check(self.lib.lac_set_option(self.ctx, _lib.LAC_OPT_BLOCK_WAVES, int(n)))

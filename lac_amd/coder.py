@@ -698,6 +698,27 @@ _TAIL_STATE = np.dtype([("l", "<i8"), ("h", "<i8"), ("lb", "<i8"), ("hb", "<i8")
                         ("done", "<i4"), ("still", "<i8"), ("nsym", "<i8")])                     # lac_tail_state
 
 
+def _bit_list(bits):
+    """A bit sequence (any iterable of 0 / 1, as the reference's run takes) -> (list of
+    ints, its bytes packed MSB first: group_bits' format).  Lists and tuples of ints go
+    through bytes() and numpy (~1 ms per 10^5 bits, against ~25 ms for the per-element
+    int() and range checks they take otherwise)."""
+    if isinstance(bits, (list, tuple)):
+        try:
+            raw = bytes(bits)
+        except (TypeError, ValueError):
+            raw = None
+        if raw is not None:
+            a = np.frombuffer(raw, dtype=np.uint8)
+            if a.size and int(a.max()) > 1:
+                raise ValueError("bits are 0 or 1")
+            return list(raw), np.packbits(a).tobytes()
+    bl = [int(b) for b in bits]
+    if any(b not in (0, 1) for b in bl):
+        raise ValueError("bits are 0 or 1")
+    return bl, np.packbits(np.asarray(bl, dtype=np.uint8)).tobytes()
+
+
 def _raise_decoder(code, sym=None):
     """The reference's exception for a decoder status (include/lac.h)."""
     if code == _lib.LAC_E_SYMBOL_RANGE:
@@ -787,7 +808,7 @@ class _Session:
 
     def load_bits(self, bl, data):
         """Take a whole bit list at once (the fast path): the same buffers add_bit builds."""
-        self.bits = list(bl)
+        self.bits = bl if isinstance(bl, list) else list(bl)
         self.buf = np.zeros(max(64, ((len(bl) >> 3) + 8) * 2 + 7 & ~7), dtype=np.uint8)   # rows 8-byte aligned
         self.buf[:len(data)] = np.frombuffer(data, dtype=np.uint8)
         self.dev = None
@@ -937,14 +958,12 @@ class A_from_bin:
             for b in bits:
                 yield from self.step(b)
         else:
-            bl = [int(b) for b in bits]
-            if any(b not in (0, 1) for b in bl):
-                raise ValueError("bits are 0 or 1")
-            yield from self._fast(bl, max_symbols)
+            bl, data = _bit_list(bits)
+            yield from self._fast(bl, max_symbols, data)
         if stop:
             yield from self.flush()
 
-    def _fast(self, bl, max_symbols):
+    def _fast(self, bl, max_symbols, data=None):
         """Determined symbols of a whole bit list: value-form decode per symbol;
         the registers before a symbol the bits do not determine (or that fails)
         are restored and parked as this decoder's session."""
@@ -954,7 +973,8 @@ class A_from_bin:
                 sess.add_bit(b)
                 yield from sess.decide()
             return
-        data = np.packbits(np.asarray(bl, dtype=np.uint8)).tobytes()     # group_bits' format
+        if data is None:
+            data = np.packbits(np.asarray(bl, dtype=np.uint8)).tobytes()     # group_bits' format
         sess.load_bits(bl, data)
         tab = sess.tab
         if tab.static:
@@ -979,10 +999,11 @@ class A_from_bin:
 
     def _fast_static(self, sess, max_symbols):
         """Determined symbols of a static model in a few launches: chunks of
-        stride-0 steps (doubling) until one holds a symbol the bits do not
-        determine (or whose window leaves [l, h]); that chunk is then replayed
-        from its first registers up to the last determined symbol, so the session
-        parks exactly where the per-symbol loop would."""
+        stride-0 steps (doubling) decoded with LAC_OPT_DECODE_STOP, so the stream
+        stops by itself before the first symbol the bits do not determine (or whose
+        window leaves [l, h]) with the registers of that point: the session parks
+        exactly where the per-symbol loop would, and nothing is decoded twice (round
+        5 replayed the last chunk up to that point: every symbol decoded twice)."""
         tab = sess.tab
         row = tab.row()
         V = len(row)
@@ -993,39 +1014,42 @@ class A_from_bin:
         check(c.lib.lac_decode_set_state(c.ctx, start.ctypes.data_as(C.c_void_p), c._stream))
         pmf = tab.row_dev(c.device).view(1, 1, V)
         # first chunk: the bits over the table's entropy (+10 %), what a stream drawn
-        # from the table holds; doubling covers the rest, a replay the overshoot
+        # from the table holds; doubling covers the rest, the stop the overshoot
         p = row[row > 0].astype(np.float64)
         p /= p.sum()
         H = float(-(p * np.log2(p)).sum())
         done, n = 0, int(min(1 << 20, 64 + 1.1 * len(sess.bits) / max(H, 1e-9)))
-        while done < max_symbols:
-            n = min(n, max_symbols - done)
-            out = c.decode(pmf.expand(n, 1, V))
-            new = np.zeros(1, dtype=_DEC_STATE)
-            check(c.lib.lac_decode_get_state(c.ctx, new.ctypes.data_as(C.c_void_p), c._stream))
-            got = int(new["ndet"][0]) - int(start["ndet"][0])
-            if int(new["err"][0]):
-                got = min(got, max(int(new["err_step"][0]) - int(start["nsym"][0]), 0))
-            if not int(new["err"][0]) and got == n:
-                syms = out[:, 0].cpu().tolist()
+        c.set_decode_stop(True)
+        try:
+            while done < max_symbols:
+                n = min(n, max_symbols - done)
+                out = c.decode(pmf.expand(n, 1, V))
+                new = np.zeros(1, dtype=_DEC_STATE)
+                check(c.lib.lac_decode_get_state(c.ctx, new.ctypes.data_as(C.c_void_p), c._stream))
+                err = int(new["err"][0])
+                # the stream stopped (undetermined) or failed at err_step with the registers of
+                # that point; every symbol before it is determined
+                got = (int(new["err_step"][0]) if err else int(new["nsym"][0])) - int(start["nsym"][0])
+                got = max(min(got, n), 0)
+                syms = out[:got, 0].cpu().tolist() if got else []
+                if err:
+                    new["err"] = 0
+                    new["err_step"] = -1
+                    new["nsym"] = start["nsym"][0] + got
+                    new["ndet"] = start["ndet"][0] + got
+                    new["det"] = 1
+                    check(c.lib.lac_decode_set_state(c.ctx, new.ctypes.data_as(C.c_void_p), c._stream))
                 start = new
-            else:
-                k = max(min(got, n), 0)
-                syms = []
-                if k:                                   # replay the determined part of the chunk
-                    check(c.lib.lac_decode_set_state(c.ctx, start.ctypes.data_as(C.c_void_p), c._stream))
-                    syms = c.decode(pmf.expand(k, 1, V))[:, 0].cpu().tolist()
-                    start = np.zeros(1, dtype=_DEC_STATE)
-                    check(c.lib.lac_decode_get_state(c.ctx, start.ctypes.data_as(C.c_void_p), c._stream))
-                n = 0
-            for s in syms:
-                tab.accept(s)
-                yield s
-            done += len(syms)
-            sess.st = start
-            if not n:
-                return
-            n *= 2
+                sess.st = start
+                for s in syms:
+                    tab.accept(s)
+                    yield s
+                done += got
+                if err or got < n:
+                    return
+                n *= 2
+        finally:
+            c.set_decode_stop(False)
 
     # ---- registers (arith_code.py:249-263): l, h and the received-bit interval [lb, hb]
     def _regs(self):

@@ -87,7 +87,7 @@ int lac_close(lac_ctx *c) {
     (void)hipFree(c->q1chunks);
     (void)hipFree(c->dmeta);
     (void)hipFree(c->dresume);
-    (void)hipFree(c->lvpre);
+    (void)hipFree(c->lcdf);
     (void)hipFree(c->lchunk);
     (void)hipFree(c->lmeta);
     (void)hipFree(c->dprogress);
@@ -116,6 +116,10 @@ int lac_set_option(lac_ctx *c, int option, int64_t value) {
     case LAC_OPT_BLOCK_WAVES:
         if (value != 0 && value != 4 && value != 8 && value != 16) return fail(LAC_E_ARG, "block waves: 0, 4, 8 or 16");
         c->block_waves = (int)value;
+        return LAC_OK;
+    case LAC_OPT_DECODE_STOP:
+        if (value != 0 && value != 1) return fail(LAC_E_ARG, "decode_stop must be 0 or 1");
+        c->dec_stop = (int)value;
         return LAC_OK;
     case LAC_OPT_DECODE_FINE:
         if (value != 0 && value != 1) return fail(LAC_E_ARG, "decode_fine must be 0 or 1");

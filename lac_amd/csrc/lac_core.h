@@ -218,6 +218,25 @@ __host__ __device__ inline uint64_t div_small_fix_mask(uint64_t q, uint64_t n, u
            sign_mask64(r - 2 * d);
 }
 
+// floor((n*m + add) / d) for a quotient of at most 2^50 with any d < 2^64, n < 2^64,
+// m <= 2^51, add < d (the lean decode step's ranges ceil(c*w/T) on u64 rows with totals
+// of 2^50 and more, prec <= 50 so w <= 2^50, where div_small's 64-bit remainder no longer
+// holds the error).  One double estimate, fma(n, m, add) * inv with inv the correctly
+// rounded 1/d: a few ulps of relative error, within 1/2 of the quotient, so its floor is
+// the quotient or one off either way; the 128-bit remainder N - q*d, in [-d, 2d), then
+// decides the correction by its sign and size, without branches.
+__host__ __device__ inline uint64_t div_mid_est(uint64_t n, uint64_t m, uint64_t add, double inv) {
+    const double e = __builtin_fma((double)n, (double)m, (double)add) * inv;
+    return (uint64_t)(e > 0.0 ? e : 0.0);
+}
+__host__ __device__ inline uint64_t div_mid_fix(uint64_t q, uint64_t n, uint64_t m, uint64_t add, uint64_t d) {
+    const u128 r = (u128)n * m + add - (u128)q * d;          // wrapping: [-d, 2d) as two's complement
+    const uint64_t rh = (uint64_t)(r >> 64), rl = (uint64_t)r;
+    const uint64_t neg = rh >> 63;
+    const uint64_t ge = (neg ^ 1) & ((uint64_t)(rh != 0) | (uint64_t)(rl >= d));
+    return q - neg + ge;
+}
+
 // CDFPredictor.fudged_dist test (arith_code.py:84): fudged iff T > w*minp.
 __host__ __device__ inline bool is_fudged(uint64_t T, uint64_t w, uint64_t minp) {
     return (u128)T > (u128)w * minp;

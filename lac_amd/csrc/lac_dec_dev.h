@@ -371,6 +371,15 @@ __device__ inline void div_small_u2(uint64_t n0, uint64_t n1, uint64_t m, uint64
     *q1 = div_small_fix_u<MASK>(e1, n1, m, add, d);
 }
 
+// div_mid (lac_core.h) with wave-uniform arguments, both of a pair's estimates first so
+// their FP64 chains overlap: the lean step's ranges on u64 rows with totals >= 2^50.
+__device__ inline void div_mid_u2(uint64_t n0, uint64_t n1, uint64_t m, uint64_t add, uint64_t d, double inv,
+                                  uint64_t *q0, uint64_t *q1) {
+    const uint64_t e0 = rfl_u64(div_mid_est(n0, m, add, inv)), e1 = rfl_u64(div_mid_est(n1, m, add, inv));
+    *q0 = div_mid_fix(e0, n0, m, add, d);
+    *q1 = div_mid_fix(e1, n1, m, add, d);
+}
+
 // Everything after the row's totals are known: val_to_symbol + symbol_to_range
 // + advance.  `find_chunk(tgt, &cv0, &G, &cb)` locates the chunk holding tgt.
 // UNI: the decoder state is wave-uniform (held in SGPRs by the caller), so the
@@ -379,7 +388,8 @@ __device__ inline void div_small_u2(uint64_t n0, uint64_t n1, uint64_t m, uint64
 template <typename E, int VEC, typename FindChunk, bool UNI = false, typename Clock = NoClock, typename Idle = NoIdle>
 __device__ inline int decode_symbol(DecState &st, const E *row, int64_t V, uint64_t T, uint64_t minp, int prec,
                                     int mapping, const uint8_t *bits, uint64_t nbits, FindChunk find_chunk,
-                                    int64_t *s_out, Clock *clk = nullptr, Idle idle = Idle()) {
+                                    int64_t *s_out, Clock *clk = nullptr, Idle idle = Idle(),
+                                    bool stop_undet = false) {
     auto mark = [&](int k) {
         if (clk) clk->mark(k);
     };
@@ -435,6 +445,9 @@ __device__ inline int decode_symbol(DecState &st, const E *row, int64_t V, uint6
         }
         det = vhi < bb;                                       // f_s > v_hi
     }
+    // LAC_OPT_DECODE_STOP: the stream stops before the first symbol its bits do not
+    // determine, registers unchanged (the drop-in decoder parks there, lac_amd.coder)
+    if (stop_undet && !det) return LAC_E_UNDETERMINED;
     if (st.det && det) st.ndet++;
     else st.det = 0;
     *s_out = s;

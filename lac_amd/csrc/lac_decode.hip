@@ -650,24 +650,32 @@ __device__ inline void dec_chunk_layout(int64_t V, int64_t *CI, int64_t *nch) {
     *nch = (nit + ci - 1) / ci;
 }
 
-// What k_decode_lean reads of a row whose total is below 2^32 (LEAN builds of k_dec_stats):
+// What k_decode_lean reads of a row (LEAN builds of k_dec_stats), besides its CDF:
 struct LeanMeta {
-    uint64_t T;            // the total; 0: not for the lean step (bad row, T >= 2^32, minp 0)
+    uint64_t T;            // the total; 0: not for the lean step (bad row, u32 total >= 2^32, minp 0)
     uint64_t fthr;         // ceil(T / minp): the ceil mapping's range is fudged iff w < fthr (arith_code.py:84)
     double iT;             // recip(T)
     uint64_t pad;
 };
+// Totals the lean step takes: below 2^32 for u32 tables (their CDF then fits the entries'
+// own width); any valid total (below 2^64) for u64 tables, whose steps divide with
+// div_small below 2^50 and with the 128-bit remainders of div_mid / div_floor_inv above.
+template <typename E> __device__ inline bool lean_total_ok(uint64_t T) {
+    return sizeof(E) == 8 || T < (1ull << 32);
+}
 
-// LEAN: also the row's vector-granular CDF for k_decode_lean -- vpre[row][v], the sum of
-// the row's entries before vector v (mod 2^32) -- its chunks' bounds lchunk[row][lane]
-// (exclusive | inclusive << 32) and a LeanMeta; exact where the total is below 2^32.
+// LEAN: also the row's per-entry CDF for k_decode_lean -- lcdf[row][i], the inclusive sum of
+// the row's entries up to i in the entries' own width (mod 2^32 / 2^64) -- its chunks'
+// exclusive bounds lchunk[row][lane] and a LeanMeta; exact where lean_total_ok.  (Round 6; rounds 4-5 wrote one CDF word per 16-B vector, and the step
+// then loaded the pmf vector and that word and summed the vector itself.)
 template <typename E, int VEC, bool LEAN = false>
 __global__ __launch_bounds__(256) void k_dec_stats(const E *__restrict__ pmf, int64_t step_stride,
                                                    int64_t stream_stride, int64_t B, int64_t rows, int64_t V,
                                                    int64_t t0, uint64_t *__restrict__ chunks,
-                                                   DecRowMeta *__restrict__ meta, uint32_t *__restrict__ vpre = nullptr,
+                                                   DecRowMeta *__restrict__ meta, E *__restrict__ lcdf = nullptr,
                                                    uint64_t *__restrict__ lchunk = nullptr,
                                                    LeanMeta *__restrict__ lmeta = nullptr) {
+    typedef typename VecT<E, VEC>::type Vt;
     const int lane = (int)lane_id();
     const int64_t r = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
     if (r >= rows) return;
@@ -682,22 +690,21 @@ __global__ __launch_bounds__(256) void k_dec_stats(const E *__restrict__ pmf, in
     // groups of 8 iterations (8 loads in flight per lane), their 8 totals from one
     // butterfly, each added into the lane of its chunk (chunk = iteration / CI)
     int64_t chunk = 0, left = CI;
-    uint32_t run = 0;                                          // LEAN: the row's sum so far, mod 2^32
-    uint32_t *vp = LEAN ? vpre + r * nvec : nullptr;
-    // LEAN: a group's vpre values are stored after the next group's loads are issued, so
-    // the in-order wait for those loads never waits on these stores (B=64: 3.41 -> 3.35 us
-    // per step; the pass stays ~1.5x the plain one, bound by its per-iteration scans)
-    uint32_t pv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    E run = 0;                                                 // LEAN: the row's sum so far
+    Vt *cp = LEAN ? reinterpret_cast<Vt *>(lcdf + r * V) : nullptr;
+    // LEAN: a group's CDF vectors are stored after the next group's loads are issued, so
+    // the in-order wait for those loads never waits on these stores
+    Vt pv[8];
     int64_t pg = -1;
     auto store_pending = [&]() {
 #pragma unroll
         for (int u = 0; u < 8; u++) {
             const int64_t vi = (pg * 8 + u) * 64 + lane;
-            if (vi < nvec) vp[vi] = pv[u];
+            if (vi < nvec) cp[vi] = pv[u];
         }
     };
     for (int64_t g = 0; g < ngrp; g++) {
-        typename VecT<E, VEC>::type x[8];
+        Vt x[8];
 #pragma unroll
         for (int u = 0; u < 8; u++) x[u] = load_vec_or0<E, VEC>(row, (g * 8 + u) * 64 + lane, nvec);
         if constexpr (LEAN) {
@@ -717,12 +724,26 @@ __global__ __launch_bounds__(256) void k_dec_stats(const E *__restrict__ pmf, in
             }
             s8[u] = a;
         }
-        if constexpr (LEAN) {
+        if constexpr (LEAN && VEC > 1) {
 #pragma unroll
             for (int u = 0; u < 8; u++) {
-                const uint32_t in = wave_incl_scan_u32((uint32_t)s8[u]);
-                pv[u] = run + in - (uint32_t)s8[u];
-                run += (uint32_t)__builtin_amdgcn_readlane((int)in, 63);
+                E in, tot;
+                if constexpr (W) {
+                    in = wave_incl_scan_u64(s8[u]);
+                    tot = readlane_u64(in, 63);
+                } else {
+                    in = wave_incl_scan_u32((uint32_t)s8[u]);
+                    tot = (uint32_t)__builtin_amdgcn_readlane((int)in, 63);
+                }
+                E c = run + in - (E)s8[u];                     // the row's sum before this lane's entries
+                Vt cv;
+#pragma unroll
+                for (int j = 0; j < VEC; j++) {
+                    c += vget<E, VEC>(x[u], j);
+                    cv[j] = c;
+                }
+                pv[u] = cv;
+                run += tot;
             }
             pg = g;
         }
@@ -746,12 +767,15 @@ __global__ __launch_bounds__(256) void k_dec_stats(const E *__restrict__ pmf, in
     chunks[r * 64 + lane] = mine;
     if (lane == 0) meta[r] = DecRowMeta{bad ? 0 : (uint64_t)acc128, minp};
     if constexpr (LEAN) {
-        const uint32_t in = wave_incl_scan_u32((uint32_t)mine);
-        lchunk[r * 64 + lane] = (uint64_t)(in - (uint32_t)mine) | ((uint64_t)in << 32);
+        const uint64_t in = wave_incl_scan_u64(mine);
+        lchunk[r * 64 + lane] = in - mine;                     // chunk lane's exclusive bound
         const uint64_t T = (uint64_t)acc128;
-        const bool ok = !bad && T < (1ull << 32) && minp != 0;
+        const bool ok = !bad && lean_total_ok<E>(T) && minp != 0;
+        // u64 rows: 1/T correctly rounded (an IEEE divide, once per row), which div_mid's
+        // one-estimate bound needs; u32 rows: the device reciprocal, as div_small's
         if (lane == 0)
-            lmeta[r] = LeanMeta{ok ? T : 0, ok ? (T + minp - 1) / minp : 0, recip(ok ? T : 1), 0};
+            lmeta[r] = LeanMeta{ok ? T : 0, ok ? (T + minp - 1) / minp : 0,
+                                W ? 1.0 / (double)(ok ? T : 1) : recip(ok ? T : 1), 0};
     }
 }
 
@@ -764,8 +788,11 @@ __global__ __launch_bounds__(256) void k_decode_seq(const E *__restrict__ pmf, i
                                             const DecRowMeta *__restrict__ meta, DecState *states,
                                             const uint8_t *bits, uint64_t stride, const uint64_t *nbits,
                                             int32_t *sym_out, int64_t B, int mapping,
-                                            const int64_t *__restrict__ resume = nullptr) {
+                                            const int64_t *__restrict__ resume = nullptr, int64_t rstep = -1,
+                                            int stop_undet = 0) {
     const int lane = (int)lane_id();
+    // rows of statistics per step: B, or 0 for a static model (stride-0 steps: one row per stream)
+    if (rstep < 0) rstep = B;
     // the stream index and its decoder state wave-uniform (SGPRs): the serial chain --
     // the targets, the ranges, the renormalisation -- then runs on the scalar unit
     // (decode_symbol<..., true>), with uniform branches instead of exec-masked ones
@@ -780,8 +807,8 @@ __global__ __launch_bounds__(256) void k_decode_seq(const E *__restrict__ pmf, i
     // after k_decode_lean: its steps are done, continue from the first it left
     const int64_t i0 = resume ? (int64_t)rfl_u64((uint64_t)(resume[b] - t0)) : 0;
     if (i0 >= nsteps) return;
-    uint64_t next = chunks[(i0 * B + b) * 64 + lane];
-    DecRowMeta nmeta = meta[i0 * B + b];
+    uint64_t next = chunks[(i0 * rstep + b) * 64 + lane];
+    DecRowMeta nmeta = meta[i0 * rstep + b];
 #if LAC_DEC_PHASES
     PhaseClock clock, *clk = &clock;
     clock.start();
@@ -794,13 +821,13 @@ __global__ __launch_bounds__(256) void k_decode_seq(const E *__restrict__ pmf, i
         const uint64_t mine = next;
         const DecRowMeta rm = nmeta;
         if (i + 1 < nsteps) {                                  // prefetch: independent of the state
-            next = chunks[((i + 1) * B + b) * 64 + lane];
-            nmeta = meta[(i + 1) * B + b];
+            next = chunks[((i + 1) * rstep + b) * 64 + lane];
+            nmeta = meta[(i + 1) * rstep + b];
         }
         int32_t *out = sym_out + t * B + b;
-        if (st.err) {
-            if (lane == 0) *out = -1;
-            continue;
+        if (st.err) {                                          // failed or stopped: -1 for the rest, 64 at once
+            for (int64_t j = i + lane; j < nsteps; j += 64) sym_out[(t0 + j) * B + b] = -1;
+            break;
         }
         const E *row = pmf + t * step_stride + b * stream_stride;
         int err = rm.T ? 0 : LAC_E_TABLE;
@@ -820,7 +847,8 @@ __global__ __launch_bounds__(256) void k_decode_seq(const E *__restrict__ pmf, i
             };
             if (clk) clk->mark(0);
             err = decode_symbol<E, VEC, decltype(find_chunk), true>(st, row, V, rfl_u64(rm.T), rfl_u64(rm.minp), prec,
-                                                                   mapping, mybits, mynbits, find_chunk, &s, clk);
+                                                                   mapping, mybits, mynbits, find_chunk, &s, clk,
+                                                                   NoIdle(), stop_undet != 0);
         }
         if (err) {
             st.err = err;
@@ -837,31 +865,36 @@ __global__ __launch_bounds__(256) void k_decode_seq(const E *__restrict__ pmf, i
 #endif
 }
 
-// ---- lean few-stream decode step (stats path, prec <= 50, row totals < 2^32)
-// k_decode_seq's serial step for what few-stream decodes nearly always are -- u32-scale
-// rows (totals below 2^32), an unfudged range (or the floor mapping), prec <= 50 -- laid
-// out for the latency of one wave, whose instructions issue in order.  Everything that
-// depends on the row alone comes precomputed from k_dec_stats<..., LEAN>: the chunk
-// bounds, T's reciprocal, the fudge threshold ceil(T/minp) and the vector-granular CDF
-// vpre, loaded two steps ahead.  Left on the chain: a ballot over the chunk bounds,
-// compared with the target floor(v*T/w) as products (ex*w <= v*T < in*w, no division),
-// one round of loads (the chunk's entries and their vpre) with the target's division
-// in its shadow, the iteration holding the target by its first vpre, a ballot over the
-// lanes' cumulative sums -- no wave scan -- the two ranges and the renormalisation.  Symbols
+// ---- lean few-stream decode step (stats path, prec <= 50)
+// k_decode_seq's serial step for what few-stream decodes nearly always are -- u32 tables
+// with totals below 2^32 and u64 tables of any valid total (llama-scale tables near 2^60,
+// the drop-in surface's static tables), an unfudged range (or the floor mapping), prec
+// <= 50 -- laid out for the latency of one wave, whose instructions issue in order.
+// Everything that depends on the row alone comes precomputed from k_dec_stats<..., LEAN>:
+// the row's per-entry CDF, the chunks' exclusive bounds, T's reciprocal and the fudge
+// threshold ceil(T/minp), the bounds and thresholds loaded two steps ahead.  Left on the
+// chain: a ballot over the chunk bounds compared with the target floor(v*T/w) as products
+// (ex*w <= v*T, no division: the chunk is the last one whose bound passes), one round of
+// loads of the chunk's CDF vectors (one 16-B vector per lane and iteration) with the
+// target's division in its shadow, the iteration by the CDF value just before it, a ballot
+// over the lanes' last entries, the two range divisions and the renormalisation.  Symbols
 // collect one per lane and leave in one store per 64 steps.
 // Results are k_decode_seq's.  A step outside the case (a bad, large or fudged row, an
-// inconsistent state or stream) ends this kernel for its stream before the step changes
-// anything: resume[b] holds the step and k_decode_seq continues from it, raising the
-// error if there is one.  One wave per workgroup: streams spread over the XCDs.
+// inconsistent state or stream) -- or, with LAC_OPT_DECODE_STOP, a symbol the bits do not
+// determine -- ends this kernel for its stream before the step changes anything:
+// resume[b] holds the step and k_decode_seq continues from it, raising the error (or
+// stopping) there.  One wave per workgroup: streams spread over the XCDs.
+// rstep: rows of statistics per step, B -- or 0 for a static model (stride-0 steps), whose
+// one row per stream every step reads (L2-resident after the first).
 // Few-stream lean decode: the re-read of step i's chunk is one dependent load per step,
 // an HBM round trip when the row is cold.  Helper waves -- workgroups of the same launch
 // placed on the decoding wave's XCD (workgroups are dealt to the 8 XCDs round-robin, so
-// index = stream mod 8) -- read one dword of every 128-B line of the rows (and vpre rows)
-// a few steps ahead of the decoder, which then finds its chunk in that XCD's L2.  They
-// only read: the values are discarded (an empty asm consumes them so the loads stay).
-// They pace themselves by the decoder's progress (a relaxed agent-scope counter it sets
-// every 8 steps), never the other way round: results do not depend on them, and a
-// helper that sees no progress for ~10 ms gives up, so the grid always drains.
+// index = stream mod 8) -- read one dword of every 128-B line of the CDF rows a few steps
+// ahead of the decoder, which then finds its chunk in that XCD's L2.  They only read: the
+// values are discarded (an empty asm consumes them so the loads stay).  They pace
+// themselves by the decoder's progress (a relaxed agent-scope counter it sets every 8
+// steps), never the other way round: results do not depend on them, and a helper that
+// sees no progress for ~10 ms gives up, so the grid always drains.
 #ifndef LAC_LEAN_AHEAD
 #define LAC_LEAN_AHEAD 16
 #endif
@@ -879,6 +912,16 @@ constexpr int kLeanHelpMaxStreams = 16;         // above: no helpers (L2: ~2.6 M
 #define LAC_LEAN_PUB 8
 #endif
 constexpr int kLeanPub = LAC_LEAN_PUB;          // the decoder publishes its progress every kLeanPub steps
+#ifndef LAC_LEAN_PROD64
+#define LAC_LEAN_PROD64 1        // k_decode_lean, u64 rows: the search by products, no target division
+#endif
+#ifndef LAC_LEAN_PROD32
+#define LAC_LEAN_PROD32 0        // the same for u32 rows (their division is short: in the loads' shadow)
+#endif
+#ifndef LAC_LEAN_BYTES
+#define LAC_LEAN_BYTES (256ll << 20)
+#endif
+constexpr int64_t kLeanBytes = LAC_LEAN_BYTES;  // CDF rows per launch: at most this many bytes
 
 __device__ inline int32_t lean_progress(const int32_t *p) {
     return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -901,8 +944,7 @@ __device__ inline void lean_touch(const uint8_t *base, int64_t bytes) {
 }
 
 template <typename E>
-__device__ void lean_helper(const E *pmf, int64_t step_stride, int64_t stream_stride, int64_t t0, int32_t n32,
-                            int64_t V, const uint32_t *vpre, int32_t nv32, int64_t B, int64_t B8,
+__device__ void lean_helper(const E *lcdf, int64_t rstep, int32_t n32, int64_t V, int64_t B, int64_t B8,
                             const int32_t *progress) {
     const int64_t hidx = (int64_t)blockIdx.x - B8;
     const int64_t b = hidx % B8, k = hidx / B8;                 // stream (same XCD: B8 % 8 == 0), helper
@@ -916,29 +958,40 @@ __device__ void lean_helper(const E *pmf, int64_t step_stride, int64_t stream_st
             if (++idle > (1 << 17)) return;                      // ~10 ms without progress
             __builtin_amdgcn_s_sleep(2);
         }
-        lean_touch(reinterpret_cast<const uint8_t *>(pmf + (t0 + t) * step_stride + b * stream_stride),
-                   V * (int64_t)sizeof(E));
-        lean_touch(reinterpret_cast<const uint8_t *>(vpre + ((int64_t)t * B + b) * nv32), (int64_t)nv32 * 4);
+        lean_touch(reinterpret_cast<const uint8_t *>(lcdf + ((int64_t)t * rstep + b) * V), V * (int64_t)sizeof(E));
+    }
+}
+
+// e * w <= P (P = v * T as hi:lo): the chunk test of the lean step, lane-parallel.  u32 tables:
+// e < 2^32, w < 2^51, the products split at bit 32 (below 2^83); u64 tables: e < 2^50, full
+// 128-bit products (below 2^101).
+template <typename E>
+__device__ inline bool lean_le(uint64_t e, uint64_t wl, uint64_t wh, uint64_t w, uint64_t ph, uint64_t pl) {
+    if constexpr (sizeof(E) == 4) {
+        const uint64_t q0 = (e & 0xffffffffull) * wl, qh = (e & 0xffffffffull) * wh + (q0 >> 32);
+        return (qh < ph) | ((qh == ph) & ((uint32_t)q0 <= (uint32_t)pl));
+    } else {
+        const u128 q = (u128)e * w;
+        const uint64_t qh = (uint64_t)(q >> 64), ql = (uint64_t)q;
+        return (qh < ph) | ((qh == ph) & (ql <= pl));
     }
 }
 
 template <typename E, int VEC, int CIM>
-__global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ pmf, int64_t step_stride,
-                                                    int64_t stream_stride, int64_t t0, int64_t nsteps, int64_t V,
-                                                    int prec, const uint32_t *__restrict__ vpre,
+__global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, int64_t rstep, int64_t t0,
+                                                    int64_t nsteps, int64_t V, int prec,
                                                     const uint64_t *__restrict__ lchunk,
                                                     const LeanMeta *__restrict__ lmeta, DecState *states,
                                                     const uint8_t *__restrict__ bits, uint64_t stride,
-                                                    const uint64_t *__restrict__ nbits,
-                                                    int32_t *sym_out, int64_t B, int mapping,
-                                                    int64_t *__restrict__ resume, int32_t *progress) {
+                                                    const uint64_t *__restrict__ nbits, int32_t *sym_out, int64_t B,
+                                                    int mapping, int stop_undet, int64_t *__restrict__ resume,
+                                                    int32_t *progress) {
     typedef typename VecT<E, VEC>::type Vt;
+    constexpr bool W = sizeof(E) == 8;
     const int lane = (int)lane_id();
     const int64_t B8 = (B + 7) & ~(int64_t)7;
     if ((int64_t)blockIdx.x >= B8) {                             // a helper workgroup
-        if (progress)
-            lean_helper<E>(pmf, step_stride, stream_stride, t0, (int32_t)nsteps, V, vpre, (int32_t)(V / VEC), B, B8,
-                           progress);
+        if (progress) lean_helper<E>(lcdf, rstep, (int32_t)nsteps, V, B, B8, progress);
         return;
     }
     const int64_t b = blockIdx.x;
@@ -953,19 +1006,25 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ pmf, i
     const uint32_t ci64 = (uint32_t)CI * 64;
     const int32_t nch32 = (int32_t)nch;
     const bool ceil_map = mapping != LAC_MAP_FLOOR;
-    const int32_t n32 = (int32_t)nsteps;                        // (<= chunk_steps)
-    // row data two steps ahead: the lane's chunk bounds (per-lane pointer) and the LeanMeta
-    // (by index, a scalar load); running pointers to row i and its vpre
-    uint64_t cw = 0, cw1 = 0;
-    LeanMeta lm{0, 0, 1.0, 0}, lm1{0, 0, 1.0, 0};
-    if (n32 > 0) { cw = lchunk[b * 64 + lane]; lm = lmeta[b]; }
-    if (n32 > 1) { cw1 = lchunk[(B + b) * 64 + lane]; lm1 = lmeta[B + b]; }
-    const uint64_t *lcv = lchunk + (2 * B + b) * 64 + lane;
-    int32_t li = (int32_t)(2 * B + b);
-    const int32_t B32 = (int32_t)B;
-    const E *rowp = pmf + t0 * step_stride + b * stream_stride;
-    const uint32_t *prp = vpre + b * (int64_t)nv32;
-    const int64_t pr_step = B * (int64_t)nv32;
+    const int32_t n32 = (int32_t)nsteps;                        // (<= the launch's steps)
+    // row data two steps ahead: the lane's chunk bound (per-lane pointer) and the LeanMeta
+    // (by index, a scalar load) in two register sets A / B that the 2x unrolled loop uses in
+    // turn, so a prefetched value is first touched two steps after its load was issued (a
+    // single set rotated by copies waited at the next step for a load issued one step
+    // earlier); a static model (rstep 0) loads its one row's once.  A running pointer to row
+    // i's CDF.
+    // The LeanMeta arrives by a vector load (lane k: word k & 3), read out with readlanes:
+    // a scalar load's wait (lgkmcnt, out of order) waits for every scalar load in flight,
+    // so a row's meta two steps ahead was waited for one step after its load.
+    const bool moving = rstep != 0;
+    const uint64_t *lmw = reinterpret_cast<const uint64_t *>(lmeta) + (lane & 3);
+    uint64_t cwA = 0, cwB = 0, lmA = 0, lmB = 0;
+    if (n32 > 0) { cwA = lchunk[b * 64 + lane]; lmA = lmw[b * 4]; }
+    if (n32 > 1) { cwB = lchunk[(rstep + b) * 64 + lane]; lmB = lmw[(rstep + b) * 4]; }
+    const uint64_t *lcv = lchunk + (2 * rstep + b) * 64 + lane;
+    int64_t li = 2 * rstep + b;
+    const Vt *rowp = reinterpret_cast<const Vt *>(lcdf + b * V);
+    const int64_t rv_step = rstep * (int64_t)nv32;               // vectors per step
     int32_t *outv = sym_out + (t0 + lane) * B + b;              // lane j: step 64k + j
     // the registers as locals (SGPRs); the counters are settled after the loop
     int64_t l = st.l, h = st.h, x = st.x;
@@ -979,136 +1038,171 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ pmf, i
 #else
     NoClock clk;
 #endif
+    // PROD: the search compares entries with the target floor(v*T/w) as products (c*w <=
+    // v*T), no division -- for u64 rows, whose target divides in 128 bits (div_floor_inv:
+    // longer than the chunk's loads); u32 rows divide (div_small_u) in the loads' shadow
+    constexpr bool PROD = W ? LAC_LEAN_PROD64 : LAC_LEAN_PROD32;
+    // one step with row data (cwi, lm); the next-but-one row's loads go into (pcw, plm) once
+    // this step's chunk loads are issued.  false: the stream leaves (not this step's case)
+    auto step = [&](const uint64_t cwi, const uint64_t lmv, uint64_t &pcw, uint64_t &plm) -> bool {
+        l = (int64_t)rfl_u64((uint64_t)l);                      // (the loop's phis are not seen as uniform)
+        h = (int64_t)rfl_u64((uint64_t)h);
+        x = (int64_t)rfl_u64((uint64_t)x);
+        pos = rfl_u64(pos);
+        const uint64_t T = readlane_u64(lmv, 0), fthr = readlane_u64(lmv, 1);   // LeanMeta {T, fthr, iT}
+        const double iT = __builtin_bit_cast(double, readlane_u64(lmv, 2));
+        const Vt *row = rowp;
+        rowp += rv_step;
+        const uint64_t w = (uint64_t)(h - l + 1), v = (uint64_t)(x - l);
+        clk.mark(0);
+        // the chunk holding tgt = floor(v*T/w) without the division: the last chunk whose
+        // exclusive bound ex passes ex <= tgt, i.e. ex*w <= v*T (ex nondecreasing over the
+        // chunks, and tgt < T, so that chunk's inclusive bound exceeds tgt)
+        uint64_t ph, pl;
+        if constexpr (W) {
+            const u128 P = (u128)v * T;
+            ph = rfl_u64((uint64_t)(P >> 64));
+            pl = rfl_u64((uint64_t)P);
+        } else {
+            const uint64_t p0 = (v & 0xffffffffull) * T;
+            ph = (v >> 32) * T + (p0 >> 32);
+            pl = (uint32_t)p0;
+        }
+        const uint32_t wl = (uint32_t)w;
+        const uint64_t wh = w >> 32;
+        auto le = [&](uint64_t e) { return lean_le<E>(e, wl, wh, w, ph, pl); };   // e <= tgt
+        const uint64_t cm = __ballot((lane < nch32) & le(cwi));
+        // the chunk's loads first (in bounds whatever the step: refused below if it is bad),
+        // then the stream window, then the next-but-one row's data, then everything that
+        // can wait for them
+        const uint32_t src = cm ? (uint32_t)(63 - __builtin_clzll((unsigned long long)cm)) : 0u;
+        const int32_t cv0 = (int32_t)(src * ci64);
+        Vt xs[CIM];
+#pragma unroll
+        for (int g = 0; g < CIM; g++) {
+            const int32_t vi = cv0 + g * 64 + lane, vc = vi < nv32 ? vi : nv32 - 1;
+            xs[g] = row[vc];
+        }
+        const BitWin win = bit_window(mybits, mynbits, pos);
+        if (moving) {                                           // row i+2 (the last row again past the end)
+            const bool more = i + 2 < n32;
+            pcw = *(more ? lcv : lcv - rstep * 64);
+            plm = lmw[(more ? li : li - rstep) * 4];
+            lcv += more ? rstep * 64 : 0;
+            li += more ? rstep : 0;
+        }
+        if (__builtin_expect(progress && (i & (kLeanPub - 1)) == 0, 0) && lane == 0)   // the helpers' pace
+            __hip_atomic_store(progress + b, i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // (after the loads)
+        // a step outside the lean case leaves at the end (a branch here would let the
+        // compiler sink the loads below it); until then its divisions run on safe values
+        // (the step's tests as sign bits of differences and ORs on the scalar unit, one
+        // exit test per step)
+        const uint64_t bad = (uint64_t)(T == 0) | ((uint64_t)(x - l) >> 63) | ((uint64_t)(h - x) >> 63) |
+                             ((uint64_t)ceil_map & ((w - fthr) >> 63)) | (uint64_t)(cm == 0);
+        const uint64_t Ts = bad ? 1 : T, ws = bad ? 1 : w, vs = bad ? 0 : v;
+        const uint64_t ex0 = W ? readlane_u64(cwi, (int)src) : (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cwi, (int)src);
+        // u64 rows with totals of 2^50 and more (llama-scale tables): div_mid's ranges
+        const bool small = !W || Ts < kSmallQuot;               // uniform
+        double iw = 0.0;
+        E te = 0;
+        if constexpr (!PROD) {
+            iw = recip(ws);
+            te = (E)div_small_u(vs, Ts, 0, ws, iw);           // < T
+        }
+        auto lte = [&](E c) { if constexpr (PROD) return le((uint64_t)c); else return c <= te; };   // c <= tgt
+        clk.mark(1);
+        const uint64_t past = pos > mynbits ? pos - mynbits : 0;
+        const int u = past < (uint64_t)prec ? (int)past : prec;
+        clk.mark(2);
+        // the iteration holding the target: the last whose CDF value just before it (the
+        // chunk's bound, else lane 63's last entry of the iteration before) is <= tgt
+        int gs = 0;
+        E exg = (E)ex0;
+#pragma unroll
+        for (int g = 1; g < CIM; g++) {
+            const E eg = W ? (E)readlane_u64((uint64_t)vget<E, VEC>(xs[g - 1], VEC - 1), 63)
+                           : (E)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)vget<E, VEC>(xs[g - 1], VEC - 1), 63);
+            const bool take = (cv0 + g * 64 < nv32) & lte(eg);
+            gs = take ? g : gs;
+            exg = take ? eg : exg;
+        }
+        Vt xg = xs[0];
+#pragma unroll
+        for (int g = 1; g < CIM; g++) xg = gs == g ? xs[g] : xg;
+        const bool real = cv0 + gs * 64 + lane < nv32;
+        const uint64_t m2 = __ballot(real & !lte(vget<E, VEC>(xg, VEC - 1)));
+        const int L = m2 ? __ffsll((unsigned long long)m2) - 1 : 0;
+        // lane L's entries: k of them <= tgt, then the symbol's; its lower bound is the
+        // entry before (lane L's, lane L-1's last, or the iteration's start value)
+        uint32_t k = 0;
+        E lo = 0, hi = vget<E, VEC>(xg, VEC - 1);
+#pragma unroll
+        for (int j = VEC - 1; j >= 0; j--) {
+            const E c = vget<E, VEC>(xg, j);
+            const bool cle = lte(c);
+            k += cle ? 1 : 0;
+            hi = cle ? hi : c;
+            lo = (cle && lo == 0) ? c : lo;                     // the last entry <= tgt (entries ascend)
+        }
+        const int Lp = L > 0 ? L - 1 : 0;
+        uint64_t lo_l, hi_c, prev;
+        if constexpr (W) {
+            lo_l = readlane_u64(lo, L);
+            hi_c = readlane_u64(hi, L);
+            prev = readlane_u64(vget<E, VEC>(xg, VEC - 1), Lp);
+        } else {
+            lo_l = (uint32_t)__builtin_amdgcn_readlane((int)lo, L);
+            hi_c = (uint32_t)__builtin_amdgcn_readlane((int)hi, L);
+            prev = (uint32_t)__builtin_amdgcn_readlane((int)vget<E, VEC>(xg, VEC - 1), Lp);
+        }
+        const uint32_t kL = (uint32_t)__builtin_amdgcn_readlane((int)k, L);
+        const uint64_t lo_c = kL ? lo_l : (L > 0 ? prev : (uint64_t)exg);
+        const int32_t sym = (cv0 + gs * 64 + L) * VEC + (int32_t)kL;
+        clk.mark(3);
+        uint64_t a, bb;
+        if (small) div_small_u2(lo_c, hi_c, ws, ceil_map ? Ts - 1 : 0, Ts, bad ? 1.0 : iT, &a, &bb);
+        else div_mid_u2(lo_c, hi_c, ws, ceil_map ? Ts - 1 : 0, Ts, bad ? 1.0 : iT, &a, &bb);
+        // (l + a <= x <= l + bb - 1: v in [a, bb))
+        if (bad | (uint64_t)(m2 == 0) | ((vs - a) >> 63) | (((vs - bb) >> 63) ^ 1)) return false;
+        clk.mark(4);
+        // the 1-padded end past the stream's end (u > 0; before it the step is determined):
+        // determined iff vhi < w and floor(vhi*T/w) < hi_c, i.e. vhi*T < hi_c*w
+        if (__builtin_expect(u != 0, 0)) {
+            const uint64_t vhi = vs + ((1ull << u) - 1);
+            const bool vhi_in = (vhi - ws) >> 63;                 // vhi < w
+            const u128 PH = (u128)vhi * Ts, HW = (u128)hi_c * ws;
+            if (!(vhi_in && PH < HW)) {                           // not determined
+                if (stop_undet) return false;                     // k_decode_seq stops the stream here
+                if (firstnd < 0) firstnd = i;
+            }
+        }
+        // narrow + renormalise (decode_advance<true>) without branches: kk = 0 keeps the
+        // registers, and window_bits_nb(.., 0) is 0
+        int64_t nl = l + (int64_t)a, nh = l + (int64_t)bb - 1;
+        const uint64_t d = (uint64_t)(nh - nl);
+        const int sh = bitlen64(d), kk0 = prec - sh, kk = kk0 > 0 ? kk0 : 0;   // (renorm: kk <= 0 is 0)
+        const uint64_t Ev = kk > 0 ? (uint64_t)nl >> sh : 0;
+        nl = (int64_t)(((uint64_t)nl - (Ev << (sh & 63))) << kk);
+        nh = nl + (int64_t)((d + 1) << kk) - 1;
+        const BitWin wu{rfl_u64(win.w0), rfl_u64(win.w1)};
+        x = (int64_t)((((uint64_t)x - (Ev << (sh & 63))) << kk) | window_bits_nb(wu, mynbits, pos, kk));
+        pos += (uint64_t)kk;
+        l = nl;
+        h = nh;
+        if (lane == (i & 63)) sbuf = sym;
+        if (__builtin_expect((i & 63) == 63, 0)) {
+            *outv = sbuf;
+            outv += B * 64;
+        }
+        clk.mark(5);
+        return true;
+    };
     if (!st.err) {
-        for (; i < n32; i++) {
-            l = (int64_t)rfl_u64((uint64_t)l);                  // (the loop's phis are not seen as uniform)
-            h = (int64_t)rfl_u64((uint64_t)h);
-            x = (int64_t)rfl_u64((uint64_t)x);
-            pos = rfl_u64(pos);
-            const uint64_t T = rfl_u64(lm.T), fthr = rfl_u64(lm.fthr);
-            const double iT = lm.iT;
-            const uint64_t cwi = cw;
-            cw = cw1;
-            lm = lm1;
-            {                                                   // row i+2 (the last row again past the end)
-                const bool more = i + 2 < n32;
-                cw1 = *(more ? lcv : lcv - (int64_t)B32 * 64);
-                lm1 = lmeta[more ? li : li - B32];
-            }
-            lcv += i + 2 < n32 ? (int64_t)B32 * 64 : 0;
-            li += i + 2 < n32 ? B32 : 0;
-            const E *row = rowp;
-            const uint32_t *pr = prp;
-            rowp += step_stride;
-            prp += pr_step;
-            const uint64_t w = (uint64_t)(h - l + 1), v = (uint64_t)(x - l);
-            clk.mark(0);
-            // the chunk holding tgt = floor(v*T/w) without the division: ex <= tgt < in
-            // iff ex*w <= v*T < in*w, products below 2^83 as (bits 32.., bits 0..31)
-            const uint64_t pl = (v & 0xffffffffull) * T, ph = (v >> 32) * T + (pl >> 32);
-            const uint32_t plo = (uint32_t)pl;
-            const uint32_t wl = (uint32_t)w, wh = (uint32_t)(w >> 32);
-            auto le_p = [&](uint32_t e) {                       // e*w <= v*T (no short circuits: no branches)
-                const uint64_t q0 = (uint64_t)e * wl, qh = (uint64_t)e * wh + (q0 >> 32);
-                return (qh < ph) | ((qh == ph) & ((uint32_t)q0 <= plo));
-            };
-            const uint64_t cm = __ballot((lane < nch32) & le_p((uint32_t)cwi) & !le_p((uint32_t)(cwi >> 32)));
-            // the chunk's loads first (in bounds whatever the step: refused below if it is bad),
-            // then the stream window, then everything that can wait for them
-            const uint32_t src = cm ? (uint32_t)(__ffsll((unsigned long long)cm) - 1) : 0u;
-            const int32_t cv0 = (int32_t)(src * ci64);
-            Vt xs[CIM];
-            uint32_t ps[CIM];
-#pragma unroll
-            for (int g = 0; g < CIM; g++) {
-                const int32_t vi = cv0 + g * 64 + lane, vc = vi < nv32 ? vi : nv32 - 1;
-                xs[g] = reinterpret_cast<const Vt *>(row)[vc];
-                ps[g] = pr[vc];
-            }
-            const BitWin win = bit_window(mybits, mynbits, pos);
-            if (__builtin_expect(progress && (i & (kLeanPub - 1)) == 0, 0) && lane == 0)   // the helpers' pace
-                __hip_atomic_store(progress + b, i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // (after the loads)
-            // a step outside the lean case leaves at the end (a branch here would let the
-            // compiler sink the loads below it); until then its divisions run on safe values
-            // (the step's tests as sign bits of differences and ORs on the scalar unit, one
-            // exit test per step: each ordered 64-bit compare had been a VALU compare feeding
-            // a branch)
-            const uint64_t bad = (uint64_t)(T == 0) | ((uint64_t)(x - l) >> 63) | ((uint64_t)(h - x) >> 63) |
-                                 ((uint64_t)ceil_map & ((w - fthr) >> 63)) | (uint64_t)(cm == 0);
-            const uint64_t Ts = bad ? 1 : T, ws = bad ? 1 : w, vs = bad ? 0 : v;
-            const double iw = recip(ws);
-            const uint64_t tgt = div_small_u(vs, Ts, 0, ws, iw);   // < T < 2^32
-            const uint32_t t32 = (uint32_t)tgt;
-            clk.mark(1);
-            const uint64_t past = pos > mynbits ? pos - mynbits : 0;
-            const int u = past < (uint64_t)prec ? (int)past : prec;
-            clk.mark(2);
-            // the iteration holding the target: the last whose first vector starts at or below it
-            int gs = 0;
-#pragma unroll
-            for (int g = 1; g < CIM; g++) {
-                const bool take = (cv0 + g * 64 < nv32) & ((uint32_t)__builtin_amdgcn_readfirstlane((int)ps[g]) <= t32);
-                gs = take ? g : gs;
-            }
-            Vt xg = xs[0];
-            uint32_t pg = ps[0];
-#pragma unroll
-            for (int g = 1; g < CIM; g++) {
-                xg = gs == g ? xs[g] : xg;
-                pg = gs == g ? ps[g] : pg;
-            }
-            const bool real = cv0 + gs * 64 + lane < nv32;
-            uint32_t c[VEC];
-            uint32_t acc = pg;
-#pragma unroll
-            for (int j = 0; j < VEC; j++) { acc += real ? (uint32_t)vget<E, VEC>(xg, j) : 0u; c[j] = acc; }
-            const uint64_t m2 = __ballot(real & (c[VEC - 1] > t32));
-            const int L = m2 ? __ffsll((unsigned long long)m2) - 1 : 0;
-            uint32_t k = 0, lo = pg, hi = c[VEC - 1];
-#pragma unroll
-            for (int j = VEC - 1; j >= 0; j--) {
-                const bool le = c[j] <= t32;
-                k += le ? 1 : 0;
-                hi = le ? hi : c[j];
-            }
-#pragma unroll
-            for (int j = 0; j < VEC; j++) lo = c[j] <= t32 ? c[j] : lo;
-            const uint64_t lo_c = (uint32_t)__builtin_amdgcn_readlane((int)lo, L);
-            const uint64_t hi_c = (uint32_t)__builtin_amdgcn_readlane((int)hi, L);
-            const int32_t sym = (cv0 + gs * 64 + L) * VEC + __builtin_amdgcn_readlane((int)k, L);
-            clk.mark(3);
-            uint64_t a, bb;
-            div_small_u2(lo_c, hi_c, ws, ceil_map ? Ts - 1 : 0, Ts, bad ? 1.0 : iT, &a, &bb);
-            // (l + a <= x <= l + bb - 1: v in [a, bb))
-            if (bad | (uint64_t)(m2 == 0) | ((vs - a) >> 63) | (((vs - bb) >> 63) ^ 1)) break;
-            clk.mark(4);
-            // the 1-padded end's target only past the stream's end (u > 0): before it the
-            // step is determined (thi = tgt < hi_c)
-            if (__builtin_expect(u != 0, 0)) {
-                const uint64_t vhi = vs + ((1ull << u) - 1);
-                const bool vhi_in = (vhi - ws) >> 63;             // vhi < w
-                const uint64_t thi = vhi_in ? div_small_u(vhi, Ts, 0, ws, iw) : 0;
-                if (firstnd < 0 && !(vhi_in && ((thi - hi_c) >> 63))) firstnd = i;
-            }
-            // narrow + renormalise (decode_advance<true>) without branches: kk = 0 keeps the
-            // registers, and window_bits_nb(.., 0) is 0
-            int64_t nl = l + (int64_t)a, nh = l + (int64_t)bb - 1;
-            const uint64_t d = (uint64_t)(nh - nl);
-            const int sh = bitlen64(d), kk0 = prec - sh, kk = kk0 > 0 ? kk0 : 0;   // (renorm: kk <= 0 is 0)
-            const uint64_t Ev = kk > 0 ? (uint64_t)nl >> sh : 0;
-            nl = (int64_t)(((uint64_t)nl - (Ev << (sh & 63))) << kk);
-            nh = nl + (int64_t)((d + 1) << kk) - 1;
-            const BitWin wu{rfl_u64(win.w0), rfl_u64(win.w1)};
-            x = (int64_t)((((uint64_t)x - (Ev << (sh & 63))) << kk) | window_bits_nb(wu, mynbits, pos, kk));
-            pos += (uint64_t)kk;
-            l = nl;
-            h = nh;
-            if (lane == (i & 63)) sbuf = sym;
-            if (__builtin_expect((i & 63) == 63, 0)) {
-                *outv = sbuf;
-                outv += (int64_t)B32 * 64;
-            }
-            clk.mark(5);
+        for (;;) {
+            if (i >= n32 || !step(cwA, lmA, cwA, lmA)) break;
+            i++;
+            if (i >= n32 || !step(cwB, lmB, cwB, lmB)) break;
+            i++;
         }
     }
 #if LAC_DEC_PHASES
@@ -1200,75 +1294,91 @@ static int decode_stats_path(lac_ctx *c, const E *pmf, int64_t step_stride, int6
     int rc = ensure_chunk_buffers(c);
     if (rc) return rc;
     const unsigned blocks = (unsigned)((c->B + kWavesPerBlock - 1) / kWavesPerBlock);
-    // k_decode_lean: u32 tables, prec <= 50, chunks of at most 4 iterations (V <= 65536); its
-    // buffers hold up to 64 MB of vector CDFs, so its launches take at most that many steps
+    // A static model (stride-0 steps): every step reads the same row per stream, so the
+    // statistics are computed once per stream (rstep 0) and one launch pair covers any
+    // number of steps.
+    const bool stat = step_stride == 0;
+    const int64_t rstep = stat ? 0 : c->B;
+    // k_decode_lean: prec <= 50, chunks of at most 4 iterations (V <= 65536 u32 / 32768 u64
+    // entries), totals lean_total_ok<E> (checked per row); its CDF buffer holds up to
+    // kLeanBytes, so a launch takes at most that many steps' rows
     const int64_t nvec = c->V / VEC, nit = (nvec + 63) / 64;
     const int64_t CI = nit ? (nit + 63) / 64 : 1;
-    // (u64 tables: totals >= 2^32.)  Only for the fewest streams: the stats pass writes a
-    // quarter of the rows' bytes more (the vector CDF), which costs more than the shorter
-    // chain saves once enough streams run side by side (same box, V=32000: B=4 1.36 vs
-    // 2.66 us/step, 64 3.41 vs 3.96, 128 5.39 vs 5.26, 512 18.0 vs 13.3, 1024 34.1 vs 22.8;
-    // profiles/r04/lean/fewstreams/)
-    const bool lean = LAC_LEAN && sizeof(E) == 4 && c->prec <= 50 && CI <= 4 && nvec > 0 && c->B <= kLeanMaxStreams;
-    int64_t cs = c->chunk_steps;
+    // Only for the fewest streams: the stats pass writes as many bytes more as it reads (the
+    // CDF), which costs more than the shorter chain saves once enough streams run side by
+    // side (round 4, per-vector CDF, V=32000: B=4 1.36 vs 2.66 us/step, 64 3.41 vs 3.96, 128
+    // 5.39 vs 5.26; profiles/r04/lean/fewstreams/)
+    bool lean = false;
+    if constexpr (VEC > 1) lean = LAC_LEAN && c->prec <= 50 && CI <= 4 && nvec > 0 && c->B <= kLeanMaxStreams;
+    int64_t cs = stat ? steps : c->chunk_steps;
     if (lean) {
-        const int64_t per = c->B * nvec * (int64_t)sizeof(uint32_t);
-        const int64_t fit = ((int64_t)64 << 20) / per;
-        const int64_t ls = fit < 64 ? 64 : fit / 64 * 64;
-        cs = ls < cs ? ls : cs;
-        if (c->lean_steps < cs) {
-            (void)hipFree(c->lvpre);
+        const int64_t rows_fit = kLeanBytes / (c->V * (int64_t)sizeof(E));
+        if (!stat) {
+            const int64_t fit = rows_fit / c->B;
+            const int64_t ls = fit < 64 ? 64 : fit / 64 * 64;
+            cs = ls < cs ? ls : cs;
+        }
+        const int64_t need = stat ? c->B : cs * c->B;          // CDF rows per launch
+        if (c->lean_rows < need || c->lean_esize != (int)sizeof(E)) {
+            (void)hipFree(c->lcdf);
             (void)hipFree(c->lchunk);
             (void)hipFree(c->lmeta);
-            c->lvpre = nullptr;
+            c->lcdf = nullptr;
             c->lchunk = nullptr;
             c->lmeta = nullptr;
-            c->lean_steps = 0;
-            HIPCHK(hipMalloc(&c->lvpre, sizeof(uint32_t) * cs * c->B * nvec));
-            HIPCHK(hipMalloc(&c->lchunk, sizeof(uint64_t) * 64 * cs * c->B));
-            HIPCHK(hipMalloc(&c->lmeta, sizeof(LeanMeta) * cs * c->B));
-            c->lean_steps = cs;
+            c->lean_rows = 0;
+            HIPCHK(hipMalloc(&c->lcdf, sizeof(E) * need * c->V));
+            HIPCHK(hipMalloc(&c->lchunk, sizeof(uint64_t) * 64 * need));
+            HIPCHK(hipMalloc(&c->lmeta, sizeof(LeanMeta) * need));
+            c->lean_rows = need;
+            c->lean_esize = (int)sizeof(E);
         }
         if (!c->dresume) HIPCHK(hipMalloc(&c->dresume, sizeof(int64_t) * c->B));
     }
     // prefetching helper workgroups for the fewest streams (kLeanHelpers per stream, dealt
-    // to the stream's XCD)
-    const bool help = lean && LAC_LEAN_HELP && c->B <= kLeanHelpMaxStreams;
+    // to the stream's XCD); a static model's rows stay in L2 without them
+    const bool help = lean && !stat && LAC_LEAN_HELP && c->B <= kLeanHelpMaxStreams;
     const int64_t B8 = (c->B + 7) & ~(int64_t)7;
     const unsigned lean_blocks = (unsigned)(help ? B8 * (1 + kLeanHelpers) : c->B);
     if (help && !c->dprogress) HIPCHK(hipMalloc(&c->dprogress, sizeof(int32_t) * c->B));
     for (int64_t t0 = 0; t0 < steps; t0 += cs) {
         const int64_t n = (steps - t0) < cs ? (steps - t0) : cs;
-        const int64_t rows = n * c->B;
+        const int64_t rows = stat ? c->B : n * c->B;
         ProfScope ps(c, KID_DECODE, st);
         const unsigned sblocks = (unsigned)((rows + kWavesPerBlock - 1) / kWavesPerBlock);
-        if (lean) {
-            k_dec_stats<E, VEC, true><<<sblocks, 64 * kWavesPerBlock, 0, st>>>(
-                pmf, step_stride, stream_stride, c->B, rows, c->V, t0, c->q1chunks, (DecRowMeta *)c->dmeta,
-                (uint32_t *)c->lvpre, c->lchunk, (LeanMeta *)c->lmeta);
-            CHECK_LAUNCH();
-            if (help) HIPCHK(hipMemsetAsync(c->dprogress, 0, sizeof(int32_t) * c->B, st));
+        // (a static model's statistics are computed by the first launch only)
+        const bool fresh = !stat || t0 == 0;
+        if constexpr (VEC > 1) {
+            if (lean) {
+                if (fresh) {
+                    k_dec_stats<E, VEC, true><<<sblocks, 64 * kWavesPerBlock, 0, st>>>(
+                        pmf, step_stride, stream_stride, c->B, rows, c->V, t0, c->q1chunks, (DecRowMeta *)c->dmeta,
+                        (E *)c->lcdf, c->lchunk, (LeanMeta *)c->lmeta);
+                    CHECK_LAUNCH();
+                }
+                if (help) HIPCHK(hipMemsetAsync(c->dprogress, 0, sizeof(int32_t) * c->B, st));
 #define LAC_LEAN_K(CIM)                                                                                          \
     k_decode_lean<E, VEC, CIM><<<lean_blocks, 64, 0, st>>>(                                                    \
-        pmf, step_stride, stream_stride, t0, n, c->V, c->prec, (const uint32_t *)c->lvpre, c->lchunk,          \
-        (const LeanMeta *)c->lmeta, c->dec, c->dbits, c->dstride, c->dnbits, out, c->B, c->mapping, c->dresume, \
-        help ? c->dprogress : nullptr)
-            switch (CI) {
-            case 1: LAC_LEAN_K(1); break;
-            case 2: LAC_LEAN_K(2); break;
-            case 3: LAC_LEAN_K(3); break;
-            default: LAC_LEAN_K(4); break;
-            }
+        (const E *)c->lcdf, rstep, t0, n, c->V, c->prec, c->lchunk, (const LeanMeta *)c->lmeta, c->dec, c->dbits, \
+        c->dstride, c->dnbits, out, c->B, c->mapping, c->dec_stop, c->dresume, help ? c->dprogress : nullptr)
+                switch (CI) {
+                case 1: LAC_LEAN_K(1); break;
+                case 2: LAC_LEAN_K(2); break;
+                case 3: LAC_LEAN_K(3); break;
+                default: LAC_LEAN_K(4); break;
+                }
 #undef LAC_LEAN_K
-            CHECK_LAUNCH();
-        } else {
+                CHECK_LAUNCH();
+            }
+        }
+        if (!lean && fresh) {
             k_dec_stats<E, VEC><<<sblocks, 64 * kWavesPerBlock, 0, st>>>(
                 pmf, step_stride, stream_stride, c->B, rows, c->V, t0, c->q1chunks, (DecRowMeta *)c->dmeta);
             CHECK_LAUNCH();
         }
         k_decode_seq<E, VEC><<<blocks, 64 * kWavesPerBlock, 0, st>>>(
             pmf, step_stride, stream_stride, t0, n, c->V, c->prec, c->q1chunks, (const DecRowMeta *)c->dmeta, c->dec,
-            c->dbits, c->dstride, c->dnbits, out, c->B, c->mapping, lean ? c->dresume : nullptr);
+            c->dbits, c->dstride, c->dnbits, out, c->B, c->mapping, lean ? c->dresume : nullptr, rstep, c->dec_stop);
         CHECK_LAUNCH();
     }
     return LAC_OK;
@@ -1294,6 +1404,15 @@ static int decode_block_launch(lac_ctx *c, const E *pmf, int64_t step_stride, in
 static int decode_dispatch(lac_ctx *c, const void *pmf, int64_t step_stride, int64_t stream_stride, int64_t steps,
                            int32_t *out, hipStream_t st) {
     const uintptr_t p = (uintptr_t)pmf;
+    if (c->dec_stop) {                      // LAC_OPT_DECODE_STOP: the stats path's kernels implement it
+        if (c->pmf_bits == 32)
+            return (p % 16 == 0) && c->V % 4 == 0 && step_stride % 4 == 0 && stream_stride % 4 == 0
+                       ? decode_stats_path<uint32_t, 4>(c, (const uint32_t *)pmf, step_stride, stream_stride, steps, out, st)
+                       : decode_stats_path<uint32_t, 1>(c, (const uint32_t *)pmf, step_stride, stream_stride, steps, out, st);
+        return (p % 16 == 0) && c->V % 2 == 0 && step_stride % 2 == 0 && stream_stride % 2 == 0
+                   ? decode_stats_path<uint64_t, 2>(c, (const uint64_t *)pmf, step_stride, stream_stride, steps, out, st)
+                   : decode_stats_path<uint64_t, 1>(c, (const uint64_t *)pmf, step_stride, stream_stride, steps, out, st);
+    }
     const bool wave = c->dpath == LAC_PATH_FUSED || (c->dpath == LAC_PATH_AUTO && c->B >= c->wave_decode_min_streams);
     const int vw = c->pmf_bits == 32 ? 4 : 2;
     const bool vec = (p % 16 == 0) && c->V % vw == 0 && step_stride % vw == 0 && stream_stride % vw == 0;

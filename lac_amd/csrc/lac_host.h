@@ -34,6 +34,7 @@ struct lac_ctx {
     int dpath = LAC_PATH_AUTO;          // decode kernel path
     int64_t wave_decode_min_streams = 2048;   // measured: the stats path wins at 1024 streams
     int fine_decode = 1;                // one-wave decode: per-iteration totals (k_decode_wave_fine)
+    int dec_stop = 0;                   // LAC_OPT_DECODE_STOP: stop before the first undetermined symbol
     int64_t block_decode_min_streams = 1536;  // AUTO below wave_decode_min_streams: block path from here
                                               // (measured after the serial-step rework: the stats path wins
                                               // at 4-128 and 288-1024 streams, block at 160-256 -- its
@@ -50,10 +51,11 @@ struct lac_ctx {
     uint64_t *q1chunks = nullptr;       // logits / stats-path decode: [chunk_steps * B][64] chunk totals
     void *dmeta = nullptr;              // stats-path decode: [chunk_steps * B] DecRowMeta
     int64_t *dresume = nullptr;         //                    [B] first step k_decode_lean left
-    void *lvpre = nullptr;              // lean decode: [lean_steps * B][V / VEC] uint32 vector CDF
-    uint64_t *lchunk = nullptr;         //              [lean_steps * B][64] chunk bounds
-    void *lmeta = nullptr;              //              [lean_steps * B] LeanMeta
-    int64_t lean_steps = 0;             //              steps per launch the buffers hold
+    void *lcdf = nullptr;               // lean decode: [lean_rows][V] per-entry CDF (entry width)
+    uint64_t *lchunk = nullptr;         //              [lean_rows][64] chunk exclusive bounds
+    void *lmeta = nullptr;              //              [lean_rows] LeanMeta
+    int64_t lean_rows = 0;              //              rows the buffers hold
+    int lean_esize = 0;                 //              their entry width (4 / 8 bytes)
     int32_t *dprogress = nullptr;       //              [B] decoder progress for the prefetch helpers
     float *q1m = nullptr;               //                [chunk_steps * B] row maxima
     uint64_t *pxch = nullptr;           // paired row stats (shape 19): [2 * cus] maximum words

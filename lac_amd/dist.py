@@ -566,7 +566,9 @@ class BitstreamGatherer:
         return torch.cat(bits), torch.cat([p[1] for p in parts])
 
     def close(self):
-        """Free the mapped words; the coder writes to its own buffers again."""
+        """Free the mapped words; the coder writes to its own buffers again.  Call it
+        between jobs: lac_set_output refuses a coder that is decoding or holds an
+        unfinished encode (LAC_E_STATE; BatchCoder.reset() first)."""
         if self.trace:
             import json
             with open(self.trace_path, "a") as f:
@@ -575,11 +577,13 @@ class BitstreamGatherer:
                     f.write(json.dumps({"t_us": round((t - t0) * 1e6, 1), "job": k, "what": what, "extra": extra})
                             + "\n")
             self.trace = []
-        if self.native:
-            self.coder.set_output(None, None)
-        for bx in self.boxes:
-            if isinstance(bx["lens"], HostWords):
-                bx["lens"].close()
+        try:
+            if self.native:
+                self.coder.set_output(None, None)
+        finally:
+            for bx in self.boxes:
+                if isinstance(bx["lens"], HostWords):
+                    bx["lens"].close()
 
 
 class _nullctx:

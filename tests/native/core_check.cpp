@@ -65,6 +65,12 @@ uint64_t cc_div_small_mask(uint64_t n, uint64_t m, uint64_t add, uint64_t d, dou
     return div_small_fix_mask(div_small_est(n, m, add, (1.0 / (double)d) * (1.0 + rel)), n, m, add, d);
 }
 
+// div_mid (the lean decode step's u64 ranges): one estimate with the correctly rounded 1/d
+uint64_t cc_div_mid(uint64_t n, uint64_t m, uint64_t add, uint64_t d) {
+    const double inv = 1.0 / (double)d;
+    return div_mid_fix(div_mid_est(n, m, add, inv), n, m, add, d);
+}
+
 uint64_t cc_frac_mul_div(uint64_t c, uint64_t w, uint64_t T, int ceil) {
     const uint64_t f = row_frac(c, T);
     return f == kNoFrac ? ~0ull : frac_mul_div(f, c, w, T, ceil != 0);

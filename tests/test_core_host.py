@@ -157,6 +157,36 @@ def test_div_small_exact(core):
         assert core.cc_div_small_mask(c, w, T - 1, T, -2.0 ** -50) == -(-(c * w) // T)
 
 
+def test_div_mid_exact(core):
+    """div_mid (the lean decode step's ranges on u64 rows with totals of 2^50 and more):
+    exact floor((n*m + add)/d) for quotients up to 2^50 with d anywhere below 2^64, from
+    one estimate and the 128-bit remainder -- random, power-of-two-edge and the decoder's
+    own shapes ceil(c*w/T), c <= T < 2^64, w <= 2^50."""
+    import random
+    core.cc_div_mid.restype = C.c_uint64
+    core.cc_div_mid.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64]
+    rng = random.Random(12)
+    n_cases = 0
+    while n_cases < 40000:
+        d = rng.randint(1, (1 << rng.randint(1, 64)) - 1)
+        m = rng.randint(0, 1 << rng.randint(0, 51))
+        n = rng.randint(0, (1 << rng.randint(0, 64)) - 1)
+        add = rng.choice([0, d - 1, rng.randint(0, d - 1)])
+        q = (n * m + add) // d
+        if q > 1 << 50:
+            continue
+        assert core.cc_div_mid(n, m, add, d) == q, (n, m, add, d)
+        n_cases += 1
+    for _ in range(40000):
+        prec = rng.randint(2, 50)
+        w = rng.randint((1 << (prec - 1)) + 1, 1 << prec)
+        T = rng.choice([rng.randint(1 << 50, (1 << 64) - 1), (1 << 64) - 1, (1 << 63) + rng.randint(0, 99),
+                        rng.randint(1, (1 << 64) - 1)])
+        c = rng.choice([rng.randint(0, T), T, T - 1, 0, 1])
+        assert core.cc_div_mid(c, w, T - 1, T) == -(-(c * w) // T), (c, w, T)
+        assert core.cc_div_mid(c, w, 0, T) == c * w // T, (c, w, T)
+
+
 def test_core_matches_golden(core):
     for kind in ("static", "perstep"):
         for c in load_golden("small_cases.json")[kind]:

@@ -187,3 +187,23 @@ def test_measure_compress_is_lazy_and_prints_progress(capsys):
     # counts 3, 6, 9 print; outputs 4 and 8 print -- 5 lines, as the reference's
     # measure_compress prints for this coder (checked in the build container)
     assert sum(1 for ln in lines if "bits/tok" in ln) == 5
+
+
+def test_bit_list_fast_path_equals_generic():
+    """A_from_bin.run's bit conversion (coder._bit_list): lists / tuples of ints and bools
+    take bytes() + numpy, anything else (numpy ints, floats, strings, generators) the
+    per-element int(); both give the same bits and packed bytes, and values other than
+    0 / 1 raise ValueError either way."""
+    from lac_amd.coder import _bit_list
+    rng = np.random.default_rng(4)
+    for n in (0, 1, 7, 8, 9, 1000, 100001):
+        bits = [int(b) for b in rng.integers(0, 2, n)]
+        want = (bits, np.packbits(np.asarray(bits, dtype=np.uint8)).tobytes())
+        for form in (bits, tuple(bits), [bool(b) for b in bits], [np.int64(b) for b in bits],
+                     [float(b) for b in bits], [str(b) for b in bits], iter(bits)):
+            bl, data = _bit_list(form)
+            assert bl == want[0] and data == want[1]
+            assert all(type(b) is int for b in bl)
+    for bad in ([0, 1, 2], [0, -1], (1, 256), [0, 1, 2.0], iter([1, 3])):
+        with pytest.raises(ValueError):
+            _bit_list(bad)

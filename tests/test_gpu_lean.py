@@ -106,3 +106,153 @@ def test_lean_total_at_2_32_boundary():
     outs = _roundtrip(pmf, sym, prec)
     for path, o in outs.items():
         assert np.array_equal(o, sym), path
+
+
+# ---- round 6: u64 tables (totals below 2^50), static rows, LAC_OPT_DECODE_STOP
+
+def _dev(a):
+    a = np.ascontiguousarray(a)
+    return torch.from_numpy(a.view(np.int32) if a.dtype == np.uint32 else a.view(np.int64)).to(DEV)
+
+
+def _oracle_bits(pmf, sym, prec):
+    """The C oracle's bitstreams (test infrastructure) -> device bits [B, stride], nbits."""
+    from oracle import oracle as coracle
+    out, onb, _, rc = coracle.encode_batch(pmf, sym, prec)
+    assert rc == 0
+    B = pmf.shape[1]
+    stride = ((out.shape[1] + 7) // 8 + 1) * 8
+    buf = np.zeros((B, stride), dtype=np.uint8)
+    buf[:, :out.shape[1]] = out
+    return torch.from_numpy(buf).to(DEV), torch.from_numpy(onb.astype(np.int64)).to(DEV)
+
+
+@pytest.mark.parametrize("prec", [40, 50, 51])
+def test_lean_u64_totals_between_2_32_and_2_50(prec):
+    """u64 tables with totals in (2^32, 2^50): the lean step (prec <= 50) decodes the C
+    oracle's bitstreams to the encoded symbols, as the wave kernel does; rows at 2^50 - 1
+    (lean) and 2^50 (k_decode_seq) interleave, and a fudged row (T > w * minp) hands over
+    mid-stream.  prec 51 takes k_decode_seq throughout."""
+    from lac_amd.batch import BatchCoder
+    rng = np.random.default_rng(prec)
+    V, B, T = 3000, 3, 260
+    pmf = rng.integers(1 << 20, 1 << 24, size=(T, B, V)).astype(np.uint64)   # totals ~2^35
+    pmf[:, 1, :] = rng.integers(1 << 30, 1 << 36, size=(T, V))               # totals ~2^47
+    for t in range(0, T, 7):                                                 # 2^50 - 1 / 2^50 rows
+        row = np.full(V, (1 << 50) // V, dtype=np.uint64)
+        row[0] += (1 << 50) - int(row.sum()) - (t % 2)
+        pmf[t, 2] = row
+    pmf[90, 0, :] = 1 << 37                                                  # T ~ 2^48.6, minp 1:
+    pmf[90, 0, 11] = 1                                                       # fudged below prec 50
+    sym = rng.integers(0, V, size=(T, B)).astype(np.int32)
+    bits, nbits = _oracle_bits(pmf, sym, prec)
+    c = BatchCoder(V, B, prec=prec, pmf_bits=64, capacity_bits=T * (prec + 2) + 256, device=DEV)
+    dp = _dev(pmf)
+    for path in ("stats", "fused"):
+        c.set_decode_path(path)
+        c.decode_open(bits, nbits)
+        assert np.array_equal(c.decode(dp).cpu().numpy(), sym), path
+    c.close()
+
+
+@pytest.mark.parametrize("bits_", [32, 64])
+@pytest.mark.parametrize("prec", [24, 48])
+def test_static_rows_one_stats_row_per_stream(bits_, prec):
+    """A static model (stride-0 steps) takes its row statistics once per stream: 3000 steps
+    in one launch pair, the stats path equal to the wave path; at prec 24 the row fudges
+    (T > w * minp) on some steps, which k_decode_seq takes with the same one row."""
+    from lac_amd.batch import BatchCoder
+    rng = np.random.default_rng(bits_ + prec)
+    V, B, T = 2000, 2, 3000
+    dt = np.uint32 if bits_ == 32 else np.uint64
+    row = rng.integers(1, 1 << 14, size=(B, V)).astype(dt)
+    row[1, 7] = 1                                                            # minp 1
+    sym = rng.integers(0, V, size=(T, B)).astype(np.int32)
+    pmf = np.broadcast_to(row[None], (T, B, V))
+    c = BatchCoder(V, B, prec=prec, pmf_bits=bits_, capacity_bits=T * (prec + 2) + 256, device=DEV)
+    dp = _dev(row).view(1, B, V).expand(T, B, V)
+    c.encode_job(dp, torch.from_numpy(sym).to(DEV))
+    c.raise_on_error()
+    data, nb = c.to_bytes()
+    from oracle import oracle as coracle
+    out, onb, _, rc = coracle.encode_batch(np.ascontiguousarray(pmf), sym, prec)
+    for b in range(B):
+        assert int(nb[b]) == int(onb[b]) and data[b] == out[b, :(int(onb[b]) + 7) // 8].tobytes()
+    for path in ("stats", "fused"):
+        c.set_decode_path(path)
+        c.decode_open()
+        assert np.array_equal(c.decode(dp).cpu().numpy(), sym), path
+    c.close()
+
+
+@pytest.mark.parametrize("storage", [32, 64])
+def test_decode_stop_at_reference_count(storage):
+    """LAC_OPT_DECODE_STOP: decoding past a stream's end, each stream stops by itself
+    before the first symbol its bits do not determine -- after exactly the symbols the
+    reference's bit-serial run(bits, stop=0) emits (decoded_count of the reference-run
+    fixtures: the encoded symbols and the extra ones, rows past the end repeating the last,
+    as the fixtures' Replay predictor) -- with LAC_E_UNDETERMINED, the lean step (prec <= 50)
+    and k_decode_seq alike."""
+    from conftest import load_golden
+    from lac_amd import synth
+    from lac_amd.batch import BatchCoder
+    from lac_amd import _lib
+    from lac_amd.coder import _DEC_STATE
+    import ctypes as C
+    cases = [c for c in load_golden("gen_cases.json") + load_golden("straight_cases.json") if "decoded_count" in c]
+    assert len(cases) >= 10
+    for case in cases:
+        rows = np.stack([synth.pmf_row(case["seed"], t, 0, case["V"], case["kind"], case["exp_range"])
+                         for t in range(case["steps"])])
+        if storage == 32 and rows.dtype != np.uint32:
+            continue
+        rows = rows.astype(np.uint32 if storage == 32 else np.uint64)
+        T, V, prec, n = case["steps"], case["V"], case["prec"], case["decoded_count"]
+        extra = n - T + 20
+        pmf = np.concatenate([rows, np.repeat(rows[-1:], extra, axis=0)])[:, None, :]
+        L = case["L"]
+        data = bytes.fromhex(case["bytes"])
+        buf = np.zeros((1, ((len(data) + 7) // 8 + 1) * 8), dtype=np.uint8)
+        buf[0, :len(data)] = np.frombuffer(data, dtype=np.uint8)
+        c = BatchCoder(V, 1, prec=prec, pmf_bits=storage, capacity_bits=64, device=DEV)
+        c.set_decode_stop(True)
+        c.decode_open(torch.from_numpy(buf).to(DEV), torch.tensor([L], dtype=torch.int64, device=DEV))
+        out = c.decode(_dev(pmf)).cpu().numpy()[:, 0]
+        st = np.zeros(1, dtype=_DEC_STATE)
+        _lib.check(c.lib.lac_decode_get_state(c.ctx, st.ctypes.data_as(C.c_void_p), c._stream))
+        want = case["syms"] + case["decoded_extra"]
+        assert int(st["err"][0]) == _lib.LAC_E_UNDETERMINED and int(st["err_step"][0]) == n, (case["name"], st)
+        assert int(st["nsym"][0]) == n and int(st["ndet"][0]) == n, case["name"]
+        assert out[:n].tolist() == want and (out[n:] == -1).all(), case["name"]
+        c.close()
+
+
+@pytest.mark.parametrize("prec", [30, 48, 50])
+def test_lean_u64_wide_totals(prec):
+    """u64 rows with totals of 2^50 and more take the lean step's wide divisions (the
+    target by div_floor_inv, the ranges by div_mid): llama-scale tables (max(2,
+    floor(softmax * 2^60)), bench --pmf-bits 64), rows with totals in [2^63, 2^64) and
+    just below 2^64, all against the C oracle's bitstreams and the wave kernel."""
+    from lac_amd import synth
+    from lac_amd.batch import BatchCoder
+    V, B, T = 4000, 3, 300
+    pmf_d, sym_d = synth.softmax_tables(T, B, V, seed=5 + prec, device=DEV, scale_bits=60, storage_bits=64)
+    pmf = pmf_d.cpu().numpy().view(np.uint64).copy()
+    sym = sym_d.cpu().numpy()
+    rng = np.random.default_rng(prec)
+    for t in range(0, T, 5):                                    # stream 2: totals in [2^63, 2^64)
+        row = rng.integers(1 << 40, 1 << 51, size=V).astype(np.uint64)
+        row = (row.astype(object) * ((1 << 63) + int(rng.integers(0, 1 << 62))) // int(row.sum())).astype(np.uint64)
+        row[0] += np.uint64(t % 3)
+        pmf[t, 2] = np.maximum(row, 1)
+    pmf[7, 1, :] = np.uint64(((1 << 64) - 1) // V)             # just below 2^64
+    pmf[7, 1, 0] += np.uint64(((1 << 64) - 1) % V)
+    assert int(pmf[7, 1].astype(object).sum()) == (1 << 64) - 1
+    bits, nbits = _oracle_bits(pmf, sym, prec)
+    c = BatchCoder(V, B, prec=prec, pmf_bits=64, capacity_bits=T * (prec + 2) + 256, device=DEV)
+    dp = _dev(pmf)
+    for path in ("stats", "fused"):
+        c.set_decode_path(path)
+        c.decode_open(bits, nbits)
+        assert np.array_equal(c.decode(dp).cpu().numpy(), sym), path
+    c.close()

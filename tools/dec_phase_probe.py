@@ -32,6 +32,12 @@ def main():
     ap.add_argument("--streams", type=int, default=1)
     ap.add_argument("--kernel", default="lean", choices=("lean", "seq"),
                     help="which sequential kernel the probe library runs (seq: a -DLAC_LEAN=0 build)")
+    ap.add_argument("--pmf-bits", type=int, default=32, choices=(32, 64),
+                    help="table storage; 64: llama-scale u64 tables (max(2, floor(softmax * 2^60)))")
+    ap.add_argument("--scale-bits", type=int, default=0,
+                    help="softmax scale of the tables (default 31 for u32, 60 for u64; e.g. 40: u64 totals ~2^40)")
+    ap.add_argument("--static", action="store_true",
+                    help="one row for every step (stride 0): the drop-in surface's static model")
     ap.add_argument("--one-generator", action="store_true",
                     help="tables from one torch generator (for runs under rocprofv3 --pmc)")
     a = ap.parse_args()
@@ -40,12 +46,22 @@ def main():
     from lac_amd.batch import BatchCoder
     dev = torch.device("cuda", 0)
     V, B, T, P = a.vocab, a.streams, a.tokens, 48
-    coder = BatchCoder(V, B, prec=P, pmf_bits=32, capacity_bits=T * (P + 2) + 256, device=dev)
+    coder = BatchCoder(V, B, prec=P, pmf_bits=a.pmf_bits, capacity_bits=T * (P + 2) + 256, device=dev)
     if a.one_generator:                     # (for runs under rocprofv3 --pmc: tools/probe_tables.py)
         from tools.probe_tables import one_generator_tables
         pmf, sym = one_generator_tables(T, B, V, dev)
     else:
-        pmf, sym = synth.softmax_tables(T, B, V, seed=1234, device=dev, scale_bits=31, storage_bits=32)
+        pmf, sym = synth.softmax_tables(T, B, V, seed=1234, device=dev, scale_bits=a.scale_bits or (31 if a.pmf_bits == 32 else 60),
+                                        storage_bits=a.pmf_bits)
+    if a.static:                            # the first step's rows for every step, symbols drawn from them
+        row = pmf[:1]
+        cdf = torch.cumsum(row[0].to(torch.int64) & (0xFFFFFFFF if a.pmf_bits == 32 else -1), dim=-1)
+        g = torch.Generator(device=dev).manual_seed(5)
+        u = torch.rand((T, B), generator=g, device=dev, dtype=torch.float64)
+        tgt = (u * cdf[:, -1].double()[None]).floor().long().clamp(max=int(cdf[:, -1].min()) - 1)
+        sym = torch.stack([torch.searchsorted(cdf[b], tgt[:, b].contiguous(), right=True) for b in range(B)], 1)
+        sym = sym.to(torch.int32).contiguous()
+        pmf = row.expand(T, B, V)
     coder.encode_job(pmf, sym)
     lib = coder.lib
     probe = hasattr(lib, "lac_debug_dec_phases")     # (a plain library: kernel times only)
@@ -68,7 +84,7 @@ def main():
         if probe:
             lib.lac_debug_dec_phases(C.cast(out, C.c_void_p), 1)
         steps = max(int(out[6]), 1)
-        names = (["top+window", "target+ballot+load_issue", "shadow(thi,next_row)", "wait+scan+select", "ranges",
+        names = (["top", "chunk+load_issue+target", "past", "wait+iteration+search", "ranges+exit",
                   "advance+output"] if a.kernel == "lean" else
                  ["totals+scan", "targets", "chunk_search", "reread+scan", "ranges", "renorm"])
         cyc = {n: out[k] / steps for k, n in enumerate(names)}
