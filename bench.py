@@ -102,6 +102,12 @@ def main():
                     help="run the bitstream gather (lac_amd.dist.BitstreamGatherer) even on one rank: a "
                          "one-rank RCCL group, the gather inside the timed region, parity.gather_ok")
     ap.add_argument("--gather-batch", type=int, default=8, help="jobs per bitstream exchange (the gatherer's batch)")
+    ap.add_argument("--save-inputs", default=None, metavar="PREFIX",
+                    help="write this rank's synthetic inputs to PREFIX.r<rank>.{pmf,sym}.npy and go on")
+    ap.add_argument("--load-inputs", default=None, metavar="PREFIX",
+                    help="read the inputs --save-inputs wrote instead of generating them: the same workload "
+                         "bit for bit with no torch RNG kernel in this process (profiled runs: torch.randn's "
+                         "launches crashed the host under rocprofv3 --pmc, profiles/r06/pmc_rng/)")
     ap.add_argument("--input", default="pmf", choices=("pmf", "logits-bf16", "logits-f32"),
                     help="pmf rows (BASELINE c3, default) or raw logits quantised in-kernel (q1, SURVEY §8(f)1)")
     args = ap.parse_args()
@@ -157,7 +163,16 @@ def main():
     ebytes = args.pmf_bits // 8 if not logits_in else (2 if args.input == "logits-bf16" else 4)
     t_gen = time.time()
     coder = BatchCoder(V, B, prec=P, pmf_bits=args.pmf_bits, capacity_bits=T * (P + 2) + 256, device=dev)
-    if logits_in:
+    if args.load_inputs:
+        pre = f"{args.load_inputs}.r{rank}"
+        pmf = torch.from_numpy(np.load(pre + ".pmf.npy")).to(dev)
+        sym = torch.from_numpy(np.load(pre + ".sym.npy")).to(dev)
+        if logits_in:
+            pmf = pmf.view(torch.bfloat16 if ebytes == 2 else torch.float32)
+        if tuple(pmf.shape) != (T, B, V) or tuple(sym.shape) != (T, B):
+            raise SystemExit(f"{pre}: inputs of shape {tuple(pmf.shape)} / {tuple(sym.shape)}, expected "
+                             f"{(T, B, V)} / {(T, B)}")
+    elif logits_in:
         logits, sym = synth.logits_batch(T, B, V, seed=1234 + 7919 * rank, device=dev,
                                          dtype=torch.bfloat16 if ebytes == 2 else torch.float32,
                                          quantise=coder.quantize_logits)
@@ -169,6 +184,10 @@ def main():
     torch.cuda.synchronize()
     log(f"[rank {rank}] inputs {tuple(pmf.shape)} {pmf.dtype} ({pmf.numel() * ebytes / 2**30:.2f} GiB) "
         f"in {time.time() - t_gen:.1f}s")
+    if args.save_inputs:
+        pre = f"{args.save_inputs}.r{rank}"
+        np.save(pre + ".pmf.npy", (pmf.view(torch.int16) if ebytes == 2 and logits_in else pmf).cpu().numpy())
+        np.save(pre + ".sym.npy", sym.cpu().numpy())
 
     if args.path != "auto":
         coder.set_path(args.path)

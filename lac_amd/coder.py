@@ -1041,9 +1041,9 @@ class A_from_bin:
                     check(c.lib.lac_decode_set_state(c.ctx, new.ctypes.data_as(C.c_void_p), c._stream))
                 start = new
                 sess.st = start
-                for s in syms:
-                    tab.accept(s)
-                    yield s
+                # a static model's accept is the base no-op (_is_static): the reference calls
+                # it per symbol to no effect, so the symbols go out without the calls
+                yield from syms
                 done += got
                 if err or got < n:
                     return

@@ -912,12 +912,6 @@ constexpr int kLeanHelpMaxStreams = 16;         // above: no helpers (L2: ~2.6 M
 #define LAC_LEAN_PUB 8
 #endif
 constexpr int kLeanPub = LAC_LEAN_PUB;          // the decoder publishes its progress every kLeanPub steps
-#ifndef LAC_LEAN_PROD64
-#define LAC_LEAN_PROD64 1        // k_decode_lean, u64 rows: the search by products, no target division
-#endif
-#ifndef LAC_LEAN_PROD32
-#define LAC_LEAN_PROD32 0        // the same for u32 rows (their division is short: in the loads' shadow)
-#endif
 #ifndef LAC_LEAN_BYTES
 #define LAC_LEAN_BYTES (256ll << 20)
 #endif
@@ -1038,10 +1032,6 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
 #else
     NoClock clk;
 #endif
-    // PROD: the search compares entries with the target floor(v*T/w) as products (c*w <=
-    // v*T), no division -- for u64 rows, whose target divides in 128 bits (div_floor_inv:
-    // longer than the chunk's loads); u32 rows divide (div_small_u) in the loads' shadow
-    constexpr bool PROD = W ? LAC_LEAN_PROD64 : LAC_LEAN_PROD32;
     // one step with row data (cwi, lm); the next-but-one row's loads go into (pcw, plm) once
     // this step's chunk loads are issued.  false: the stream leaves (not this step's case)
     auto step = [&](const uint64_t cwi, const uint64_t lmv, uint64_t &pcw, uint64_t &plm) -> bool {
@@ -1101,61 +1091,65 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
                              ((uint64_t)ceil_map & ((w - fthr) >> 63)) | (uint64_t)(cm == 0);
         const uint64_t Ts = bad ? 1 : T, ws = bad ? 1 : w, vs = bad ? 0 : v;
         const uint64_t ex0 = W ? readlane_u64(cwi, (int)src) : (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cwi, (int)src);
-        // u64 rows with totals of 2^50 and more (llama-scale tables): div_mid's ranges
+        // the target: u32 rows and u64 rows below 2^50 divide (div_small, in the loads'
+        // shadow) and compare entries with it; u64 rows of 2^50 and more (llama-scale
+        // tables), whose target would divide in 128 bits past the loads' return, compare
+        // entries by products (c*w <= v*T) and take div_mid's ranges
         const bool small = !W || Ts < kSmallQuot;               // uniform
-        double iw = 0.0;
-        E te = 0;
-        if constexpr (!PROD) {
-            iw = recip(ws);
-            te = (E)div_small_u(vs, Ts, 0, ws, iw);           // < T
-        }
-        auto lte = [&](E c) { if constexpr (PROD) return le((uint64_t)c); else return c <= te; };   // c <= tgt
+        const double iw = recip(ws);
+        const E te = small ? (E)div_small_u(vs, Ts, 0, ws, iw) : (E)0;
         clk.mark(1);
         const uint64_t past = pos > mynbits ? pos - mynbits : 0;
         const int u = past < (uint64_t)prec ? (int)past : prec;
         clk.mark(2);
-        // the iteration holding the target: the last whose CDF value just before it (the
-        // chunk's bound, else lane 63's last entry of the iteration before) is <= tgt
         int gs = 0;
         E exg = (E)ex0;
+        uint64_t m2, lo_l, hi_c, prev;
+        uint32_t kL;
+        int L;
+        auto search = [&](auto lte) {                           // lte(c): c <= tgt
+            // the iteration holding the target: the last whose CDF value just before it (the
+            // chunk's bound, else lane 63's last entry of the iteration before) is <= tgt
 #pragma unroll
-        for (int g = 1; g < CIM; g++) {
-            const E eg = W ? (E)readlane_u64((uint64_t)vget<E, VEC>(xs[g - 1], VEC - 1), 63)
-                           : (E)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)vget<E, VEC>(xs[g - 1], VEC - 1), 63);
-            const bool take = (cv0 + g * 64 < nv32) & lte(eg);
-            gs = take ? g : gs;
-            exg = take ? eg : exg;
-        }
-        Vt xg = xs[0];
+            for (int g = 1; g < CIM; g++) {
+                const E eg = W ? (E)readlane_u64((uint64_t)vget<E, VEC>(xs[g - 1], VEC - 1), 63)
+                               : (E)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)vget<E, VEC>(xs[g - 1], VEC - 1), 63);
+                const bool take = (cv0 + g * 64 < nv32) & lte(eg);
+                gs = take ? g : gs;
+                exg = take ? eg : exg;
+            }
+            Vt xg = xs[0];
 #pragma unroll
-        for (int g = 1; g < CIM; g++) xg = gs == g ? xs[g] : xg;
-        const bool real = cv0 + gs * 64 + lane < nv32;
-        const uint64_t m2 = __ballot(real & !lte(vget<E, VEC>(xg, VEC - 1)));
-        const int L = m2 ? __ffsll((unsigned long long)m2) - 1 : 0;
-        // lane L's entries: k of them <= tgt, then the symbol's; its lower bound is the
-        // entry before (lane L's, lane L-1's last, or the iteration's start value)
-        uint32_t k = 0;
-        E lo = 0, hi = vget<E, VEC>(xg, VEC - 1);
+            for (int g = 1; g < CIM; g++) xg = gs == g ? xs[g] : xg;
+            const bool real = cv0 + gs * 64 + lane < nv32;
+            m2 = __ballot(real & !lte(vget<E, VEC>(xg, VEC - 1)));
+            L = m2 ? __ffsll((unsigned long long)m2) - 1 : 0;
+            // lane L's entries: k of them <= tgt, then the symbol's; its lower bound is the
+            // entry before (lane L's, lane L-1's last, or the iteration's start value)
+            uint32_t k = 0;
+            E lo = 0, hi = vget<E, VEC>(xg, VEC - 1);
 #pragma unroll
-        for (int j = VEC - 1; j >= 0; j--) {
-            const E c = vget<E, VEC>(xg, j);
-            const bool cle = lte(c);
-            k += cle ? 1 : 0;
-            hi = cle ? hi : c;
-            lo = (cle && lo == 0) ? c : lo;                     // the last entry <= tgt (entries ascend)
-        }
-        const int Lp = L > 0 ? L - 1 : 0;
-        uint64_t lo_l, hi_c, prev;
-        if constexpr (W) {
-            lo_l = readlane_u64(lo, L);
-            hi_c = readlane_u64(hi, L);
-            prev = readlane_u64(vget<E, VEC>(xg, VEC - 1), Lp);
-        } else {
-            lo_l = (uint32_t)__builtin_amdgcn_readlane((int)lo, L);
-            hi_c = (uint32_t)__builtin_amdgcn_readlane((int)hi, L);
-            prev = (uint32_t)__builtin_amdgcn_readlane((int)vget<E, VEC>(xg, VEC - 1), Lp);
-        }
-        const uint32_t kL = (uint32_t)__builtin_amdgcn_readlane((int)k, L);
+            for (int j = VEC - 1; j >= 0; j--) {
+                const E c = vget<E, VEC>(xg, j);
+                const bool cle = lte(c);
+                k += cle ? 1 : 0;
+                hi = cle ? hi : c;
+                lo = (cle && lo == 0) ? c : lo;                 // the last entry <= tgt (entries ascend)
+            }
+            const int Lp = L > 0 ? L - 1 : 0;
+            if constexpr (W) {
+                lo_l = readlane_u64(lo, L);
+                hi_c = readlane_u64(hi, L);
+                prev = readlane_u64(vget<E, VEC>(xg, VEC - 1), Lp);
+            } else {
+                lo_l = (uint32_t)__builtin_amdgcn_readlane((int)lo, L);
+                hi_c = (uint32_t)__builtin_amdgcn_readlane((int)hi, L);
+                prev = (uint32_t)__builtin_amdgcn_readlane((int)vget<E, VEC>(xg, VEC - 1), Lp);
+            }
+            kL = (uint32_t)__builtin_amdgcn_readlane((int)k, L);
+        };
+        if (!W || small) search([&](E c) { return c <= te; });
+        else search([&](E c) { return le((uint64_t)c); });
         const uint64_t lo_c = kL ? lo_l : (L > 0 ? prev : (uint64_t)exg);
         const int32_t sym = (cv0 + gs * 64 + L) * VEC + (int32_t)kL;
         clk.mark(3);

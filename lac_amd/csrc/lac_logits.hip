@@ -37,18 +37,6 @@ __constant__ uint32_t c_q1_tab[LAC_Q1_TAB_SIZE] = LAC_Q1_TAB_INIT;
 #ifndef LAC_Q1_SCHED
 #define LAC_Q1_SCHED 0           // scheduling fence between vectors in k_q1_stats
 #endif
-#ifndef LAC_Q1_CONTIG
-#define LAC_Q1_CONTIG 0          // k_q1_stats, one row per block: wave w holds 8 consecutive 64-vector groups
-#endif
-#ifndef LAC_Q1_LATE_TAIL
-#define LAC_Q1_LATE_TAIL 0       // k_q1_stats decode form (DIRECT): a row's butterfly tail + chunk store after the next row's max post
-#endif
-#ifndef LAC_Q1_ROLL_FIRST
-#define LAC_Q1_ROLL_FIRST 0      // k_q1_stats decode form: each vector's prefetch load before its halving step
-#endif
-#ifndef LAC_Q1_PERM
-#define LAC_Q1_PERM 0            // k_q1_stats decode form: register slot j holds tile position bitrev3(j), so the
-#endif                           // streamed butterfly's order (slots 0 4 2 6 1 5 3 7) rolls loads in address order
 #ifndef LAC_Q1_DEFER_DEC
 #define LAC_Q1_DEFER_DEC 0       // k_q1_stats decode form: a row's chunk stores after the next row's max
                                  // (measured: 3 VGPRs spilled, decode stats 42.1 -> 42.7 us per bf16 c3
@@ -344,13 +332,10 @@ template <int TB> struct RowSrc<false, TB> {
 // in parallel and the sequential kernels only touch a few bytes per step.
 constexpr int kQ1Waves = 8;
 
-struct Q1Ident {
-    __device__ int operator()(int j) const { return j; }
-};
-template <int R, typename Src, typename Pos = Q1Ident>
-__device__ inline void q1_load_tile(u32x4 (&x)[R], const Src &src, int base, int gt, int NT, Pos pos = Pos()) {
+template <int R, typename Src>
+__device__ inline void q1_load_tile(u32x4 (&x)[R], const Src &src, int base, int gt, int NT) {
 #pragma unroll
-    for (int j = 0; j < R; j++) x[j] = src(base + gt + NT * pos(j));
+    for (int j = 0; j < R; j++) x[j] = src(base + gt + NT * j);
 }
 
 template <typename LT, int RW, int R, bool DEC, bool MULTI, bool PF, int NWB>
@@ -385,17 +370,6 @@ __global__ __launch_bounds__(64 * NWB, LAC_Q1_MINW) void k_q1_stats(const LT *__
     const int tid = threadIdx.x, lane = tid & 63, w = BUF ? wave_in_block() : tid >> 6;   // BUF: SGPR rows
     const int g = NR == 1 ? 0 : w / RW, wg = NR == 1 ? w : w % RW;
     int gt = tid - g * NT;
-    // vector j of a thread: cbase + cstep * j of its tile -- strided by the group's threads
-    // (wave wg holds groups wg, wg + RW, ...), or (CONTIG, one row per block) wave wg holds
-    // R consecutive groups, so its chunk totals are one contiguous store
-    constexpr bool CONTIG = LAC_Q1_CONTIG && NR == 1 && !MULTI;
-    const int cbase = CONTIG ? wg * 64 * R + lane : gt;
-    constexpr int cstep = CONTIG ? 64 : NT;
-    // PERM (decode form, 8 vectors): slot j holds the tile's vector at position bitrev3(j) --
-    // the streamed butterfly consumes slots 0 4 2 6 1 5 3 7, and its rolling prefetch then
-    // issues the next row's loads in address order
-    constexpr bool PERM = LAC_Q1_PERM && DEC && R == 8 && !MULTI;
-    auto spos = [](int j) { return PERM ? (((j & 1) << 2) | (j & 2) | ((j >> 2) & 1)) : j; };
     if (DEC && wg == 0) bins[g][lane] = 0;
     const int nvec = (int)(V / N);
     const int ntiles = MULTI ? (nvec + NT * R - 1) / (NT * R) : 1;
@@ -404,7 +378,7 @@ __global__ __launch_bounds__(64 * NWB, LAC_Q1_MINW) void k_q1_stats(const LT *__
     u32x4 x[R];
     if (PF) {                                                  // first tile of the block's first row,
         const int64_t r0 = (int64_t)blockIdx.x * NR + g;      // in flight while the table fills
-        q1_load_tile<R>(x, Src(r0 < rows ? row_of(r0) : lg, r0 < rows, nvec), 0, cbase, cstep, spos);
+        q1_load_tile<R>(x, Src(r0 < rows ? row_of(r0) : lg, r0 < rows, nvec), 0, gt, NT);
     }
     // the 16-vector shapes sit at the 128-VGPR cap: the fast fill's live loads spill them
     // (bf16 V = 128256 decode stats 220 -> 283 us per step)
@@ -412,7 +386,7 @@ __global__ __launch_bounds__(64 * NWB, LAC_Q1_MINW) void k_q1_stats(const LT *__
     else q1_fill_tab_rep<kQ1Rep, 64 * NWB>(tabr, xsh);
     const uint32_t loff = (uint32_t)(lane & (kQ1Rep - 1)) << 2;
     // one 16-B vector of a tile, for the rolling prefetches
-    auto ld_vec = [&](const Src &src, int tile, int j) { return src(tile * NT * R + cbase + cstep * spos(j)); };
+    auto ld_vec = [&](const Src &src, int tile, int j) { return src(tile * NT * R + gt + NT * j); };
     // decode form, deferred stores (LAC_Q1_DEFER_DEC): the group's writer wave keeps row
     // r's 64 chunk totals and maximum in registers and stores them once the next row's
     // maximum is taken.  A store counts in vmcnt like a load, so one issued at the row's
@@ -429,25 +403,6 @@ __global__ __launch_bounds__(64 * NWB, LAC_Q1_MINW) void k_q1_stats(const LT *__
             pend_r = -1;
         }
     };
-    // LATE (decode form, DIRECT): row r's last butterfly steps and chunk stores run after row
-    // r+1's maximum is posted, before the barrier that gathers it, so a wave's tail overlaps
-    // the other waves' arrival instead of preceding its own
-    constexpr bool LATE = DEC && LAC_Q1_LATE_TAIL && !MULTI && R == 8 && RW * R == 64 && !LAC_Q1_DEFER_DEC &&
-                          LAC_Q1_DEC_DIRECT;
-    uint32_t late_sv = 0;
-    float late_m = 0.f;
-    int64_t late_r = -1;
-    auto late_tail = [&]() {
-        if constexpr (LATE) {
-            if (late_r >= 0) {                                 // block-uniform
-                const uint64_t gsum = wave_multi_sum32_tail8(late_sv);
-                const int grp = wg + RW * spos(q_index<R>(lane));
-                if (lane < R) chunks[late_r * 64 + grp] = grp * 64 < nvec ? gsum : 0;
-                if (w == 0 && lane == 0) mrow[late_r] = late_m;
-                late_r = -1;
-            }
-        }
-    };
     int par = 0;
     for (int64_t rb = (int64_t)blockIdx.x * NR; rb < rows; rb += stride, par ^= 1) {
         // gt opaque per row: the R per-vector lane offsets / indices derived from it are
@@ -461,7 +416,7 @@ __global__ __launch_bounds__(64 * NWB, LAC_Q1_MINW) void k_q1_stats(const LT *__
         if (MULTI) {
             // PF: tile k+1's vector j loads into x[j] as soon as tile k's max has used it
             for (int tile = 0; tile < ntiles; tile++) {
-                if (!PF) q1_load_tile<R>(x, row, tile * NT * R, cbase, cstep, spos);
+                if (!PF) q1_load_tile<R>(x, row, tile * NT * R, gt, NT);
 #pragma unroll
                 for (int j = 0; j < R; j++) {
 #pragma unroll
@@ -473,7 +428,7 @@ __global__ __launch_bounds__(64 * NWB, LAC_Q1_MINW) void k_q1_stats(const LT *__
                 }
             }
         } else {
-            if (!PF) q1_load_tile<R>(x, row, 0, cbase, cstep, spos);   // PF: loaded during the last row
+            if (!PF) q1_load_tile<R>(x, row, 0, gt, NT);   // PF: loaded during the last row
             if constexpr (!IMAX) {
 #pragma unroll
                 for (int j = 0; j < R; j++)
@@ -502,7 +457,6 @@ __global__ __launch_bounds__(64 * NWB, LAC_Q1_MINW) void k_q1_stats(const LT *__
             });
             if (lane == 0) smaxi[par][w] = wi;
             if (!DEC && gt == 0) sps[g] = 0;
-            late_tail();
             __syncthreads();
             int bi = smaxi[par][0];
 #pragma unroll
@@ -525,7 +479,6 @@ __global__ __launch_bounds__(64 * NWB, LAC_Q1_MINW) void k_q1_stats(const LT *__
             mx = wave_max_f32(mx);
             if (lane == 0) smax[par][w] = mx;
             if (!DEC && gt == 0) sps[g] = 0;
-            late_tail();
             __syncthreads();
             m = smax[par][g * RW];
 #pragma unroll
@@ -549,10 +502,10 @@ __global__ __launch_bounds__(64 * NWB, LAC_Q1_MINW) void k_q1_stats(const LT *__
             for (int j = 0; j < R; j++) asm volatile("" : "+v"(x[j]));
         }
         for (int tile = ntiles - 1; tile >= 0; tile--) {
-            if (MULTI && !PF && tile != ntiles - 1) q1_load_tile<R>(x, row, tile * NT * R, cbase, cstep, spos);
+            if (MULTI && !PF && tile != ntiles - 1) q1_load_tile<R>(x, row, tile * NT * R, gt, NT);
             uint32_t sv[R];
             auto take = [&](int j, uint32_t sl) {
-                const int vi = tile * NT * R + cbase + cstep * spos(j);
+                const int vi = tile * NT * R + gt + NT * j;
                 sl = vi < nvec ? sl : 0;
                 if (DEC) {
                     sv[j] = sl;
@@ -607,40 +560,33 @@ __global__ __launch_bounds__(64 * NWB, LAC_Q1_MINW) void k_q1_stats(const LT *__
             // vector earlier, not the instruction before -- DPP after a VALU write of its
             // source needs wait states, and roll()'s scheduling fence kept the compiler
             // from filling them)
-            constexpr bool RF = STREAM && LAC_Q1_ROLL_FIRST;   // the load before the halving step
             if (fast) {                                        // row-uniform branch, outside the vector loop
 #pragma unroll
                 for (int q = 0; q < R; q++) {
                     const int j = STREAM ? kHalveOrder[q] : q;
                     take(j, q1_vec_sum<LT>(x[j], c, true, tabr, loff));
-                    if (RF) roll(j);
                     if (q > 0) pair_halve(STREAM ? kHalveOrder[q - 1] : q - 1);
-                    if (!RF) roll(j);
+                    roll(j);
                 }
             } else {
 #pragma unroll
                 for (int q = 0; q < R; q++) {
                     const int j = STREAM ? kHalveOrder[q] : q;
                     take(j, q1_vec_sum<LT>(x[j], c, false, tabr, loff));
-                    if (RF) roll(j);
                     if (q > 0) pair_halve(STREAM ? kHalveOrder[q - 1] : q - 1);
-                    if (!RF) roll(j);
+                    roll(j);
                 }
             }
             pair_halve(STREAM ? kHalveOrder[R - 1] : R - 1);
-            if constexpr (LATE) {                              // the tail after the next row's max post
-                late_sv = sv[0];
-                late_m = m;
-                late_r = valid ? r : -1;
-            } else if (DEC) {
+            if (DEC) {
                 uint64_t gsum;                                 // group total of index q_index(lane)
                 if constexpr (STREAM) gsum = wave_multi_sum32_tail8(sv[0]);
                 else gsum = wave_multi_sum32<R>(sv);
                 if constexpr (DIRECT) {                        // every chunk once: grp covers 0..63
-                    const int grp = CONTIG ? wg * R + q_index<R>(lane) : wg + RW * spos(q_index<R>(lane));
+                    const int grp = wg + RW * q_index<R>(lane);
                     if (lane < R && valid) chunks[r * 64 + grp] = grp * 64 < nvec ? gsum : 0;
                 } else if (lane < R) {
-                    const int grp = tile * RW * R + (CONTIG ? wg * R + q_index<R>(lane) : wg + RW * spos(q_index<R>(lane)));
+                    const int grp = tile * RW * R + wg + RW * q_index<R>(lane);
                     if (grp * 64 < nvec) atomicAdd(&bins[g][grp / (int)G], (unsigned long long)gsum);
                 }
             }
@@ -650,7 +596,7 @@ __global__ __launch_bounds__(64 * NWB, LAC_Q1_MINW) void k_q1_stats(const LT *__
             if (lane == 0) { ssum[w][0] = t64; ssum[w][1] = l64; }
         }
         if constexpr (DIRECT) {
-            if (!LATE && valid && w == 0 && lane == 0) mrow[r] = m;
+            if (valid && w == 0 && lane == 0) mrow[r] = m;
         } else {
             __syncthreads();
         }
@@ -681,7 +627,6 @@ __global__ __launch_bounds__(64 * NWB, LAC_Q1_MINW) void k_q1_stats(const LT *__
         }
     }
     flush_pending();
-    late_tail();
 }
 
 // k_q1_stats_rl: the q1 row statistics for rows of 8193..16384 16-B vectors (bf16
