@@ -699,10 +699,11 @@ _TAIL_STATE = np.dtype([("l", "<i8"), ("h", "<i8"), ("lb", "<i8"), ("hb", "<i8")
 
 
 def _bit_list(bits):
-    """A bit sequence (any iterable of 0 / 1, as the reference's run takes) -> (list of
-    ints, its bytes packed MSB first: group_bits' format).  Lists and tuples of ints go
-    through bytes() and numpy (~1 ms per 10^5 bits, against ~25 ms for the per-element
-    int() and range checks they take otherwise)."""
+    """A bit sequence (any iterable of 0 / 1, as the reference's run takes) -> (the bits
+    as a sequence of ints -- a list, or a bytearray, which a session appends to and
+    indexes alike -- and their bytes packed MSB first: group_bits' format).  Lists and
+    tuples of ints go through bytes() and numpy (~0.3 ms per 10^5 bits, against ~25 ms
+    for the per-element int() and range checks they take otherwise)."""
     if isinstance(bits, (list, tuple)):
         try:
             raw = bytes(bits)
@@ -712,7 +713,7 @@ def _bit_list(bits):
             a = np.frombuffer(raw, dtype=np.uint8)
             if a.size and int(a.max()) > 1:
                 raise ValueError("bits are 0 or 1")
-            return list(raw), np.packbits(a).tobytes()
+            return bytearray(raw), np.packbits(a).tobytes()
     bl = [int(b) for b in bits]
     if any(b not in (0, 1) for b in bl):
         raise ValueError("bits are 0 or 1")
@@ -756,6 +757,7 @@ class _Session:
         self.st["det"] = 1
         self.st["err_step"] = -1
         self.tst = None                                   # reference frame (tail mode)
+        self.stopped_undetermined = False                 # _fast_static stopped before an undetermined symbol
         if self.tab.uniform:
             # Predictor(n)'s val_to_symbol is not the inverse of its floor
             # symbol_to_range, so emit_symbol's overlap check (arith_code.py:277)
@@ -808,7 +810,7 @@ class _Session:
 
     def load_bits(self, bl, data):
         """Take a whole bit list at once (the fast path): the same buffers add_bit builds."""
-        self.bits = bl if isinstance(bl, list) else list(bl)
+        self.bits = bl if isinstance(bl, (list, bytearray)) else list(bl)
         self.buf = np.zeros(max(64, ((len(bl) >> 3) + 8) * 2 + 7 & ~7), dtype=np.uint8)   # rows 8-byte aligned
         self.buf[:len(data)] = np.frombuffer(data, dtype=np.uint8)
         self.dev = None
@@ -979,7 +981,8 @@ class A_from_bin:
         tab = sess.tab
         if tab.static:
             yield from self._fast_static(sess, max_symbols)
-            yield from sess.decide()
+            if not sess.stopped_undetermined:          # (else decide() would find the same)
+                yield from sess.decide()
             return
         for _ in range(max_symbols):
             row = tab.row()
@@ -1027,6 +1030,7 @@ class A_from_bin:
                 new = np.zeros(1, dtype=_DEC_STATE)
                 check(c.lib.lac_decode_get_state(c.ctx, new.ctypes.data_as(C.c_void_p), c._stream))
                 err = int(new["err"][0])
+                sess.stopped_undetermined = err == _lib.LAC_E_UNDETERMINED
                 # the stream stopped (undetermined) or failed at err_step with the registers of
                 # that point; every symbol before it is determined
                 got = (int(new["err_step"][0]) if err else int(new["nsym"][0])) - int(start["nsym"][0])

@@ -237,6 +237,22 @@ __host__ __device__ inline uint64_t div_mid_fix(uint64_t q, uint64_t n, uint64_t
     return q - neg + ge;
 }
 
+// floor((n*m + add) / d) from a rounded estimate within one of the quotient (div_small_est
+// with inv good to a few ulps and a quotient whose ulps stay below 1/2) and a remainder
+// n*m + add - q*d in [-d, 2d) that wrapping 64-bit arithmetic holds (d < 2^62): two sign
+// tests instead of div_small_fix_mask's five.  The lean decode step's u32 rows (T < 2^32):
+// the target floor(v*T/w) (quotient < 2^32, inv = the device reciprocal of w) and the
+// ranges ceil(c*w/T) (c <= T, quotient <= 2^50, inv = 1/T correctly rounded).  N32: n
+// below 2^32 (the ranges' CDF entries), so n*m is a 32 x 64-bit product.
+template <bool N32 = false>
+__host__ __device__ inline uint64_t div_near_fix(uint64_t q, uint64_t n, uint64_t m, uint64_t add, uint64_t d) {
+    const uint64_t nm = N32 ? (uint64_t)(uint32_t)n * m : n * m;
+    const uint64_t r = nm + add - q * d;
+    const uint64_t neg = sign_mask64(r);                      // r < 0: one less
+    const uint64_t ge = ~sign_mask64(r - d) & ~neg;           // r >= d: one more
+    return q + neg - ge;
+}
+
 // CDFPredictor.fudged_dist test (arith_code.py:84): fudged iff T > w*minp.
 __host__ __device__ inline bool is_fudged(uint64_t T, uint64_t w, uint64_t minp) {
     return (u128)T > (u128)w * minp;

@@ -371,6 +371,24 @@ __device__ inline void div_small_u2(uint64_t n0, uint64_t n1, uint64_t m, uint64
     *q1 = div_small_fix_u<MASK>(e1, n1, m, add, d);
 }
 
+// div_near (lac_core.h div_near_fix) with wave-uniform arguments: the lean step's u32 rows
+__device__ inline uint64_t div_near_u(uint64_t n, uint64_t m, uint64_t add, uint64_t d, double inv) {
+    return div_near_fix(rfl_u64(div_small_est(n, m, add, inv)), n, m, add, d);
+}
+template <bool N32 = true>
+__device__ inline void div_near_u2(uint64_t n0, uint64_t n1, uint64_t m, uint64_t add, uint64_t d, double inv,
+                                   uint64_t *q0, uint64_t *q1) {
+    const uint64_t e0 = rfl_u64(div_small_est(n0, m, add, inv)), e1 = rfl_u64(div_small_est(n1, m, add, inv));
+    *q0 = div_near_fix<N32>(e0, n0, m, add, d);
+    *q1 = div_near_fix<N32>(e1, n1, m, add, d);
+}
+// 1/d to ~1 ulp: the device reciprocal with two Newton steps (recip() takes one), for
+// estimates whose quotient reaches 2^50 and must stay within one (div_near on u64 rows)
+__device__ inline double recip2(uint64_t d) {
+    const double dd = (double)d, r = recip(d);
+    return __builtin_fma(r, __builtin_fma(-dd, r, 1.0), r);
+}
+
 // div_mid (lac_core.h) with wave-uniform arguments, both of a pair's estimates first so
 // their FP64 chains overlap: the lean step's ranges on u64 rows with totals >= 2^50.
 __device__ inline void div_mid_u2(uint64_t n0, uint64_t n1, uint64_t m, uint64_t add, uint64_t d, double inv,

@@ -771,11 +771,10 @@ __global__ __launch_bounds__(256) void k_dec_stats(const E *__restrict__ pmf, in
         lchunk[r * 64 + lane] = in - mine;                     // chunk lane's exclusive bound
         const uint64_t T = (uint64_t)acc128;
         const bool ok = !bad && lean_total_ok<E>(T) && minp != 0;
-        // u64 rows: 1/T correctly rounded (an IEEE divide, once per row), which div_mid's
-        // one-estimate bound needs; u32 rows: the device reciprocal, as div_small's
+        // 1/T correctly rounded (an IEEE divide, once per row): the one-estimate bounds of
+        // div_mid (u64 rows) and div_near (u32 rows) need it
         if (lane == 0)
-            lmeta[r] = LeanMeta{ok ? T : 0, ok ? (T + minp - 1) / minp : 0,
-                                W ? 1.0 / (double)(ok ? T : 1) : recip(ok ? T : 1), 0};
+            lmeta[r] = LeanMeta{ok ? T : 0, ok ? (T + minp - 1) / minp : 0, 1.0 / (double)(ok ? T : 1), 0};
     }
 }
 
@@ -1089,15 +1088,19 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
         // exit test per step)
         const uint64_t bad = (uint64_t)(T == 0) | ((uint64_t)(x - l) >> 63) | ((uint64_t)(h - x) >> 63) |
                              ((uint64_t)ceil_map & ((w - fthr) >> 63)) | (uint64_t)(cm == 0);
-        const uint64_t Ts = bad ? 1 : T, ws = bad ? 1 : w, vs = bad ? 0 : v;
+        // (a bad step computes on whatever values it has -- no load or store depends on them
+        // -- and leaves at the exit test below)
+        const uint64_t Ts = T, ws = w, vs = v;
         const uint64_t ex0 = W ? readlane_u64(cwi, (int)src) : (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cwi, (int)src);
         // the target: u32 rows and u64 rows below 2^50 divide (div_small, in the loads'
         // shadow) and compare entries with it; u64 rows of 2^50 and more (llama-scale
         // tables), whose target would divide in 128 bits past the loads' return, compare
         // entries by products (c*w <= v*T) and take div_mid's ranges
         const bool small = !W || Ts < kSmallQuot;               // uniform
-        const double iw = recip(ws);
-        const E te = small ? (E)div_small_u(vs, Ts, 0, ws, iw) : (E)0;
+        // (div_near: the estimate is within one of the quotient, two sign tests; for u64 rows,
+        // whose target reaches 2^50, with 1/w to ~1 ulp)
+        const double iw = W ? recip2(ws) : recip(ws);
+        const E te = (!W || small) ? (E)div_near_u(vs, Ts, 0, ws, iw) : (E)0;
         clk.mark(1);
         const uint64_t past = pos > mynbits ? pos - mynbits : 0;
         const int u = past < (uint64_t)prec ? (int)past : prec;
@@ -1154,8 +1157,9 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
         const int32_t sym = (cv0 + gs * 64 + L) * VEC + (int32_t)kL;
         clk.mark(3);
         uint64_t a, bb;
-        if (small) div_small_u2(lo_c, hi_c, ws, ceil_map ? Ts - 1 : 0, Ts, bad ? 1.0 : iT, &a, &bb);
-        else div_mid_u2(lo_c, hi_c, ws, ceil_map ? Ts - 1 : 0, Ts, bad ? 1.0 : iT, &a, &bb);
+        if (!W) div_near_u2<true>(lo_c, hi_c, ws, ceil_map ? Ts - 1 : 0, Ts, iT, &a, &bb);
+        else if (small) div_near_u2<false>(lo_c, hi_c, ws, ceil_map ? Ts - 1 : 0, Ts, iT, &a, &bb);
+        else div_mid_u2(lo_c, hi_c, ws, ceil_map ? Ts - 1 : 0, Ts, iT, &a, &bb);
         // (l + a <= x <= l + bb - 1: v in [a, bb))
         if (bad | (uint64_t)(m2 == 0) | ((vs - a) >> 63) | (((vs - bb) >> 63) ^ 1)) return false;
         clk.mark(4);

@@ -71,6 +71,15 @@ uint64_t cc_div_mid(uint64_t n, uint64_t m, uint64_t add, uint64_t d) {
     return div_mid_fix(div_mid_est(n, m, add, inv), n, m, add, d);
 }
 
+// div_near (the lean decode step's u32 rows): estimate with 1/d moved `ulps` ULPs off the
+// correctly rounded value (the target's device reciprocal), two sign tests; n32: n < 2^32
+uint64_t cc_div_near(uint64_t n, uint64_t m, uint64_t add, uint64_t d, int ulps, int n32) {
+    double inv = 1.0 / (double)d;
+    for (int i = 0; i < (ulps < 0 ? -ulps : ulps); i++) inv = nextafter(inv, ulps < 0 ? 0.0 : 1.0e300);
+    const uint64_t q = div_small_est(n, m, add, inv);
+    return n32 ? div_near_fix<true>(q, n, m, add, d) : div_near_fix<false>(q, n, m, add, d);
+}
+
 uint64_t cc_frac_mul_div(uint64_t c, uint64_t w, uint64_t T, int ceil) {
     const uint64_t f = row_frac(c, T);
     return f == kNoFrac ? ~0ull : frac_mul_div(f, c, w, T, ceil != 0);

@@ -187,6 +187,37 @@ def test_div_mid_exact(core):
         assert core.cc_div_mid(c, w, 0, T) == c * w // T, (c, w, T)
 
 
+def test_div_near_exact(core):
+    """div_near (the lean decode step's rows below 2^50, two sign tests): u32 rows' targets
+    floor(v*T/w), T < 2^32, with the reciprocal of w up to 16 ulps off (the device's
+    v_rcp_f64 + Newton is good to ~11), and the ranges ceil(c*w/T), c <= T < 2^32, with
+    the correctly rounded 1/T the stats pass stores -- prec 2..50, adversarial and random."""
+    import random
+    core.cc_div_near.restype = C.c_uint64
+    core.cc_div_near.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, C.c_int]
+    rng = random.Random(13)
+    for _ in range(60000):
+        prec = rng.randint(2, 50)
+        w = rng.choice([rng.randint((1 << (prec - 1)) + 1, 1 << prec), 1 << prec, (1 << (prec - 1)) + 1])
+        T = rng.choice([rng.randint(1, (1 << 32) - 1), (1 << 32) - 1, rng.randint(1, 1 << 16), 1])
+        v = rng.choice([rng.randint(0, w - 1), w - 1, 0])
+        ulps = rng.choice([0, 16, -16, rng.randint(-16, 16)])
+        assert core.cc_div_near(v, T, 0, w, ulps, 0) == v * T // w, (v, T, w, ulps)
+        c = rng.choice([rng.randint(0, T), T, T - 1, 0, 1])
+        assert core.cc_div_near(c, w, T - 1, T, 0, 1) == -(-(c * w) // T), (c, w, T)
+        assert core.cc_div_near(c, w, 0, T, 0, 1) == c * w // T, (c, w, T)
+    # u64 rows below 2^50: targets with 1/w within 1 ulp (recip2), ranges with 1/T exact
+    for _ in range(60000):
+        prec = rng.randint(2, 50)
+        w = rng.choice([rng.randint((1 << (prec - 1)) + 1, 1 << prec), 1 << prec, (1 << (prec - 1)) + 1])
+        T = rng.choice([rng.randint(1, (1 << 50) - 1), (1 << 50) - 1, rng.randint(1 << 32, 1 << 50)])
+        v = rng.choice([rng.randint(0, w - 1), w - 1, 0])
+        ulps = rng.choice([0, 1, -1])
+        assert core.cc_div_near(v, T, 0, w, ulps, 0) == v * T // w, (v, T, w, ulps)
+        c = rng.choice([rng.randint(0, T), T, T - 1, 0, 1])
+        assert core.cc_div_near(c, w, T - 1, T, 0, 0) == -(-(c * w) // T), (c, w, T)
+
+
 def test_core_matches_golden(core):
     for kind in ("static", "perstep"):
         for c in load_golden("small_cases.json")[kind]:

@@ -202,8 +202,8 @@ def test_bit_list_fast_path_equals_generic():
         for form in (bits, tuple(bits), [bool(b) for b in bits], [np.int64(b) for b in bits],
                      [float(b) for b in bits], [str(b) for b in bits], iter(bits)):
             bl, data = _bit_list(form)
-            assert bl == want[0] and data == want[1]
-            assert all(type(b) is int for b in bl)
+            assert list(bl) == want[0] and data == want[1]
+            assert all(type(b) is int for b in bl) and isinstance(bl, (list, bytearray))
     for bad in ([0, 1, 2], [0, -1], (1, 256), [0, 1, 2.0], iter([1, 3])):
         with pytest.raises(ValueError):
             _bit_list(bad)
