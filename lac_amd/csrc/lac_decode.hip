@@ -1100,6 +1100,9 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
         // (div_near: the estimate is within one of the quotient, two sign tests; for u64 rows,
         // whose target reaches 2^50, with 1/w to ~1 ulp)
         const double iw = W ? recip2(ws) : recip(ws);
+        // (u64 rows of 2^50 and more: the search compares by products -- their target by
+        // div_floor_inv's two estimates and 128-bit remainders in the loads' shadow measured
+        // slower, 1.775 vs 1.70 us per c2 step, profiles/r06/lean/)
         const E te = (!W || small) ? (E)div_near_u(vs, Ts, 0, ws, iw) : (E)0;
         clk.mark(1);
         const uint64_t past = pos > mynbits ? pos - mynbits : 0;
