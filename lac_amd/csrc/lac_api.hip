@@ -91,6 +91,7 @@ int lac_close(lac_ctx *c) {
     (void)hipFree(c->lchunk);
     (void)hipFree(c->lmeta);
     (void)hipFree(c->dprogress);
+    (void)hipFree(c->lwin);
     (void)hipFree(c->q1m);
     (void)hipFree(c->pxch);
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);

@@ -6,6 +6,8 @@
 // one wave per stream (k_decode_wave_fine); fewer streams take the block and stats
 // paths (k_decode_block; k_dec_stats + k_decode_seq / k_decode_lean); the flush and
 // windows that leave [l, h] run in the reference's own frame (lac_tail.h).
+#include <type_traits>
+
 #include "lac_host.h"
 #include "lac_dec_dev.h"
 
@@ -768,9 +770,12 @@ __global__ __launch_bounds__(256) void k_dec_stats(const E *__restrict__ pmf, in
     if (lane == 0) meta[r] = DecRowMeta{bad ? 0 : (uint64_t)acc128, minp};
     if constexpr (LEAN) {
         const uint64_t in = wave_incl_scan_u64(mine);
-        lchunk[r * 64 + lane] = in - mine;                     // chunk lane's exclusive bound
         const uint64_t T = (uint64_t)acc128;
         const bool ok = !bad && lean_total_ok<E>(T) && minp != 0;
+        // chunk lane's exclusive bound; a row not for the lean step gets bounds no target
+        // passes (c*w <= v*T fails for c = 2^64 - 1 and for its low word), so the step finds
+        // no chunk and leaves without testing T
+        lchunk[r * 64 + lane] = ok ? in - mine : ~0ull;
         // 1/T correctly rounded (an IEEE divide, once per row): the one-estimate bounds of
         // div_mid (u64 rows) and div_near (u32 rows) need it
         if (lane == 0)
@@ -955,6 +960,30 @@ __device__ void lean_helper(const E *lcdf, int64_t rstep, int32_t n32, int64_t V
     }
 }
 
+// The bit streams as k_decode_lean reads them: word j of stream b holds stream bits
+// 64j .. 64j+63 in reading order (the stream's 8 bytes byte-swapped), bits past nbits cleared,
+// then zero words to the row's end (wstride = stride / 8 + 2 words per stream).  The step then
+// reads its 128-bit window as two scalar words at one clamped index, with no end mask and no
+// byte swaps on its chain.  Built once per decode call (the streams are constant while open).
+__global__ __launch_bounds__(256) void k_lean_window(const uint8_t *__restrict__ bits, uint64_t stride,
+                                                     const uint64_t *__restrict__ nbits, uint64_t *__restrict__ win,
+                                                     int64_t wstride, int64_t B) {
+    const int64_t b = blockIdx.y;
+    if (b >= B) return;
+    const uint64_t nb = nbits[b], cap = stride / 8;
+    const uint64_t nw = (nb + 63) >> 6 < cap ? (nb + 63) >> 6 : cap;   // (nb > 8 * stride fails in k_dec_init)
+    const uint64_t *src = reinterpret_cast<const uint64_t *>(bits + b * stride);
+    for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < wstride; j += (int64_t)gridDim.x * 256) {
+        uint64_t w = 0;
+        if ((uint64_t)j < nw) {
+            w = bswap64(src[j]);
+            const uint64_t in = nb - (uint64_t)j * 64;         // stream bits in this word
+            if (in < 64) w &= ~0ull << (64 - in);
+        }
+        win[b * wstride + j] = w;
+    }
+}
+
 // e * w <= P (P = v * T as hi:lo): the chunk test of the lean step, lane-parallel.  u32 tables:
 // e < 2^32, w < 2^51, the products split at bit 32 (below 2^83); u64 tables: e < 2^50, full
 // 128-bit products (below 2^101).
@@ -975,7 +1004,7 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
                                                     int64_t nsteps, int64_t V, int prec,
                                                     const uint64_t *__restrict__ lchunk,
                                                     const LeanMeta *__restrict__ lmeta, DecState *states,
-                                                    const uint8_t *__restrict__ bits, uint64_t stride,
+                                                    const uint64_t *__restrict__ lwin, int64_t wstride,
                                                     const uint64_t *__restrict__ nbits, int32_t *sym_out, int64_t B,
                                                     int mapping, int stop_undet, int64_t *__restrict__ resume,
                                                     int32_t *progress) {
@@ -991,8 +1020,10 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
     if (b >= B) return;
     DecState st = states[b];
     dec_state_uniform(st);
-    const uint8_t *mybits = bits + b * stride;
+    const uint64_t *mywin = lwin + b * wstride;
     const uint64_t mynbits = rfl_u64(nbits[b]);
+    const uint64_t nwc = (uint64_t)wstride - 2;                 // words past the stream's own: zero
+    const uint64_t mynw = (mynbits + 63) >> 6 < nwc ? (mynbits + 63) >> 6 : nwc;
     int64_t CI, nch;
     dec_chunk_layout<E, VEC>(V, &CI, &nch);
     const int32_t nv32 = (int32_t)(V / VEC);                    // (<= 16384: CI <= 4)
@@ -1033,7 +1064,8 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
 #endif
     // one step with row data (cwi, lm); the next-but-one row's loads go into (pcw, plm) once
     // this step's chunk loads are issued.  false: the stream leaves (not this step's case)
-    auto step = [&](const uint64_t cwi, const uint64_t lmv, uint64_t &pcw, uint64_t &plm) -> bool {
+    // PUB: the first step of a pair, whose i is even, publishes the decoder's progress
+    auto step = [&](const uint64_t cwi, const uint64_t lmv, uint64_t &pcw, uint64_t &plm, auto pub) -> bool {
         l = (int64_t)rfl_u64((uint64_t)l);                      // (the loop's phis are not seen as uniform)
         h = (int64_t)rfl_u64((uint64_t)h);
         x = (int64_t)rfl_u64((uint64_t)x);
@@ -1072,21 +1104,25 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
             const int32_t vi = cv0 + g * 64 + lane, vc = vi < nv32 ? vi : nv32 - 1;
             xs[g] = row[vc];
         }
-        const BitWin win = bit_window(mybits, mynbits, pos);
-        if (moving) {                                           // row i+2 (the last row again past the end)
-            const bool more = i + 2 < n32;
-            pcw = *(more ? lcv : lcv - rstep * 64);
-            plm = lmw[(more ? li : li - rstep) * 4];
-            lcv += more ? rstep * 64 : 0;
-            li += more ? rstep : 0;
+        // the stream window: words pos/64 and the next, clamped to the zero words past the end
+        const uint64_t wi = (pos >> 6) < mynw ? (pos >> 6) : mynw;
+        const uint64_t W0 = mywin[wi], W1 = mywin[wi + 1];
+        if (moving) {                                           // row i+2 (the buffers hold two rows past the
+            pcw = *lcv;                                         // launch's last: read, never used)
+            plm = lmw[li * 4];
+            lcv += rstep * 64;
+            li += rstep;
         }
-        if (__builtin_expect(progress && (i & (kLeanPub - 1)) == 0, 0) && lane == 0)   // the helpers' pace
-            __hip_atomic_store(progress + b, i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // (after the loads)
+        if constexpr (decltype(pub)::value) {
+            if (__builtin_expect(progress && (i & (kLeanPub - 1)) == 0, 0) && lane == 0)   // the helpers' pace
+                __hip_atomic_store(progress + b, i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // (after the loads)
+        }
         // a step outside the lean case leaves at the end (a branch here would let the
         // compiler sink the loads below it); until then its divisions run on safe values
         // (the step's tests as sign bits of differences and ORs on the scalar unit, one
         // exit test per step)
-        const uint64_t bad = (uint64_t)(T == 0) | ((uint64_t)(x - l) >> 63) | ((uint64_t)(h - x) >> 63) |
+        // (a row not for the lean step, T = 0 in its LeanMeta, has chunk bounds no target passes: cm == 0)
+        const uint64_t bad = ((uint64_t)(x - l) >> 63) | ((uint64_t)(h - x) >> 63) |
                              ((uint64_t)ceil_map & ((w - fthr) >> 63)) | (uint64_t)(cm == 0);
         // (a bad step computes on whatever values it has -- no load or store depends on them
         // -- and leaves at the exit test below)
@@ -1115,7 +1151,10 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
         int L;
         auto search = [&](auto lte) {                           // lte(c): c <= tgt
             // the iteration holding the target: the last whose CDF value just before it (the
-            // chunk's bound, else lane 63's last entry of the iteration before) is <= tgt
+            // chunk's bound, else lane 63's last entry of the iteration before) is <= tgt.
+            // (Its vectors selected by the take tests themselves: a select on gs == g was
+            // turned into an indexed read of xs[] through scratch memory for CIM >= 3.)
+            Vt xg = xs[0];
 #pragma unroll
             for (int g = 1; g < CIM; g++) {
                 const E eg = W ? (E)readlane_u64((uint64_t)vget<E, VEC>(xs[g - 1], VEC - 1), 63)
@@ -1123,10 +1162,8 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
                 const bool take = (cv0 + g * 64 < nv32) & lte(eg);
                 gs = take ? g : gs;
                 exg = take ? eg : exg;
+                xg = take ? xs[g] : xg;
             }
-            Vt xg = xs[0];
-#pragma unroll
-            for (int g = 1; g < CIM; g++) xg = gs == g ? xs[g] : xg;
             const bool real = cv0 + gs * 64 + lane < nv32;
             m2 = __ballot(real & !lte(vget<E, VEC>(xg, VEC - 1)));
             L = m2 ? __ffsll((unsigned long long)m2) - 1 : 0;
@@ -1185,8 +1222,11 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
         const uint64_t Ev = kk > 0 ? (uint64_t)nl >> sh : 0;
         nl = (int64_t)(((uint64_t)nl - (Ev << (sh & 63))) << kk);
         nh = nl + (int64_t)((d + 1) << kk) - 1;
-        const BitWin wu{rfl_u64(win.w0), rfl_u64(win.w1)};
-        x = (int64_t)((((uint64_t)x - (Ev << (sh & 63))) << kk) | window_bits_nb(wu, mynbits, pos, kk));
+        // the top kk bits of the window at pos (kk <= 50; bits past the stream's end are zeros)
+        const int off = (int)(pos & 63);
+        const uint64_t W0u = rfl_u64(W0), W1u = rfl_u64(W1);
+        const uint64_t wv = (((W0u << off) | ((W1u >> 1) >> (63 - off))) >> 1) >> (63 - kk);
+        x = (int64_t)((((uint64_t)x - (Ev << (sh & 63))) << kk) | wv);
         pos += (uint64_t)kk;
         l = nl;
         h = nh;
@@ -1200,9 +1240,9 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
     };
     if (!st.err) {
         for (;;) {
-            if (i >= n32 || !step(cwA, lmA, cwA, lmA)) break;
+            if (i >= n32 || !step(cwA, lmA, cwA, lmA, std::true_type{})) break;
             i++;
-            if (i >= n32 || !step(cwB, lmB, cwB, lmB)) break;
+            if (i >= n32 || !step(cwB, lmB, cwB, lmB, std::false_type{})) break;
             i++;
         }
     }
@@ -1309,6 +1349,7 @@ static int decode_stats_path(lac_ctx *c, const E *pmf, int64_t step_stride, int6
     // CDF), which costs more than the shorter chain saves once enough streams run side by
     // side (round 4, per-vector CDF, V=32000: B=4 1.36 vs 2.66 us/step, 64 3.41 vs 3.96, 128
     // 5.39 vs 5.26; profiles/r04/lean/fewstreams/)
+    const int64_t wstride = (int64_t)(c->dstride / 8) + 2;     // k_lean_window's words per stream
     bool lean = false;
     if constexpr (VEC > 1) lean = LAC_LEAN && c->prec <= 50 && CI <= 4 && nvec > 0 && c->B <= kLeanMaxStreams;
     int64_t cs = stat ? steps : c->chunk_steps;
@@ -1329,12 +1370,25 @@ static int decode_stats_path(lac_ctx *c, const E *pmf, int64_t step_stride, int6
             c->lmeta = nullptr;
             c->lean_rows = 0;
             HIPCHK(hipMalloc(&c->lcdf, sizeof(E) * need * c->V));
-            HIPCHK(hipMalloc(&c->lchunk, sizeof(uint64_t) * 64 * need));
-            HIPCHK(hipMalloc(&c->lmeta, sizeof(LeanMeta) * need));
+            // (two rows more: the step's prefetch of row i+2 reads past the launch's last row)
+            HIPCHK(hipMalloc(&c->lchunk, sizeof(uint64_t) * 64 * (need + 2 * c->B)));
+            HIPCHK(hipMalloc(&c->lmeta, sizeof(LeanMeta) * (need + 2 * c->B)));
             c->lean_rows = need;
             c->lean_esize = (int)sizeof(E);
         }
         if (!c->dresume) HIPCHK(hipMalloc(&c->dresume, sizeof(int64_t) * c->B));
+        const int64_t words = c->B * wstride;
+        if (c->lwin_words < words) {
+            (void)hipFree(c->lwin);
+            c->lwin = nullptr;
+            c->lwin_words = 0;
+            HIPCHK(hipMalloc(&c->lwin, sizeof(uint64_t) * words));
+            c->lwin_words = words;
+        }
+        const unsigned wblocks = (unsigned)((wstride + 255) / 256 < 64 ? (wstride + 255) / 256 : 64);
+        k_lean_window<<<dim3(wblocks, (unsigned)c->B), 256, 0, st>>>(c->dbits, c->dstride, c->dnbits, c->lwin, wstride,
+                                                                     c->B);
+        CHECK_LAUNCH();
     }
     // prefetching helper workgroups for the fewest streams (kLeanHelpers per stream, dealt
     // to the stream's XCD); a static model's rows stay in L2 without them
@@ -1360,8 +1414,8 @@ static int decode_stats_path(lac_ctx *c, const E *pmf, int64_t step_stride, int6
                 if (help) HIPCHK(hipMemsetAsync(c->dprogress, 0, sizeof(int32_t) * c->B, st));
 #define LAC_LEAN_K(CIM)                                                                                          \
     k_decode_lean<E, VEC, CIM><<<lean_blocks, 64, 0, st>>>(                                                    \
-        (const E *)c->lcdf, rstep, t0, n, c->V, c->prec, c->lchunk, (const LeanMeta *)c->lmeta, c->dec, c->dbits, \
-        c->dstride, c->dnbits, out, c->B, c->mapping, c->dec_stop, c->dresume, help ? c->dprogress : nullptr)
+        (const E *)c->lcdf, rstep, t0, n, c->V, c->prec, c->lchunk, (const LeanMeta *)c->lmeta, c->dec, c->lwin,   \
+        wstride, c->dnbits, out, c->B, c->mapping, c->dec_stop, c->dresume, help ? c->dprogress : nullptr)
                 switch (CI) {
                 case 1: LAC_LEAN_K(1); break;
                 case 2: LAC_LEAN_K(2); break;

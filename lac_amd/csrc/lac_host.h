@@ -57,6 +57,8 @@ struct lac_ctx {
     int64_t lean_rows = 0;              //              rows the buffers hold
     int lean_esize = 0;                 //              their entry width (4 / 8 bytes)
     int32_t *dprogress = nullptr;       //              [B] decoder progress for the prefetch helpers
+    uint64_t *lwin = nullptr;           //              [B][lwin_stride] the bit streams as big-endian words, zero-padded
+    int64_t lwin_words = 0;             //              words lwin holds
     float *q1m = nullptr;               //                [chunk_steps * B] row maxima
     uint64_t *pxch = nullptr;           // paired row stats (shape 19): [2 * cus] maximum words
     int64_t xch_abort = -1;             // word of pxch holding the last row-group launch's abort flag
