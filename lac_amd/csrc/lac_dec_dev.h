@@ -389,6 +389,18 @@ __device__ inline double recip2(uint64_t d) {
     return __builtin_fma(r, __builtin_fma(-dd, r, 1.0), r);
 }
 
+// recip / recip2 of a d below 2^52, converted by the 2^52 magic (small_to_f64) instead of a
+// general u64 -> f64 conversion: the lean step's 1/w (w <= 2^50), the same values
+__device__ inline double recip_small(uint64_t d) {
+    const double dd = small_to_f64(d);
+    const double r = __builtin_amdgcn_rcp(dd);
+    return __builtin_fma(r, __builtin_fma(-dd, r, 1.0), r);
+}
+__device__ inline double recip2_small(uint64_t d) {
+    const double dd = small_to_f64(d), r = recip_small(d);
+    return __builtin_fma(r, __builtin_fma(-dd, r, 1.0), r);
+}
+
 // div_mid (lac_core.h) with wave-uniform arguments, both of a pair's estimates first so
 // their FP64 chains overlap: the lean step's ranges on u64 rows with totals >= 2^50.
 __device__ inline void div_mid_u2(uint64_t n0, uint64_t n1, uint64_t m, uint64_t add, uint64_t d, double inv,

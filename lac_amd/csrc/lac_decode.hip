@@ -1122,7 +1122,9 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
         // (the step's tests as sign bits of differences and ORs on the scalar unit, one
         // exit test per step)
         // (a row not for the lean step, T = 0 in its LeanMeta, has chunk bounds no target passes: cm == 0)
-        const uint64_t bad = ((uint64_t)(x - l) >> 63) | ((uint64_t)(h - x) >> 63) |
+        // (unsigned differences: signed ones were folded back into ordered 64-bit compares,
+        // which are vector instructions)
+        const uint64_t bad = (((uint64_t)x - (uint64_t)l) >> 63) | (((uint64_t)h - (uint64_t)x) >> 63) |
                              ((uint64_t)ceil_map & ((w - fthr) >> 63)) | (uint64_t)(cm == 0);
         // (a bad step computes on whatever values it has -- no load or store depends on them
         // -- and leaves at the exit test below)
@@ -1135,14 +1137,12 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
         const bool small = !W || Ts < kSmallQuot;               // uniform
         // (div_near: the estimate is within one of the quotient, two sign tests; for u64 rows,
         // whose target reaches 2^50, with 1/w to ~1 ulp)
-        const double iw = W ? recip2(ws) : recip(ws);
+        const double iw = W ? recip2_small(ws) : recip_small(ws);   // (w <= 2^50: exact as a double)
         // (u64 rows of 2^50 and more: the search compares by products -- their target by
         // div_floor_inv's two estimates and 128-bit remainders in the loads' shadow measured
         // slower, 1.775 vs 1.70 us per c2 step, profiles/r06/lean/)
         const E te = (!W || small) ? (E)div_near_u(vs, Ts, 0, ws, iw) : (E)0;
         clk.mark(1);
-        const uint64_t past = pos > mynbits ? pos - mynbits : 0;
-        const int u = past < (uint64_t)prec ? (int)past : prec;
         clk.mark(2);
         int gs = 0;
         E exg = (E)ex0;
@@ -1205,7 +1205,9 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
         clk.mark(4);
         // the 1-padded end past the stream's end (u > 0; before it the step is determined):
         // determined iff vhi < w and floor(vhi*T/w) < hi_c, i.e. vhi*T < hi_c*w
-        if (__builtin_expect(u != 0, 0)) {
+        if (__builtin_expect((mynbits - pos) >> 63, 0)) {        // pos > nbits
+            const uint64_t past = pos - mynbits;
+            const int u = past < (uint64_t)prec ? (int)past : prec;
             const uint64_t vhi = vs + ((1ull << u) - 1);
             const bool vhi_in = (vhi - ws) >> 63;                 // vhi < w
             const u128 PH = (u128)vhi * Ts, HW = (u128)hi_c * ws;
