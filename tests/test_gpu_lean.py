@@ -256,3 +256,25 @@ def test_lean_u64_wide_totals(prec):
         c.decode_open(bits, nbits)
         assert np.array_equal(c.decode(dp).cpu().numpy(), sym), path
     c.close()
+
+
+def test_lean_many_groups_two_streams():
+    """V = 32000 u32 with 2 streams: the 256 MB lean buffers hold 1024 steps' rows, so
+    4000 steps are four launch groups; one stream leaves the lean case (totals >= 2^32)
+    for 100 steps inside the second group and comes back in it."""
+    from lac_amd.batch import BatchCoder
+    rng = np.random.default_rng(21)
+    V, B, T, prec = 32000, 2, 4000, 48
+    pmf = rng.integers(1, 60000, size=(T, B, V)).astype(np.uint32)
+    pmf[1500:1600, 1, :] = rng.integers(1 << 17, 1 << 18, size=(100, V))   # totals > 2^32
+    sym = rng.integers(0, V, size=(T, B)).astype(np.int32)
+    c = BatchCoder(V, B, prec=prec, capacity_bits=T * (prec + 20) + 256, device=DEV)
+    dp = torch.from_numpy(pmf.view(np.int32)).to(DEV)
+    c.encode_job(dp, torch.from_numpy(sym).to(DEV))
+    c.raise_on_error()
+    for path in ("stats", "fused"):
+        c.set_decode_path(path)
+        c.decode_open()
+        got = c.decode(dp).cpu().numpy()
+        assert np.array_equal(got, sym), (path, np.argwhere(got != sym)[:4])
+    c.close()
