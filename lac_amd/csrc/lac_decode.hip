@@ -656,7 +656,7 @@ __device__ inline void dec_chunk_layout(int64_t V, int64_t *CI, int64_t *nch) {
 struct LeanMeta {
     uint64_t T;            // the total; 0: not for the lean step (bad row, u32 total >= 2^32, minp 0)
     uint64_t fthr;         // ceil(T / minp): the ceil mapping's range is fudged iff w < fthr (arith_code.py:84)
-    double iT;             // recip(T)
+    double iT;             // 1/T correctly rounded
     uint64_t pad;
 };
 // Totals the lean step takes: below 2^32 for u32 tables (their CDF then fits the entries'
@@ -1140,7 +1140,8 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
         const double iw = W ? recip2_small(ws) : recip_small(ws);   // (w <= 2^50: exact as a double)
         // (u64 rows of 2^50 and more: the search compares by products -- their target by
         // div_floor_inv's two estimates and 128-bit remainders in the loads' shadow measured
-        // slower, 1.775 vs 1.70 us per c2 step, profiles/r06/lean/)
+        // slower, 1.775 vs 1.70 us per c2 step, profiles/r06/lean/, and a search against a
+        // double window around the target no faster, profiles/r06/lean2/wideapprox/)
         const E te = (!W || small) ? (E)div_near_u(vs, Ts, 0, ws, iw) : (E)0;
         clk.mark(1);
         clk.mark(2);

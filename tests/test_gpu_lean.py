@@ -229,8 +229,8 @@ def test_decode_stop_at_reference_count(storage):
 
 @pytest.mark.parametrize("prec", [30, 48, 50])
 def test_lean_u64_wide_totals(prec):
-    """u64 rows with totals of 2^50 and more take the lean step's wide divisions (the
-    target by div_floor_inv, the ranges by div_mid): llama-scale tables (max(2,
+    """u64 rows with totals of 2^50 and more take the lean step's wide form (the search
+    against a double window around the target, the ranges by div_mid): llama-scale tables (max(2,
     floor(softmax * 2^60)), bench --pmf-bits 64), rows with totals in [2^63, 2^64) and
     just below 2^64, all against the C oracle's bitstreams and the wave kernel."""
     from lac_amd import synth
@@ -277,4 +277,34 @@ def test_lean_many_groups_two_streams():
         c.decode_open()
         got = c.decode(dp).cpu().numpy()
         assert np.array_equal(got, sym), (path, np.argwhere(got != sym)[:4])
+    c.close()
+
+
+@pytest.mark.parametrize("prec", [49, 50])
+def test_lean_u64_wide_clustered_entries(prec):
+    """Wide rows (totals near 2^60) whose small entries (4096 .. 8191, so the ceil mapping
+    is never fudged at prec >= 49) sit closer together than the search's double window:
+    targets among them make the window ambiguous and the search reruns with products.
+    Most symbols are drawn from that cluster; against the C oracle and the wave kernel."""
+    from lac_amd.batch import BatchCoder
+    rng = np.random.default_rng(prec)
+    V, B, T = 2000, 2, 300
+    pmf = rng.integers(4096, 8192, size=(T, B, V)).astype(np.uint64)
+    big = rng.choice(V, size=(T, B, 8))
+    for t in range(T):
+        for b in range(B):
+            pmf[t, b, big[t, b]] = rng.integers(1 << 56, 1 << 57, size=8).astype(np.uint64)
+    sym = rng.integers(0, V, size=(T, B)).astype(np.int32)
+    pick_big = rng.random((T, B)) < 0.2
+    for t in range(T):
+        for b in range(B):
+            if pick_big[t, b]:
+                sym[t, b] = big[t, b, rng.integers(0, 8)]
+    bits, nbits = _oracle_bits(pmf, sym, prec)
+    c = BatchCoder(V, B, prec=prec, pmf_bits=64, capacity_bits=T * (prec + 2) + 256, device=DEV)
+    dp = _dev(pmf)
+    for path in ("stats", "fused"):
+        c.set_decode_path(path)
+        c.decode_open(bits, nbits)
+        assert np.array_equal(c.decode(dp).cpu().numpy(), sym), path
     c.close()
