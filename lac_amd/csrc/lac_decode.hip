@@ -942,8 +942,8 @@ __device__ inline void lean_touch(const uint8_t *base, int64_t bytes) {
 }
 
 template <typename E>
-__device__ void lean_helper(const E *lcdf, int64_t rstep, int32_t n32, int64_t V, int64_t B, int64_t B8,
-                            const int32_t *progress) {
+__device__ void lean_helper(const E *lcdf, const uint64_t *lchunk, const LeanMeta *lmeta, int64_t rstep, int32_t n32,
+                            int64_t V, int64_t B, int64_t B8, const int32_t *progress) {
     const int64_t hidx = (int64_t)blockIdx.x - B8;
     const int64_t b = hidx % B8, k = hidx / B8;                 // stream (same XCD: B8 % 8 == 0), helper
     if (b >= B || k >= kLeanHelpers) return;
@@ -956,7 +956,11 @@ __device__ void lean_helper(const E *lcdf, int64_t rstep, int32_t n32, int64_t V
             if (++idle > (1 << 17)) return;                      // ~10 ms without progress
             __builtin_amdgcn_s_sleep(2);
         }
-        lean_touch(reinterpret_cast<const uint8_t *>(lcdf + ((int64_t)t * rstep + b) * V), V * (int64_t)sizeof(E));
+        const int64_t r = (int64_t)t * rstep + b;
+        lean_touch(reinterpret_cast<const uint8_t *>(lcdf + r * V), V * (int64_t)sizeof(E));
+        // the row's chunk bounds and LeanMeta, which the decoder loads two steps ahead
+        lean_touch(reinterpret_cast<const uint8_t *>(lchunk + r * 64), 64 * (int64_t)sizeof(uint64_t));
+        lean_touch(reinterpret_cast<const uint8_t *>(lmeta + r), (int64_t)sizeof(LeanMeta));
     }
 }
 
@@ -1013,7 +1017,7 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
     const int lane = (int)lane_id();
     const int64_t B8 = (B + 7) & ~(int64_t)7;
     if ((int64_t)blockIdx.x >= B8) {                             // a helper workgroup
-        if (progress) lean_helper<E>(lcdf, rstep, (int32_t)nsteps, V, B, B8, progress);
+        if (progress) lean_helper<E>(lcdf, lchunk, lmeta, rstep, (int32_t)nsteps, V, B, B8, progress);
         return;
     }
     const int64_t b = blockIdx.x;
@@ -1042,9 +1046,12 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
     // so a row's meta two steps ahead was waited for one step after its load.
     const bool moving = rstep != 0;
     const uint64_t *lmw = reinterpret_cast<const uint64_t *>(lmeta) + (lane & 3);
-    uint64_t cwA = 0, cwB = 0, lmA = 0, lmB = 0;
-    if (n32 > 0) { cwA = lchunk[b * 64 + lane]; lmA = lmw[b * 4]; }
-    if (n32 > 1) { cwB = lchunk[(rstep + b) * 64 + lane]; lmB = lmw[(rstep + b) * 4]; }
+    // (unconditional -- the buffers hold two rows past a launch's last -- and drained here:
+    // loads that differ between the loop's entry paths made the wait at its top a full drain
+    // on every step)
+    uint64_t cwA = lchunk[b * 64 + lane], lmA = lmw[b * 4];
+    uint64_t cwB = lchunk[(rstep + b) * 64 + lane], lmB = lmw[(rstep + b) * 4];
+    __builtin_amdgcn_s_waitcnt(0);
     const uint64_t *lcv = lchunk + (2 * rstep + b) * 64 + lane;
     int64_t li = 2 * rstep + b;
     const Vt *rowp = reinterpret_cast<const Vt *>(lcdf + b * V);
@@ -1107,12 +1114,14 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
         // the stream window: words pos/64 and the next, clamped to the zero words past the end
         const uint64_t wi = (pos >> 6) < mynw ? (pos >> 6) : mynw;
         const uint64_t W0 = mywin[wi], W1 = mywin[wi + 1];
-        if (moving) {                                           // row i+2 (the buffers hold two rows past the
-            pcw = *lcv;                                         // launch's last: read, never used)
-            plm = lmw[li * 4];
-            lcv += rstep * 64;
-            li += rstep;
-        }
+        // row i+2 (the buffers hold two rows past the launch's last: read, never used); a
+        // static model reloads its one row.  Unconditional: under a branch the two paths'
+        // load counts differ, and the wait for this step's chunk vectors then also waited
+        // for these loads (from HBM) on the moving path.
+        pcw = *lcv;
+        plm = lmw[li * 4];
+        lcv += rstep * 64;
+        li += rstep;
         if constexpr (decltype(pub)::value) {
             if (__builtin_expect(progress && (i & (kLeanPub - 1)) == 0, 0) && lane == 0)   // the helpers' pace
                 __hip_atomic_store(progress + b, i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // (after the loads)
