@@ -259,9 +259,9 @@ def test_lean_u64_wide_totals(prec):
 
 
 def test_lean_many_groups_two_streams():
-    """V = 32000 u32 with 2 streams: the 256 MB lean buffers hold 1024 steps' rows, so
-    4000 steps are four launch groups; one stream leaves the lean case (totals >= 2^32)
-    for 100 steps inside the second group and comes back in it."""
+    """V = 32000 u32 with 2 streams: the 512 MB lean buffers hold 2048 steps' rows, so
+    4000 steps are two launch groups; one stream leaves the lean case (totals >= 2^32)
+    for 100 steps inside the first group and comes back in it."""
     from lac_amd.batch import BatchCoder
     rng = np.random.default_rng(21)
     V, B, T, prec = 32000, 2, 4000, 48
