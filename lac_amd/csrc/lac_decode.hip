@@ -657,7 +657,7 @@ struct LeanMeta {
     uint64_t T;            // the total; 0: not for the lean step (bad row, u32 total >= 2^32, minp 0)
     uint64_t fthr;         // ceil(T / minp): the ceil mapping's range is fudged iff w < fthr (arith_code.py:84)
     double iT;             // 1/T correctly rounded
-    uint64_t pad;
+    double Td;             // T rounded to a double (the wide rows' target window)
 };
 // Totals the lean step takes: below 2^32 for u32 tables (their CDF then fits the entries'
 // own width); any valid total (below 2^64) for u64 tables, whose steps divide with
@@ -779,7 +779,7 @@ __global__ __launch_bounds__(256) void k_dec_stats(const E *__restrict__ pmf, in
         // 1/T correctly rounded (an IEEE divide, once per row): the one-estimate bounds of
         // div_mid (u64 rows) and div_near (u32 rows) need it
         if (lane == 0)
-            lmeta[r] = LeanMeta{ok ? T : 0, ok ? (T + minp - 1) / minp : 0, 1.0 / (double)(ok ? T : 1), 0};
+            lmeta[r] = LeanMeta{ok ? T : 0, ok ? (T + minp - 1) / minp : 0, 1.0 / (double)(ok ? T : 1), (double)T};
     }
 }
 
@@ -920,6 +920,9 @@ constexpr int kLeanPub = LAC_LEAN_PUB;          // the decoder publishes its pro
 #define LAC_LEAN_BYTES (512ll << 20)   // (256 MB: c2 u64 1.47 us per step, 512 MB 1.44: more stats waves per CU)
 #endif
 constexpr int64_t kLeanBytes = LAC_LEAN_BYTES;  // CDF rows per launch: at most this many bytes
+#ifndef LAC_LEAN_WIDE_WINDOW
+#define LAC_LEAN_WIDE_WINDOW 1                  // wide u64 rows: the search against a double window
+#endif
 
 __device__ inline int32_t lean_progress(const int32_t *p) {
     return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -1079,6 +1082,7 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
         pos = rfl_u64(pos);
         const uint64_t T = readlane_u64(lmv, 0), fthr = readlane_u64(lmv, 1);   // LeanMeta {T, fthr, iT}
         const double iT = __builtin_bit_cast(double, readlane_u64(lmv, 2));
+        const double Td = __builtin_bit_cast(double, readlane_u64(lmv, 3));
         const Vt *row = rowp;
         rowp += rv_step;
         const uint64_t w = (uint64_t)(h - l + 1), v = (uint64_t)(x - l);
@@ -1150,8 +1154,20 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
         // (u64 rows of 2^50 and more: the search compares by products -- their target by
         // div_floor_inv's two estimates and 128-bit remainders in the loads' shadow measured
         // slower, 1.775 vs 1.70 us per c2 step, profiles/r06/lean/, and a search against a
-        // double window around the target no faster, profiles/r06/lean2/wideapprox/)
+        // double window around the target: 1.418 vs 1.442 us, profiles/r06/lean3/widewindow/)
         const E te = (!W || small) ? (E)div_near_u(vs, Ts, 0, ws, iw) : (E)0;
+        // u64 rows of 2^50 and more: a window [tlo, thi] around v*T/w from doubles that holds
+        // the target -- v exact, T and 1/w within an ulp or two, so the estimate is within 2^14
+        // of v*T/w < 2^64 -- with 2^15 of margin either side.  The search compares entries with
+        // tlo; it equals the exact search unless a compared entry lies in (tlo, thi], which one
+        // ballot tests (then the search reruns with products).
+        uint64_t tlo = 0, thi = 0;
+        if constexpr (W) {
+            const double ted = small_to_f64(vs) * Td * recip2_small(ws);
+            const double lo_d = ted - 32768.0, hi_d = ted + 32768.0;
+            tlo = rfl_u64(lo_d > 0.0 ? (uint64_t)lo_d : 0);
+            thi = rfl_u64(hi_d < 18446744073709551616.0 ? (uint64_t)hi_d : ~0ull);
+        }
         clk.mark(1);
         clk.mark(2);
         int gs = 0;
@@ -1159,6 +1175,7 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
         uint64_t m2, lo_l, hi_c, prev;
         uint32_t kL;
         int L;
+        Vt xgo;                                                 // the iteration's vectors the search took
         auto search = [&](auto lte) {                           // lte(c): c <= tgt
             // the iteration holding the target: the last whose CDF value just before it (the
             // chunk's bound, else lane 63's last entry of the iteration before) is <= tgt.
@@ -1174,6 +1191,7 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
                 exg = take ? eg : exg;
                 xg = take ? xs[g] : xg;
             }
+            xgo = xg;
             const bool real = cv0 + gs * 64 + lane < nv32;
             m2 = __ballot(real & !lte(vget<E, VEC>(xg, VEC - 1)));
             L = m2 ? __ffsll((unsigned long long)m2) - 1 : 0;
@@ -1202,7 +1220,23 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
             kL = (uint32_t)__builtin_amdgcn_readlane((int)k, L);
         };
         if (!W || small) search([&](E c) { return c <= te; });
-        else search([&](E c) { return le((uint64_t)c); });
+        else if (!LAC_LEAN_WIDE_WINDOW) search([&](E c) { return le((uint64_t)c); });
+        else {
+            search([&](E c) { return (uint64_t)c <= tlo; });
+            auto inw = [&](uint64_t c) { return (c > tlo) & (c <= thi); };
+            bool amb = false;
+#pragma unroll
+            for (int g = 1; g < CIM; g++)
+                amb |= inw(readlane_u64((uint64_t)vget<E, VEC>(xs[g - 1], VEC - 1), 63));
+            bool la = false;
+#pragma unroll
+            for (int j = 0; j < VEC; j++) la |= inw((uint64_t)vget<E, VEC>(xgo, j));
+            if (__builtin_expect(amb | (__ballot(la) != 0), 0)) {
+                gs = 0;
+                exg = (E)ex0;
+                search([&](E c) { return le((uint64_t)c); });
+            }
+        }
         const uint64_t lo_c = kL ? lo_l : (L > 0 ? prev : (uint64_t)exg);
         const int32_t sym = (cv0 + gs * 64 + L) * VEC + (int32_t)kL;
         clk.mark(3);
