@@ -1151,10 +1151,10 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
         // (div_near: the estimate is within one of the quotient, two sign tests; for u64 rows,
         // whose target reaches 2^50, with 1/w to ~1 ulp)
         const double iw = W ? recip2_small(ws) : recip_small(ws);   // (w <= 2^50: exact as a double)
-        // (u64 rows of 2^50 and more: the search compares by products -- their target by
-        // div_floor_inv's two estimates and 128-bit remainders in the loads' shadow measured
-        // slower, 1.775 vs 1.70 us per c2 step, profiles/r06/lean/, and a search against a
-        // double window around the target: 1.418 vs 1.442 us, profiles/r06/lean3/widewindow/)
+        // (u64 rows of 2^50 and more: no exact target -- by div_floor_inv's two estimates and
+        // 128-bit remainders in the loads' shadow it measured slower, 1.775 vs 1.70 us per c2
+        // step, profiles/r06/lean/ -- but the window below: 1.418 vs 1.442 us with products
+        // alone, profiles/r06/lean3/widewindow/)
         const E te = (!W || small) ? (E)div_near_u(vs, Ts, 0, ws, iw) : (E)0;
         // u64 rows of 2^50 and more: a window [tlo, thi] around v*T/w from doubles that holds
         // the target -- v exact, T and 1/w within an ulp or two, so the estimate is within 2^14
