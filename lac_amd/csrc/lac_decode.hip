@@ -1042,12 +1042,11 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
     // (by index, a scalar load) in two register sets A / B that the 2x unrolled loop uses in
     // turn, so a prefetched value is first touched two steps after its load was issued (a
     // single set rotated by copies waited at the next step for a load issued one step
-    // earlier); a static model (rstep 0) loads its one row's once.  A running pointer to row
+    // earlier); a static model (rstep 0) reloads its one row's.  A running pointer to row
     // i's CDF.
     // The LeanMeta arrives by a vector load (lane k: word k & 3), read out with readlanes:
     // a scalar load's wait (lgkmcnt, out of order) waits for every scalar load in flight,
     // so a row's meta two steps ahead was waited for one step after its load.
-    const bool moving = rstep != 0;
     const uint64_t *lmw = reinterpret_cast<const uint64_t *>(lmeta) + (lane & 3);
     // (unconditional -- the buffers hold two rows past a launch's last -- and drained here:
     // loads that differ between the loop's entry paths made the wait at its top a full drain
@@ -1261,7 +1260,7 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
             }
         }
         // narrow + renormalise (decode_advance<true>) without branches: kk = 0 keeps the
-        // registers, and window_bits_nb(.., 0) is 0
+        // registers and reads no window bits
         int64_t nl = l + (int64_t)a, nh = l + (int64_t)bb - 1;
         const uint64_t d = (uint64_t)(nh - nl);
         const int sh = bitlen64(d), kk0 = prec - sh, kk = kk0 > 0 ? kk0 : 0;   // (renorm: kk <= 0 is 0)
