@@ -907,8 +907,12 @@ __global__ __launch_bounds__(256) void k_decode_seq(const E *__restrict__ pmf, i
 #endif
 constexpr int kLeanAhead = LAC_LEAN_AHEAD;      // rows prefetched ahead of the decoder
 constexpr int kLeanHelpers = LAC_LEAN_HELPERS;  // helper waves per stream
+// Up to 44 streams: the stats pass of the lean step writes a full CDF copy of every row, so
+// its per-step cost grows with the streams, and k_decode_seq's read-only pass overtakes it
+// between 32 and 64 (V=32000 u32, decode us per step lean / seq: 8 streams 1.17 / 2.75,
+// 16 1.76 / 2.90, 32 2.75 / 3.25, 64 4.52 / 3.91; profiles/r06/lean3/fewstreams/)
 #ifndef LAC_LEAN_MAX_STREAMS
-#define LAC_LEAN_MAX_STREAMS 64
+#define LAC_LEAN_MAX_STREAMS 44
 #endif
 constexpr int64_t kLeanMaxStreams = LAC_LEAN_MAX_STREAMS;   // k_decode_lean up to this many streams
 constexpr int kLeanHelpMaxStreams = 16;         // above: no helpers (L2: ~2.6 MB ahead per stream)
