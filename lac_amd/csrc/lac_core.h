@@ -229,6 +229,15 @@ __host__ __device__ inline uint64_t div_mid_est(uint64_t n, uint64_t m, uint64_t
     const double e = __builtin_fma((double)n, (double)m, (double)add) * inv;
     return (uint64_t)(e > 0.0 ? e : 0.0);
 }
+// div_mid_est for the lean step's wide ranges, in fewer conversions: m below 2^52 through the
+// 2^52 magic, the addend given as a double (the ceil mapping's T - 1 as T rounded to a double,
+// which moves the quotient by under 2^-38 for T >= 2^50), and the estimate rounded to the
+// nearest integer by the magic (quotients <= 2^50).  Within one of the quotient, as
+// div_mid_fix takes it (host-checked, tests/test_core_host.py).
+__host__ __device__ inline uint64_t div_mid_est_w(uint64_t n, uint64_t m, double addd, double inv) {
+    const double e = __builtin_fma((double)n, small_to_f64(m), addd) * inv;
+    return f64_to_small(e > 0.0 ? e : 0.0);
+}
 __host__ __device__ inline uint64_t div_mid_fix(uint64_t q, uint64_t n, uint64_t m, uint64_t add, uint64_t d) {
     const u128 r = (u128)n * m + add - (u128)q * d;          // wrapping: [-d, 2d) as two's complement
     const uint64_t rh = (uint64_t)(r >> 64), rl = (uint64_t)r;

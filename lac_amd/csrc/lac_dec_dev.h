@@ -409,6 +409,13 @@ __device__ inline void div_mid_u2(uint64_t n0, uint64_t n1, uint64_t m, uint64_t
     *q0 = div_mid_fix(e0, n0, m, add, d);
     *q1 = div_mid_fix(e1, n1, m, add, d);
 }
+// the same with div_mid_est_w's estimates (m < 2^52, the addend also as the double addd)
+__device__ inline void div_mid_u2w(uint64_t n0, uint64_t n1, uint64_t m, uint64_t add, double addd, uint64_t d,
+                                   double inv, uint64_t *q0, uint64_t *q1) {
+    const uint64_t e0 = rfl_u64(div_mid_est_w(n0, m, addd, inv)), e1 = rfl_u64(div_mid_est_w(n1, m, addd, inv));
+    *q0 = div_mid_fix(e0, n0, m, add, d);
+    *q1 = div_mid_fix(e1, n1, m, add, d);
+}
 
 // Everything after the row's totals are known: val_to_symbol + symbol_to_range
 // + advance.  `find_chunk(tgt, &cv0, &G, &cb)` locates the chunk holding tgt.

@@ -71,6 +71,12 @@ uint64_t cc_div_mid(uint64_t n, uint64_t m, uint64_t add, uint64_t d) {
     return div_mid_fix(div_mid_est(n, m, add, inv), n, m, add, d);
 }
 
+// div_mid_est_w (the lean step's wide ranges): the addend passed as a double
+uint64_t cc_div_mid_w(uint64_t n, uint64_t m, uint64_t add, double addd, uint64_t d) {
+    const double inv = 1.0 / (double)d;
+    return div_mid_fix(div_mid_est_w(n, m, addd, inv), n, m, add, d);
+}
+
 // div_near (the lean decode step's u32 rows): estimate with 1/d moved `ulps` ULPs off the
 // correctly rounded value (the target's device reciprocal), two sign tests; n32: n < 2^32
 uint64_t cc_div_near(uint64_t n, uint64_t m, uint64_t add, uint64_t d, int ulps, int n32) {

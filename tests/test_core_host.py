@@ -187,6 +187,36 @@ def test_div_mid_exact(core):
         assert core.cc_div_mid(c, w, 0, T) == c * w // T, (c, w, T)
 
 
+def test_div_mid_w_exact(core):
+    """div_mid_est_w (the lean step's wide ranges: m through the 2^52 magic, the estimate
+    rounded by it, the ceil mapping's addend T - 1 passed as T rounded to a double): exact
+    floor((n*m + add)/d) for quotients up to 2^50 -- random addends passed exactly, and the
+    decoder's shapes ceil(c*w/T) with T >= 2^50, c <= T, w <= 2^50."""
+    import random
+    core.cc_div_mid_w.restype = C.c_uint64
+    core.cc_div_mid_w.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_double, C.c_uint64]
+    rng = random.Random(13)
+    n_cases = 0
+    while n_cases < 40000:
+        d = rng.randint(1, (1 << rng.randint(1, 64)) - 1)
+        m = rng.randint(0, 1 << rng.randint(0, 51))
+        n = rng.randint(0, (1 << rng.randint(0, 64)) - 1)
+        add = rng.choice([0, d - 1, rng.randint(0, d - 1)])
+        q = (n * m + add) // d
+        if q > 1 << 50:
+            continue
+        assert core.cc_div_mid_w(n, m, add, float(add), d) == q, (n, m, add, d)
+        n_cases += 1
+    for _ in range(40000):
+        prec = rng.randint(2, 50)
+        w = rng.randint((1 << (prec - 1)) + 1, 1 << prec)
+        T = rng.choice([rng.randint(1 << 50, (1 << 64) - 1), (1 << 64) - 1, (1 << 63) + rng.randint(0, 99),
+                        (1 << 50) + rng.randint(0, 99)])
+        c = rng.choice([rng.randint(0, T), T, T - 1, 0, 1])
+        assert core.cc_div_mid_w(c, w, T - 1, float(T), T) == -(-(c * w) // T), (c, w, T)
+        assert core.cc_div_mid_w(c, w, 0, 0.0, T) == c * w // T, (c, w, T)
+
+
 def test_div_near_exact(core):
     """div_near (the lean decode step's rows below 2^50, two sign tests): u32 rows' targets
     floor(v*T/w), T < 2^32, with the reciprocal of w up to 16 ulps off (the device's
