@@ -1160,16 +1160,17 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
         // alone, profiles/r06/lean3/widewindow/)
         const E te = (!W || small) ? (E)div_near_u(vs, Ts, 0, ws, iw) : (E)0;
         // u64 rows of 2^50 and more: a window [tlo, thi] around v*T/w from doubles that holds
-        // the target -- v exact, T and 1/w within an ulp or two, so the estimate is within 2^14
-        // of v*T/w < 2^64 -- with 2^15 of margin either side.  The search compares entries with
-        // tlo; it equals the exact search unless a compared entry lies in (tlo, thi], which one
-        // ballot tests (then the search reruns with products).
+        // the target -- v exact, T within an ulp, 1/w to ~2^-50 (one Newton step), so the
+        // estimate is within 2^15 of v*T/w < 2^64 -- with 2^16 of margin either side.  The
+        // search compares entries with tlo; it equals the exact search unless a compared entry
+        // lies in (tlo, thi], which one ballot tests (then the search reruns with products).
         uint64_t tlo = 0, thi = 0;
         if constexpr (W) {
-            const double ted = small_to_f64(vs) * Td * recip2_small(ws);
-            const double lo_d = ted - 32768.0, hi_d = ted + 32768.0;
-            tlo = rfl_u64(lo_d > 0.0 ? (uint64_t)lo_d : 0);
-            thi = rfl_u64(hi_d < 18446744073709551616.0 ? (uint64_t)hi_d : ~0ull);
+            if (!small) {
+                const double lo_d = small_to_f64(vs) * Td * recip_small(ws) - 65536.0;
+                tlo = rfl_u64(lo_d > 0.0 ? (uint64_t)lo_d : 0);
+                thi = tlo > ~0ull - 131072 ? ~0ull : tlo + 131072;
+            }
         }
         clk.mark(1);
         clk.mark(2);
