@@ -652,6 +652,19 @@ __device__ inline void dec_chunk_layout(int64_t V, int64_t *CI, int64_t *nch) {
     *nch = (nit + ci - 1) / ci;
 }
 
+// The lean step's chunks: up to 64 * LeanCW<E> of them, LeanCW bounds per lane -- u64 rows
+// two (V = 32000: 125 chunks of 2 iterations, two 16-B loads per lane and step instead of
+// four), u32 rows one (the layout above).
+template <typename E> constexpr int LeanCW = sizeof(E) == 8 ? 2 : 1;
+typedef VecT<uint64_t, 2>::type u64x2;
+template <typename E, int VEC>
+__host__ __device__ inline void lean_chunk_layout(int64_t V, int64_t *CI, int64_t *nch) {
+    const int64_t nvec = V / VEC, nit = (nvec + 63) / 64, per = 64 * LeanCW<E>;
+    const int64_t ci = nit ? (nit + per - 1) / per : 1;
+    *CI = ci;
+    *nch = (nit + ci - 1) / ci;
+}
+
 // What k_decode_lean reads of a row (LEAN builds of k_dec_stats), besides its CDF:
 struct LeanMeta {
     uint64_t T;            // the total; 0: not for the lean step (bad row, u32 total >= 2^32, minp 0)
@@ -690,8 +703,13 @@ __global__ __launch_bounds__(256) void k_dec_stats(const E *__restrict__ pmf, in
     E mn = (E)~(E)0;
     uint32_t ovf = 0;
     // groups of 8 iterations (8 loads in flight per lane), their 8 totals from one
-    // butterfly, each added into the lane of its chunk (chunk = iteration / CI)
+    // butterfly, each added into the lane of its chunk (chunk = iteration / CI); LEAN u64
+    // rows also into the lane of their lean chunk (lean_chunk_layout), chunks 64.. in lmB
     int64_t chunk = 0, left = CI;
+    int64_t LCI = CI, lnch = nch;
+    if constexpr (LEAN && LeanCW<E> == 2) lean_chunk_layout<E, VEC>(V, &LCI, &lnch);
+    int64_t lch = 0, lleft = LCI;
+    uint64_t lmA = 0, lmB = 0;
     E run = 0;                                                 // LEAN: the row's sum so far
     Vt *cp = LEAN ? reinterpret_cast<Vt *>(lcdf + r * V) : nullptr;
     // LEAN: a group's CDF vectors are stored after the next group's loads are issued, so
@@ -756,6 +774,13 @@ __global__ __launch_bounds__(256) void k_dec_stats(const E *__restrict__ pmf, in
             const uint64_t v = readlane_u64(tot, u);
             if (lane == chunk) mine = add_ovf<W>(mine, v, ovf);
             if (--left == 0) { chunk++; left = CI; }
+            if constexpr (LEAN && LeanCW<E> == 2) {
+                if (lane == (lch & 63)) {
+                    if (lch < 64) lmA += v;
+                    else lmB += v;
+                }
+                if (--lleft == 0) { lch++; lleft = LCI; }
+            }
         }
     }
     if constexpr (LEAN) {
@@ -775,7 +800,15 @@ __global__ __launch_bounds__(256) void k_dec_stats(const E *__restrict__ pmf, in
         // chunk lane's exclusive bound; a row not for the lean step gets bounds no target
         // passes (c*w <= v*T fails for c = 2^64 - 1 and for its low word), so the step finds
         // no chunk and leaves without testing T
-        lchunk[r * 64 + lane] = ok ? in - mine : ~0ull;
+        if constexpr (LeanCW<E> == 2) {
+            const uint64_t ia = wave_incl_scan_u64(lmA), ib = wave_incl_scan_u64(lmB) + readlane_u64(ia, 63);
+            u64x2 bnd;
+            bnd.x = ok ? ia - lmA : ~0ull;
+            bnd.y = ok ? ib - lmB : ~0ull;
+            reinterpret_cast<u64x2 *>(lchunk)[r * 64 + lane] = bnd;
+        } else {
+            lchunk[r * 64 + lane] = ok ? in - mine : ~0ull;
+        }
         // 1/T correctly rounded (an IEEE divide, once per row): the one-estimate bounds of
         // div_mid (u64 rows) and div_near (u32 rows) need it
         if (lane == 0)
@@ -966,7 +999,7 @@ __device__ void lean_helper(const E *lcdf, const uint64_t *lchunk, const LeanMet
         const int64_t r = (int64_t)t * rstep + b;
         lean_touch(reinterpret_cast<const uint8_t *>(lcdf + r * V), V * (int64_t)sizeof(E));
         // the row's chunk bounds and LeanMeta, which the decoder loads two steps ahead
-        lean_touch(reinterpret_cast<const uint8_t *>(lchunk + r * 64), 64 * (int64_t)sizeof(uint64_t));
+        lean_touch(reinterpret_cast<const uint8_t *>(lchunk + r * 64 * LeanCW<E>), 64 * LeanCW<E> * (int64_t)sizeof(uint64_t));
         lean_touch(reinterpret_cast<const uint8_t *>(lmeta + r), (int64_t)sizeof(LeanMeta));
     }
 }
@@ -1036,8 +1069,8 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
     const uint64_t nwc = (uint64_t)wstride - 2;                 // words past the stream's own: zero
     const uint64_t mynw = (mynbits + 63) >> 6 < nwc ? (mynbits + 63) >> 6 : nwc;
     int64_t CI, nch;
-    dec_chunk_layout<E, VEC>(V, &CI, &nch);
-    const int32_t nv32 = (int32_t)(V / VEC);                    // (<= 16384: CI <= 4)
+    lean_chunk_layout<E, VEC>(V, &CI, &nch);
+    const int32_t nv32 = (int32_t)(V / VEC);                    // (<= 32768: CI <= 4)
     const uint32_t ci64 = (uint32_t)CI * 64;
     const int32_t nch32 = (int32_t)nch;
     const bool ceil_map = mapping != LAC_MAP_FLOOR;
@@ -1055,10 +1088,13 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
     // (unconditional -- the buffers hold two rows past a launch's last -- and drained here:
     // loads that differ between the loop's entry paths made the wait at its top a full drain
     // on every step)
-    uint64_t cwA = lchunk[b * 64 + lane], lmA = lmw[b * 4];
-    uint64_t cwB = lchunk[(rstep + b) * 64 + lane], lmB = lmw[(rstep + b) * 4];
+    // (u64 rows: the lane's two chunk bounds, chunks lane and 64 + lane, as one 16-B vector)
+    typedef typename std::conditional<W, u64x2, uint64_t>::type CWt;
+    const CWt *lcw = reinterpret_cast<const CWt *>(lchunk);
+    CWt cwA = lcw[b * 64 + lane], cwB = lcw[(rstep + b) * 64 + lane];
+    uint64_t lmA = lmw[b * 4], lmB = lmw[(rstep + b) * 4];
     __builtin_amdgcn_s_waitcnt(0);
-    const uint64_t *lcv = lchunk + (2 * rstep + b) * 64 + lane;
+    const CWt *lcv = lcw + (2 * rstep + b) * 64 + lane;
     int64_t li = 2 * rstep + b;
     const Vt *rowp = reinterpret_cast<const Vt *>(lcdf + b * V);
     const int64_t rv_step = rstep * (int64_t)nv32;               // vectors per step
@@ -1078,7 +1114,7 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
     // one step with row data (cwi, lm); the next-but-one row's loads go into (pcw, plm) once
     // this step's chunk loads are issued.  false: the stream leaves (not this step's case)
     // PUB: the first step of a pair, whose i is even, publishes the decoder's progress
-    auto step = [&](const uint64_t cwi, const uint64_t lmv, uint64_t &pcw, uint64_t &plm, auto pub) -> bool {
+    auto step = [&](const CWt cwi, const uint64_t lmv, CWt &pcw, uint64_t &plm, auto pub) -> bool {
         l = (int64_t)rfl_u64((uint64_t)l);                      // (the loop's phis are not seen as uniform)
         h = (int64_t)rfl_u64((uint64_t)h);
         x = (int64_t)rfl_u64((uint64_t)x);
@@ -1106,11 +1142,20 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
         const uint32_t wl = (uint32_t)w;
         const uint64_t wh = w >> 32;
         auto le = [&](uint64_t e) { return lean_le<E>(e, wl, wh, w, ph, pl); };   // e <= tgt
-        const uint64_t cm = __ballot((lane < nch32) & le(cwi));
+        uint64_t cm;
+        uint32_t src;
         // the chunk's loads first (in bounds whatever the step: refused below if it is bad),
         // then the stream window, then the next-but-one row's data, then everything that
         // can wait for them
-        const uint32_t src = cm ? (uint32_t)(63 - __builtin_clzll((unsigned long long)cm)) : 0u;
+        if constexpr (W) {
+            cm = __ballot((lane < nch32) & le(cwi.x));
+            const uint64_t cm1 = __ballot((lane + 64 < nch32) & le(cwi.y));
+            src = cm1 ? 127u - (uint32_t)__builtin_clzll((unsigned long long)cm1)
+                      : cm ? (uint32_t)(63 - __builtin_clzll((unsigned long long)cm)) : 0u;
+        } else {
+            cm = __ballot((lane < nch32) & le(cwi));
+            src = cm ? (uint32_t)(63 - __builtin_clzll((unsigned long long)cm)) : 0u;
+        }
         const int32_t cv0 = (int32_t)(src * ci64);
         Vt xs[CIM];
 #pragma unroll
@@ -1145,7 +1190,9 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
         // (a bad step computes on whatever values it has -- no load or store depends on them
         // -- and leaves at the exit test below)
         const uint64_t Ts = T, ws = w, vs = v;
-        const uint64_t ex0 = W ? readlane_u64(cwi, (int)src) : (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cwi, (int)src);
+        uint64_t ex0;
+        if constexpr (W) ex0 = readlane_u64(src >= 64 ? cwi.y : cwi.x, (int)(src & 63));
+        else ex0 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cwi, (int)src);
         // the target: u32 rows and u64 rows below 2^50 divide (div_small, in the loads'
         // shadow) and compare entries with it; u64 rows of 2^50 and more (llama-scale
         // tables), whose target would divide in 128 bits past the loads' return, compare
@@ -1390,11 +1437,12 @@ static int decode_stats_path(lac_ctx *c, const E *pmf, int64_t step_stride, int6
     // number of steps.
     const bool stat = step_stride == 0;
     const int64_t rstep = stat ? 0 : c->B;
-    // k_decode_lean: prec <= 50, chunks of at most 4 iterations (V <= 65536 u32 / 32768 u64
-    // entries), totals lean_total_ok<E> (checked per row); its CDF buffer holds up to
-    // kLeanBytes, so a launch takes at most that many steps' rows
-    const int64_t nvec = c->V / VEC, nit = (nvec + 63) / 64;
-    const int64_t CI = nit ? (nit + 63) / 64 : 1;
+    // k_decode_lean: prec <= 50, chunks of at most 4 iterations (V <= 65536 entries: 64 chunk
+    // bounds per u32 row, 128 per u64 row), totals lean_total_ok<E> (checked per row); its
+    // CDF buffer holds up to kLeanBytes, so a launch takes at most that many steps' rows
+    const int64_t nvec = c->V / VEC;
+    int64_t CI, lnch;
+    lean_chunk_layout<E, VEC>(c->V, &CI, &lnch);
     // Only for the fewest streams: the stats pass writes as many bytes more as it reads (the
     // CDF), which costs more than the shorter chain saves once enough streams run side by
     // side (round 4, per-vector CDF, V=32000: B=4 1.36 vs 2.66 us/step, 64 3.41 vs 3.96, 128
@@ -1421,7 +1469,7 @@ static int decode_stats_path(lac_ctx *c, const E *pmf, int64_t step_stride, int6
             c->lean_rows = 0;
             HIPCHK(hipMalloc(&c->lcdf, sizeof(E) * need * c->V));
             // (two rows more: the step's prefetch of row i+2 reads past the launch's last row)
-            HIPCHK(hipMalloc(&c->lchunk, sizeof(uint64_t) * 64 * (need + 2 * c->B)));
+            HIPCHK(hipMalloc(&c->lchunk, sizeof(uint64_t) * 64 * LeanCW<E> * (need + 2 * c->B)));
             HIPCHK(hipMalloc(&c->lmeta, sizeof(LeanMeta) * (need + 2 * c->B)));
             c->lean_rows = need;
             c->lean_esize = (int)sizeof(E);

@@ -308,3 +308,25 @@ def test_lean_u64_wide_clustered_entries(prec):
         c.decode_open(bits, nbits)
         assert np.array_equal(c.decode(dp).cpu().numpy(), sym), path
     c.close()
+
+
+@pytest.mark.parametrize("V", [20000, 65536])
+def test_lean_u64_two_chunk_bounds_per_lane(V):
+    """u64 rows carry up to 128 chunk bounds, two per lane (lean_chunk_layout): V = 20000
+    puts chunks 64.. in the lanes' second bound, V = 65536 (four iterations per chunk) is
+    the widest u64 row the lean step takes.  Llama-scale tables against the C oracle's
+    bitstreams and the wave kernel."""
+    from lac_amd import synth
+    from lac_amd.batch import BatchCoder
+    B, T, prec = 2, 200, 48
+    pmf_d, sym_d = synth.softmax_tables(T, B, V, seed=V, device=DEV, scale_bits=60, storage_bits=64)
+    pmf = pmf_d.cpu().numpy().view(np.uint64).copy()
+    sym = sym_d.cpu().numpy()
+    bits, nbits = _oracle_bits(pmf, sym, prec)
+    c = BatchCoder(V, B, prec=prec, pmf_bits=64, capacity_bits=T * (prec + 2) + 256, device=DEV)
+    dp = _dev(pmf)
+    for path in ("stats", "fused"):
+        c.set_decode_path(path)
+        c.decode_open(bits, nbits)
+        assert np.array_equal(c.decode(dp).cpu().numpy(), sym), path
+    c.close()
