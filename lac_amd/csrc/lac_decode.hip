@@ -655,7 +655,10 @@ __device__ inline void dec_chunk_layout(int64_t V, int64_t *CI, int64_t *nch) {
 // The lean step's chunks: up to 64 * LeanCW<E> of them, LeanCW bounds per lane -- u64 rows
 // two (V = 32000: 125 chunks of 2 iterations, two 16-B loads per lane and step instead of
 // four), u32 rows one (the layout above).
-template <typename E> constexpr int LeanCW = sizeof(E) == 8 ? 2 : 1;
+#ifndef LAC_LEAN_CW32
+#define LAC_LEAN_CW32 1          // (2 for u32 rows too: c2 0.849-0.851 vs 0.848-0.850 us, profiles/r06/lean3/cw32/)
+#endif
+template <typename E> constexpr int LeanCW = sizeof(E) == 8 ? 2 : LAC_LEAN_CW32;
 typedef VecT<uint64_t, 2>::type u64x2;
 template <typename E, int VEC>
 __host__ __device__ inline void lean_chunk_layout(int64_t V, int64_t *CI, int64_t *nch) {
@@ -1089,7 +1092,7 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
     // loads that differ between the loop's entry paths made the wait at its top a full drain
     // on every step)
     // (u64 rows: the lane's two chunk bounds, chunks lane and 64 + lane, as one 16-B vector)
-    typedef typename std::conditional<W, u64x2, uint64_t>::type CWt;
+    typedef typename std::conditional<LeanCW<E> == 2, u64x2, uint64_t>::type CWt;
     const CWt *lcw = reinterpret_cast<const CWt *>(lchunk);
     CWt cwA = lcw[b * 64 + lane], cwB = lcw[(rstep + b) * 64 + lane];
     uint64_t lmA = lmw[b * 4], lmB = lmw[(rstep + b) * 4];
@@ -1147,7 +1150,7 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
         // the chunk's loads first (in bounds whatever the step: refused below if it is bad),
         // then the stream window, then the next-but-one row's data, then everything that
         // can wait for them
-        if constexpr (W) {
+        if constexpr (LeanCW<E> == 2) {
             cm = __ballot((lane < nch32) & le(cwi.x));
             const uint64_t cm1 = __ballot((lane + 64 < nch32) & le(cwi.y));
             src = cm1 ? 127u - (uint32_t)__builtin_clzll((unsigned long long)cm1)
@@ -1191,7 +1194,7 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
         // -- and leaves at the exit test below)
         const uint64_t Ts = T, ws = w, vs = v;
         uint64_t ex0;
-        if constexpr (W) ex0 = readlane_u64(src >= 64 ? cwi.y : cwi.x, (int)(src & 63));
+        if constexpr (LeanCW<E> == 2) ex0 = readlane_u64(src >= 64 ? cwi.y : cwi.x, (int)(src & 63));
         else ex0 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cwi, (int)src);
         // the target: u32 rows and u64 rows below 2^50 divide (div_small, in the loads'
         // shadow) and compare entries with it; u64 rows of 2^50 and more (llama-scale
