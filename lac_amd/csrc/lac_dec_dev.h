@@ -382,15 +382,11 @@ __device__ inline void div_near_u2(uint64_t n0, uint64_t n1, uint64_t m, uint64_
     *q0 = div_near_fix<N32>(e0, n0, m, add, d);
     *q1 = div_near_fix<N32>(e1, n1, m, add, d);
 }
-// 1/d to ~1 ulp: the device reciprocal with two Newton steps (recip() takes one), for
-// estimates whose quotient reaches 2^50 and must stay within one (div_near on u64 rows)
-__device__ inline double recip2(uint64_t d) {
-    const double dd = (double)d, r = recip(d);
-    return __builtin_fma(r, __builtin_fma(-dd, r, 1.0), r);
-}
 
-// recip / recip2 of a d below 2^52, converted by the 2^52 magic (small_to_f64) instead of a
-// general u64 -> f64 conversion: the lean step's 1/w (w <= 2^50), the same values
+// 1/d for a d below 2^52, converted by the 2^52 magic (small_to_f64) instead of a general
+// u64 -> f64 conversion (the lean step's 1/w, w <= 2^50): recip's one Newton step, and
+// recip2_small's two -- 1/d to ~1 ulp, for estimates whose quotient reaches 2^50 and must
+// stay within one (div_near on u64 rows)
 __device__ inline double recip_small(uint64_t d) {
     const double dd = small_to_f64(d);
     const double r = __builtin_amdgcn_rcp(dd);
@@ -401,17 +397,11 @@ __device__ inline double recip2_small(uint64_t d) {
     return __builtin_fma(r, __builtin_fma(-dd, r, 1.0), r);
 }
 
-// div_mid (lac_core.h) with wave-uniform arguments, both of a pair's estimates first so
-// their FP64 chains overlap: the lean step's ranges on u64 rows with totals >= 2^50.
-__device__ inline void div_mid_u2(uint64_t n0, uint64_t n1, uint64_t m, uint64_t add, uint64_t d, double inv,
-                                  uint64_t *q0, uint64_t *q1) {
-    const uint64_t e0 = rfl_u64(div_mid_est(n0, m, add, inv)), e1 = rfl_u64(div_mid_est(n1, m, add, inv));
-    *q0 = div_mid_fix(e0, n0, m, add, d);
-    *q1 = div_mid_fix(e1, n1, m, add, d);
-}
-// the same with div_mid_est_w's estimates (m < 2^52, the addend also as the double addd)
-__device__ inline void div_mid_u2w(uint64_t n0, uint64_t n1, uint64_t m, uint64_t add, double addd, uint64_t d,
-                                   double inv, uint64_t *q0, uint64_t *q1) {
+// div_mid (lac_core.h) with wave-uniform arguments and div_mid_est_w's estimates (m < 2^52,
+// the addend also as the double addd), both of a pair's estimates first so their FP64
+// chains overlap: the lean step's ranges on u64 rows with totals >= 2^50.
+__device__ inline void div_mid_u2(uint64_t n0, uint64_t n1, uint64_t m, uint64_t add, double addd, uint64_t d,
+                                  double inv, uint64_t *q0, uint64_t *q1) {
     const uint64_t e0 = rfl_u64(div_mid_est_w(n0, m, addd, inv)), e1 = rfl_u64(div_mid_est_w(n1, m, addd, inv));
     *q0 = div_mid_fix(e0, n0, m, add, d);
     *q1 = div_mid_fix(e1, n1, m, add, d);

@@ -1297,7 +1297,7 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
         uint64_t a, bb;
         if (!W) div_near_u2<true>(lo_c, hi_c, ws, ceil_map ? Ts - 1 : 0, Ts, iT, &a, &bb);
         else if (small) div_near_u2<false>(lo_c, hi_c, ws, ceil_map ? Ts - 1 : 0, Ts, iT, &a, &bb);
-        else div_mid_u2w(lo_c, hi_c, ws, ceil_map ? Ts - 1 : 0, ceil_map ? Td : 0.0, Ts, iT, &a, &bb);
+        else div_mid_u2(lo_c, hi_c, ws, ceil_map ? Ts - 1 : 0, ceil_map ? Td : 0.0, Ts, iT, &a, &bb);
         // (l + a <= x <= l + bb - 1: v in [a, bb))
         if (bad | (uint64_t)(m2 == 0) | ((vs - a) >> 63) | (((vs - bb) >> 63) ^ 1)) return false;
         clk.mark(4);
