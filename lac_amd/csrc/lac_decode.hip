@@ -828,8 +828,8 @@ __global__ __launch_bounds__(256) void k_decode_seq(const E *__restrict__ pmf, i
                                             const DecRowMeta *__restrict__ meta, DecState *states,
                                             const uint8_t *bits, uint64_t stride, const uint64_t *nbits,
                                             int32_t *sym_out, int64_t B, int mapping,
-                                            const int64_t *__restrict__ resume = nullptr, int64_t rstep = -1,
-                                            int stop_undet = 0) {
+                                            int64_t *__restrict__ resume = nullptr, int64_t rstep = -1,
+                                            int stop_undet = 0, int64_t max_steps = INT64_MAX) {
     const int lane = (int)lane_id();
     // rows of statistics per step: B, or 0 for a static model (stride-0 steps: one row per stream)
     if (rstep < 0) rstep = B;
@@ -847,6 +847,9 @@ __global__ __launch_bounds__(256) void k_decode_seq(const E *__restrict__ pmf, i
     // after k_decode_lean: its steps are done, continue from the first it left
     const int64_t i0 = resume ? (int64_t)rfl_u64((uint64_t)(resume[b] - t0)) : 0;
     if (i0 >= nsteps) return;
+    // max_steps: only that many -- the step a lean launch left at; resume[b] then moves past
+    // them and the next lean launch goes on from there
+    const int64_t iend = max_steps < nsteps - i0 ? i0 + max_steps : nsteps;
     uint64_t next = chunks[(i0 * rstep + b) * 64 + lane];
     DecRowMeta nmeta = meta[i0 * rstep + b];
 #if LAC_DEC_PHASES
@@ -855,12 +858,12 @@ __global__ __launch_bounds__(256) void k_decode_seq(const E *__restrict__ pmf, i
 #else
     NoClock *clk = nullptr;
 #endif
-    for (int64_t i = i0; i < nsteps; i++) {
+    for (int64_t i = i0; i < iend; i++) {
         dec_state_uniform(st);                                 // (the loop's phis are not seen as uniform)
         const int64_t t = t0 + i;
         const uint64_t mine = next;
         const DecRowMeta rm = nmeta;
-        if (i + 1 < nsteps) {                                  // prefetch: independent of the state
+        if (i + 1 < iend) {                                    // prefetch: independent of the state
             next = chunks[((i + 1) * rstep + b) * 64 + lane];
             nmeta = meta[(i + 1) * rstep + b];
         }
@@ -897,6 +900,7 @@ __global__ __launch_bounds__(256) void k_decode_seq(const E *__restrict__ pmf, i
         if (lane == 0) *out = err ? -1 : (int32_t)s;
     }
     if (lane == 0) states[b] = st;
+    if (max_steps != INT64_MAX && lane == 0) resume[b] = t0 + iend;
 #if LAC_DEC_PHASES
     if (lane == 0) {
         for (int k = 0; k < 6; k++) atomicAdd(&g_dec_phase[k], (unsigned long long)clock.acc[k]);
@@ -960,6 +964,10 @@ constexpr int kLeanPub = LAC_LEAN_PUB;          // the decoder publishes its pro
 #define LAC_LEAN_BYTES (512ll << 20)   // (256 MB: c2 u64 1.47 us per step, 512 MB 1.44: more stats waves per CU)
 #endif
 constexpr int64_t kLeanBytes = LAC_LEAN_BYTES;  // CDF rows per launch: at most this many bytes
+#ifndef LAC_LEAN_ROUNDS
+#define LAC_LEAN_ROUNDS 3
+#endif
+constexpr int kLeanRounds = LAC_LEAN_ROUNDS;    // k_decode_seq one step + lean again, per launch group
 #ifndef LAC_LEAN_WIDE_WINDOW
 #define LAC_LEAN_WIDE_WINDOW 1                  // wide u64 rows: the search against a double window
 #endif
@@ -1054,7 +1062,7 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
                                                     const uint64_t *__restrict__ lwin, int64_t wstride,
                                                     const uint64_t *__restrict__ nbits, int32_t *sym_out, int64_t B,
                                                     int mapping, int stop_undet, int64_t *__restrict__ resume,
-                                                    int32_t *progress) {
+                                                    int32_t *progress, int restart) {
     typedef typename VecT<E, VEC>::type Vt;
     constexpr bool W = sizeof(E) == 8;
     const int lane = (int)lane_id();
@@ -1077,7 +1085,10 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
     const uint32_t ci64 = (uint32_t)CI * 64;
     const int32_t nch32 = (int32_t)nch;
     const bool ceil_map = mapping != LAC_MAP_FLOOR;
-    const int32_t n32 = (int32_t)nsteps;                        // (<= the launch's steps)
+    // restart: a later launch over the same group, from the step after the one k_decode_seq
+    // took for the stream (resume[b]); its steps and rows are counted from there
+    const int32_t i0 = restart ? (int32_t)rfl_u64((uint64_t)(resume[b] - t0)) : 0;
+    const int32_t n32 = (int32_t)nsteps - i0;                  // (<= the launch's steps)
     // row data two steps ahead: the lane's chunk bound (per-lane pointer) and the LeanMeta
     // (by index, a scalar load) in two register sets A / B that the 2x unrolled loop uses in
     // turn, so a prefetched value is first touched two steps after its load was issued (a
@@ -1094,14 +1105,15 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
     // (u64 rows: the lane's two chunk bounds, chunks lane and 64 + lane, as one 16-B vector)
     typedef typename std::conditional<LeanCW<E> == 2, u64x2, uint64_t>::type CWt;
     const CWt *lcw = reinterpret_cast<const CWt *>(lchunk);
-    CWt cwA = lcw[b * 64 + lane], cwB = lcw[(rstep + b) * 64 + lane];
-    uint64_t lmA = lmw[b * 4], lmB = lmw[(rstep + b) * 4];
+    const int64_t r0 = (int64_t)i0 * rstep + b;                // this launch's first row
+    CWt cwA = lcw[r0 * 64 + lane], cwB = lcw[(r0 + rstep) * 64 + lane];
+    uint64_t lmA = lmw[r0 * 4], lmB = lmw[(r0 + rstep) * 4];
     __builtin_amdgcn_s_waitcnt(0);
-    const CWt *lcv = lcw + (2 * rstep + b) * 64 + lane;
-    int64_t li = 2 * rstep + b;
-    const Vt *rowp = reinterpret_cast<const Vt *>(lcdf + b * V);
+    const CWt *lcv = lcw + (r0 + 2 * rstep) * 64 + lane;
+    int64_t li = r0 + 2 * rstep;
+    const Vt *rowp = reinterpret_cast<const Vt *>(lcdf + r0 * V);
     const int64_t rv_step = rstep * (int64_t)nv32;               // vectors per step
-    int32_t *outv = sym_out + (t0 + lane) * B + b;              // lane j: step 64k + j
+    int32_t *outv = sym_out + (t0 + i0 + lane) * B + b;         // lane j: step i0 + 64k + j
     // the registers as locals (SGPRs); the counters are settled after the loop
     int64_t l = st.l, h = st.h, x = st.x;
     uint64_t pos = st.pos;
@@ -1367,7 +1379,7 @@ __global__ __launch_bounds__(64) void k_decode_lean(const E *__restrict__ lcdf, 
         st.x = x;
         st.pos = pos;
         states[b] = st;
-        resume[b] = t0 + i;
+        resume[b] = t0 + i0 + i;
     }
 }
 
@@ -1513,18 +1525,33 @@ static int decode_stats_path(lac_ctx *c, const E *pmf, int64_t step_stride, int6
                     CHECK_LAUNCH();
                 }
                 if (help) HIPCHK(hipMemsetAsync(c->dprogress, 0, sizeof(int32_t) * c->B, st));
-#define LAC_LEAN_K(CIM)                                                                                          \
-    k_decode_lean<E, VEC, CIM><<<lean_blocks, 64, 0, st>>>(                                                    \
+#define LAC_LEAN_K(CIM, NB, PROG, RESTART)                                                                      \
+    k_decode_lean<E, VEC, CIM><<<NB, 64, 0, st>>>(                                                             \
         (const E *)c->lcdf, rstep, t0, n, c->V, c->prec, c->lchunk, (const LeanMeta *)c->lmeta, c->dec, c->lwin,   \
-        wstride, c->dnbits, out, c->B, c->mapping, c->dec_stop, c->dresume, help ? c->dprogress : nullptr)
-                switch (CI) {
-                case 1: LAC_LEAN_K(1); break;
-                case 2: LAC_LEAN_K(2); break;
-                case 3: LAC_LEAN_K(3); break;
-                default: LAC_LEAN_K(4); break;
-                }
-#undef LAC_LEAN_K
+        wstride, c->dnbits, out, c->B, c->mapping, c->dec_stop, c->dresume, PROG, RESTART)
+#define LAC_LEAN_SW(NB, PROG, RESTART)                                                                           \
+    switch (CI) {                                                                                                \
+    case 1: LAC_LEAN_K(1, NB, PROG, RESTART); break;                                                             \
+    case 2: LAC_LEAN_K(2, NB, PROG, RESTART); break;                                                             \
+    case 3: LAC_LEAN_K(3, NB, PROG, RESTART); break;                                                             \
+    default: LAC_LEAN_K(4, NB, PROG, RESTART); break;                                                            \
+    }
+                LAC_LEAN_SW(lean_blocks, help ? c->dprogress : nullptr, 0);
                 CHECK_LAUNCH();
+                // a stream that left the lean step (a fudged range, a row outside the lean case)
+                // gets that one step from k_decode_seq and the lean step again from the next,
+                // kLeanRounds times; k_decode_seq then takes what is left.  A stream that did not
+                // leave finds nothing to do in these launches.
+                for (int k = 0; k < kLeanRounds; k++) {
+                    k_decode_seq<E, VEC><<<blocks, 64 * kWavesPerBlock, 0, st>>>(
+                        pmf, step_stride, stream_stride, t0, n, c->V, c->prec, c->q1chunks, (const DecRowMeta *)c->dmeta,
+                        c->dec, c->dbits, c->dstride, c->dnbits, out, c->B, c->mapping, c->dresume, rstep, c->dec_stop, 1);
+                    CHECK_LAUNCH();
+                    LAC_LEAN_SW((unsigned)c->B, nullptr, 1);
+                    CHECK_LAUNCH();
+                }
+#undef LAC_LEAN_SW
+#undef LAC_LEAN_K
             }
         }
         if (!lean && fresh) {

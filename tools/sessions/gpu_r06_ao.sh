@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round 6: the lean step takes the steps it cannot do (fudged ranges, rows outside the lean
-# case) in place, as k_decode_seq would, and stays on the lean step afterwards: lean / drop-in
+# Round 6: a stream that leaves the lean step gets that step from k_decode_seq and the lean
+# step again (three rounds per launch group): lean / drop-in
 # / parity / api / fuzz tests, c2 u32 / u64 lines, one-stream V = 65536 u64 (2.6 us per step
 # before: one row in 2048 can fudge, and the stream then finished its launch group on
 # k_decode_seq), and the drop-in line.
